@@ -1,0 +1,237 @@
+"""ctypes binding of libaiqmc_hip.so (the C-ABI declared in include/aiqmc.h).
+
+The product path has no CPU fallback: if the shared library is missing or a
+call fails, this module raises.  torch is imported before the library is
+loaded so that the process uses ONE HIP runtime (torch's libamdhip64.so.7
+satisfies the library's NEEDED entry by SONAME).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+import torch  # noqa: F401  (must precede loading the HIP library)
+
+AIQMC_F32 = 0
+AIQMC_F64 = 1
+AIQMC_RNG_HOST = 0
+AIQMC_RNG_PHILOX = 1
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaiqmc_hip.so")
+
+EXPORTED_SYMBOLS = (
+    "aiqmc_create", "aiqmc_destroy", "aiqmc_param_count", "aiqmc_set_params",
+    "aiqmc_logpsi", "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_mc_step",
+    "aiqmc_workspace_bytes", "aiqmc_last_error", "aiqmc_supported_shapes",
+)
+
+
+class AiqmcCfg(ctypes.Structure):
+    _fields_ = [
+        ("nelectrons", ctypes.c_int32),
+        ("natoms", ctypes.c_int32),
+        ("nspins", ctypes.c_int32 * 2),
+        ("dtype", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("atoms", ctypes.POINTER(ctypes.c_double)),
+        ("charges", ctypes.POINTER(ctypes.c_double)),
+        ("spin_up_indices", ctypes.POINTER(ctypes.c_int32)),
+        ("spin_down_indices", ctypes.POINTER(ctypes.c_int32)),
+        ("parallel_indices", ctypes.POINTER(ctypes.c_int32)),
+        ("n_parallel", ctypes.c_int32),
+        ("antiparallel_indices", ctypes.POINTER(ctypes.c_int32)),
+        ("n_antiparallel", ctypes.c_int32),
+        ("hidden_dims", (ctypes.c_int32 * 2) * 3),
+        ("hidden_dims_ynlm", ctypes.c_int32 * 3),
+    ]
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load() -> ctypes.CDLL:
+    """Load the HIP library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: build it with `make -C <pkg>/csrc` or __graft_entry__.build(); "
+            "the AIQMC hot path has no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    lib.aiqmc_create.argtypes = [ctypes.POINTER(AiqmcCfg), ctypes.POINTER(vp)]
+    lib.aiqmc_destroy.argtypes = [vp]
+    lib.aiqmc_param_count.argtypes = [vp]
+    lib.aiqmc_param_count.restype = i64
+    lib.aiqmc_workspace_bytes.argtypes = [vp]
+    lib.aiqmc_workspace_bytes.restype = i64
+    lib.aiqmc_set_params.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i64, vp]
+    lib.aiqmc_logpsi.argtypes = [vp, vp, i32, vp, vp, vp]
+    lib.aiqmc_logpsi_grad.argtypes = [vp, vp, i32, vp, vp, vp]
+    lib.aiqmc_local_energy.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+    lib.aiqmc_mc_step.argtypes = [vp, vp, i32, i32, ctypes.c_double, i32, vp, vp, vp,
+                                  ctypes.c_uint64, ctypes.c_uint64, vp, vp]
+    lib.aiqmc_last_error.restype = ctypes.c_char_p
+    lib.aiqmc_supported_shapes.restype = ctypes.c_char_p
+    for name in ("aiqmc_create", "aiqmc_destroy", "aiqmc_set_params", "aiqmc_logpsi",
+                 "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_mc_step"):
+        getattr(lib, name).restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    return load().aiqmc_last_error().decode()
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc}): {last_error()}")
+
+
+def supported_shapes():
+    s = load().aiqmc_supported_shapes().decode()
+    return [tuple(int(v) for v in p.split(":")) for p in s.split(",") if p]
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class Context:
+    """One aiqmc_ctx: a system/network configuration bound to one GPU and dtype."""
+
+    def __init__(self, nelectrons: int, natoms: int, nspins: Sequence[int], atoms, charges,
+                 spin_up_indices, spin_down_indices, parallel_indices, antiparallel_indices,
+                 dtype: torch.dtype = torch.float32, device: int = 0):
+        lib = load()
+        if dtype not in (torch.float32, torch.float64):
+            raise ValueError("dtype must be torch.float32 or torch.float64")
+        self.dtype = dtype
+        self.device = torch.device("cuda", device)
+        self.N = int(nelectrons)
+        self.A = int(natoms)
+        self._keep = []
+
+        def dbl(a):
+            a = np.ascontiguousarray(np.asarray(a, dtype=np.float64).reshape(-1))
+            self._keep.append(a)
+            return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+        def i32(a):
+            a = np.ascontiguousarray(np.asarray(a, dtype=np.int32).reshape(-1))
+            self._keep.append(a)
+            return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+        par = np.asarray(parallel_indices, dtype=np.int32).reshape(2, -1)
+        anti = np.asarray(antiparallel_indices, dtype=np.int32).reshape(2, -1)
+        cfg = AiqmcCfg()
+        cfg.nelectrons = self.N
+        cfg.natoms = self.A
+        cfg.nspins[0], cfg.nspins[1] = int(nspins[0]), int(nspins[1])
+        cfg.dtype = AIQMC_F32 if dtype == torch.float32 else AIQMC_F64
+        cfg.device = int(device)
+        cfg.atoms = dbl(atoms)
+        cfg.charges = dbl(charges)
+        cfg.spin_up_indices = i32(spin_up_indices)
+        cfg.spin_down_indices = i32(spin_down_indices)
+        cfg.parallel_indices = i32(par)
+        cfg.n_parallel = par.shape[1]
+        cfg.antiparallel_indices = i32(anti)
+        cfg.n_antiparallel = anti.shape[1]
+        for l in range(3):
+            cfg.hidden_dims[l][0] = 4
+            cfg.hidden_dims[l][1] = 4
+            cfg.hidden_dims_ynlm[l] = 6
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib.aiqmc_create(ctypes.byref(cfg), ctypes.byref(h)), "aiqmc_create")
+        self._h = h
+        self._lib = lib
+        self.nparams = int(lib.aiqmc_param_count(h))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                self._lib.aiqmc_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    # -- helpers ---------------------------------------------------------
+    def _pos(self, pos: torch.Tensor) -> torch.Tensor:
+        if not isinstance(pos, torch.Tensor):
+            pos = torch.as_tensor(np.asarray(pos))
+        pos = pos.to(device=self.device, dtype=self.dtype).contiguous()
+        if pos.shape[-1] != 3 * self.N:
+            raise ValueError(f"positions must have trailing dim 3N={3 * self.N}, got {tuple(pos.shape)}")
+        return pos.reshape(-1, 3 * self.N)
+
+    def set_params(self, flat: np.ndarray):
+        flat = np.ascontiguousarray(np.asarray(flat, dtype=np.float64).reshape(-1))
+        if flat.size != self.nparams:
+            raise ValueError(f"expected {self.nparams} parameters, got {flat.size}")
+        with torch.cuda.device(self.device):
+            check(self._lib.aiqmc_set_params(self._h, flat.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                             flat.size, _stream(self.device)), "aiqmc_set_params")
+
+    def logpsi(self, pos: torch.Tensor, with_phase: bool = True):
+        p = self._pos(pos)
+        B = p.shape[0]
+        logabs = torch.empty(B, dtype=self.dtype, device=self.device)
+        phase = torch.empty(B, dtype=self.dtype, device=self.device) if with_phase else None
+        check(self._lib.aiqmc_logpsi(self._h, _ptr(p), B, _ptr(logabs), _ptr(phase), _stream(self.device)),
+              "aiqmc_logpsi")
+        return logabs, phase
+
+    def logpsi_grad(self, pos: torch.Tensor):
+        p = self._pos(pos)
+        B = p.shape[0]
+        logabs = torch.empty(B, dtype=self.dtype, device=self.device)
+        grad = torch.empty_like(p)
+        check(self._lib.aiqmc_logpsi_grad(self._h, _ptr(p), B, _ptr(logabs), _ptr(grad), _stream(self.device)),
+              "aiqmc_logpsi_grad")
+        return logabs, grad
+
+    def local_energy(self, pos: torch.Tensor, want_logabs: bool = False, want_grad: bool = False,
+                     out: Optional[torch.Tensor] = None):
+        p = self._pos(pos)
+        B = p.shape[0]
+        el = out if out is not None else torch.empty(B, dtype=self.dtype, device=self.device)
+        logabs = torch.empty(B, dtype=self.dtype, device=self.device) if want_logabs else None
+        grad = torch.empty_like(p) if want_grad else None
+        check(self._lib.aiqmc_local_energy(self._h, _ptr(p), B, _ptr(el), _ptr(logabs), _ptr(grad),
+                                           _stream(self.device)), "aiqmc_local_energy")
+        return el, logabs, grad
+
+    def mc_step(self, pos: torch.Tensor, nsteps: int, tstep: float, gauss1=None, gauss2=None, u=None,
+                seed: int = 0, offset: int = 0, count_accepts: bool = False):
+        """In-place Metropolis on `pos` (must be a contiguous device tensor of ctx dtype)."""
+        if not (pos.is_cuda and pos.dtype == self.dtype and pos.is_contiguous()):
+            raise ValueError("mc_step needs a contiguous device tensor of the context dtype (updated in place)")
+        B = pos.numel() // (3 * self.N)
+        host = gauss1 is not None
+        acc = torch.zeros(B, dtype=torch.int32, device=self.device) if count_accepts else None
+        if host:
+            g1 = gauss1.to(self.device, self.dtype).contiguous()
+            g2 = gauss2.to(self.device, self.dtype).contiguous()
+            uu = u.to(self.device, self.dtype).contiguous()
+            if g1.numel() != nsteps * B * 3 * self.N or g2.numel() != nsteps * B * self.N * 3 or \
+                    uu.numel() != nsteps * B * self.N:
+                raise ValueError("host draws have the wrong size")
+        else:
+            g1 = g2 = uu = None
+        check(self._lib.aiqmc_mc_step(self._h, _ptr(pos), B, int(nsteps), float(tstep),
+                                      AIQMC_RNG_HOST if host else AIQMC_RNG_PHILOX,
+                                      _ptr(g1), _ptr(g2), _ptr(uu), ctypes.c_uint64(seed),
+                                      ctypes.c_uint64(offset), _ptr(acc), _stream(self.device)),
+              "aiqmc_mc_step")
+        return acc

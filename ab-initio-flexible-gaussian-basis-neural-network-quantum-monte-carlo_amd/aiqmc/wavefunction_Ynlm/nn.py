@@ -1,0 +1,209 @@
+"""AIQMC wavefunction factory (drop-in for AIQMCrelease3/wavefunction_Ynlm/nn.py).
+
+``make_ai_net`` has the reference signature (nn.py:511-526) and returns a
+``Network(init, apply, orbitals)``.  ``apply(params, pos, spins, atoms,
+charges) -> (phase, log|psi|)`` evaluates on the GPU through the HIP kernel
+``k_walker`` (libaiqmc_hip.so); unlike the reference it accepts a batch
+``pos[..., 3N]`` directly (the reference callers vmap it).
+
+Parameters are the reference pytree (nested dict/list of arrays, nn.py:203-278,
+370-407); they are flattened in JAX ``tree_flatten`` order for the C-ABI.
+Reference behaviours kept: ``spins`` is ignored by apply (the spin tables are
+closures), ``determinants`` is ignored (one full determinant, Q10), the import
+side effects of nn.py:557-599 are NOT reproduced (Q12).
+"""
+from __future__ import annotations
+
+import dataclasses
+import hashlib
+import math
+from typing import Any, Dict, Optional, Tuple
+
+import numpy as np
+import torch
+
+from .. import _lib
+
+DEFAULT_HIDDEN_DIMS = ((4, 4), (4, 4), (4, 4))
+DEFAULT_HIDDEN_DIMS_YNLM = (6, 6, 6)
+
+
+@dataclasses.dataclass
+class AINetData:
+    """nn.py:20-25.  positions [B,3N]; spins/atoms/charges per walker or shared."""
+    positions: Any
+    spins: Any
+    atoms: Any
+    charges: Any
+
+    def __iter__(self):
+        return iter(dataclasses.asdict(self).items())
+
+    def keys(self):
+        return [f.name for f in dataclasses.fields(self)]
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+
+@dataclasses.dataclass
+class Network:
+    init: Any
+    apply: Any
+    orbitals: Any
+
+
+def tree_flatten(tree):
+    """JAX tree_flatten leaf order: dict keys sorted, lists in order."""
+    if isinstance(tree, dict):
+        out = []
+        for k in sorted(tree.keys()):
+            out.extend(tree_flatten(tree[k]))
+        return out
+    if isinstance(tree, (list, tuple)):
+        out = []
+        for v in tree:
+            out.extend(tree_flatten(v))
+        return out
+    if isinstance(tree, torch.Tensor):
+        return [tree.detach().to("cpu", torch.float64).numpy()]
+    return [np.asarray(tree, dtype=np.float64)]
+
+
+def flatten_params(params) -> np.ndarray:
+    leaves = tree_flatten(params)
+    return np.concatenate([l.reshape(-1) for l in leaves]) if leaves else np.zeros(0)
+
+
+def _first(x):
+    """Accept jnp.nonzero-style 1-tuples or plain arrays."""
+    if isinstance(x, tuple) and len(x) == 1:
+        x = x[0]
+    return np.asarray(x, dtype=np.int32).reshape(-1)
+
+
+def _atoms_charges(atoms, charges):
+    a = atoms.detach().cpu().numpy() if isinstance(atoms, torch.Tensor) else np.asarray(atoms)
+    c = charges.detach().cpu().numpy() if isinstance(charges, torch.Tensor) else np.asarray(charges)
+    a = np.asarray(a, dtype=np.float64)
+    c = np.asarray(c, dtype=np.float64)
+    if a.ndim == 3:          # batch-tiled atoms (driver layout, main_all_electrons_adam_muti_GPU.py:87)
+        a = a.reshape(-1, a.shape[-2], a.shape[-1])[0]
+    if c.ndim == 2:
+        c = c.reshape(-1, c.shape[-1])[0]
+    return a, c
+
+
+class AINet:
+    """Holds the closures of make_ai_net and the per-(device, dtype, atoms) HIP contexts."""
+
+    def __init__(self, nspins, charges, parallel_indices, antiparallel_indices, spin_up_indices,
+                 spin_down_indices, n_parallel, n_antiparallel, ndim, natoms, nelectrons):
+        if ndim != 3:
+            raise NotImplementedError("ndim must be 3")
+        self.nspins = (int(nspins[0]), int(nspins[1]))
+        self.charges = np.asarray(charges.detach().cpu() if isinstance(charges, torch.Tensor) else charges,
+                                  dtype=np.float64)
+        self.par = np.asarray(parallel_indices, dtype=np.int32).reshape(2, -1)
+        self.anti = np.asarray(antiparallel_indices, dtype=np.int32).reshape(2, -1)
+        if self.par.shape[1] != n_parallel or self.anti.shape[1] != n_antiparallel:
+            raise ValueError("n_parallel / n_antiparallel do not match the index tables")
+        self.up = _first(spin_up_indices)
+        self.dn = _first(spin_down_indices)
+        self.natoms = int(natoms)
+        self.nelectrons = int(nelectrons)
+        self._ctx: Dict[Tuple, _lib.Context] = {}
+        self._loaded: Dict[Tuple, str] = {}
+
+    # -- init (nn.py:203-278, 370-407; network_blocks.py:63-102) --------------
+    def init(self, key) -> Dict[str, Any]:
+        rng = key if isinstance(key, np.random.Generator) else np.random.default_rng(int(key))
+        N, A = self.nelectrons, self.natoms
+        nch = len([s for s in self.nspins if s > 0])
+
+        def lin(i, o, bias=True):
+            p = {"w": rng.standard_normal((i, o)) / math.sqrt(float(i))}
+            if bias:
+                p["b"] = rng.standard_normal((o,))
+            return p
+
+        d1, d2, dy = 4 * A, 4, 4 * A + 2
+        streams, streams_y = [], []
+        for l in range(3):
+            din = (nch + 1) * d1 + nch * d2
+            layer = {"convolutional": {"w": rng.standard_normal((N, din)) / math.sqrt(float(N)),
+                                       "b": rng.standard_normal((N, din // 4))},
+                     "single": lin(din // 4, 4)}
+            if l < 2:
+                layer["double"] = lin(d2, 4)
+            streams.append(layer)
+            streams_y.append({"single_Ynlm": lin(dy, 6)})
+            d1, d2, dy = 4, 4, 6
+        return {
+            "layers": {"input": {}, "streams": streams, "streams_y": streams_y},
+            "orbitals": [lin(d1, 2 * N) for _ in range(nch)],
+            "y": [{"w": rng.standard_normal((dy, N)) / math.sqrt(float(dy))}],
+            "jastrow_ee": {"ee_par": np.ones(self.par.shape[1]), "ee_anti": np.ones(self.anti.shape[1])},
+            "jastrow_ae": {"ae": np.ones((N, A))},
+            "envelope": [{"pi": np.ones((A, 3)), "sigma": np.ones((A, 3)), "alpha": np.ones(1),
+                          "beta": np.ones(A), "xi": np.ones(1), "eplion": np.ones((A, 3)),
+                          "mu": np.ones(A), "nu": np.ones(A)} for _ in range(N)],
+        }
+
+    # -- HIP context management ---------------------------------------------
+    def context(self, atoms, dtype=torch.float32, device: Optional[int] = None) -> _lib.Context:
+        a, _ = _atoms_charges(atoms, self.charges)
+        if device is None:
+            device = torch.cuda.current_device()
+        key = (int(device), dtype, a.tobytes())
+        ctx = self._ctx.get(key)
+        if ctx is None:
+            ctx = _lib.Context(self.nelectrons, self.natoms, self.nspins, a, self.charges, self.up, self.dn,
+                               self.par, self.anti, dtype=dtype, device=int(device))
+            self._ctx[key] = ctx
+        return ctx
+
+    def bind(self, params, atoms, dtype=torch.float32, device: Optional[int] = None) -> _lib.Context:
+        """Context with `params` uploaded (re-uploads only when the values changed)."""
+        ctx = self.context(atoms, dtype, device)
+        flat = flatten_params(params)
+        digest = hashlib.sha1(flat.tobytes()).hexdigest()
+        k = id(ctx)
+        if self._loaded.get(k) != digest:
+            ctx.set_params(flat)
+            self._loaded[k] = digest
+        return ctx
+
+    # -- apply (nn.py:545-551) --------------------------------------------------
+    def apply(self, params, pos, spins=None, atoms=None, charges=None):
+        del spins, charges   # closures, as in the reference
+        pos_t = pos if isinstance(pos, torch.Tensor) else torch.as_tensor(np.asarray(pos))
+        dtype = pos_t.dtype if pos_t.dtype in (torch.float32, torch.float64) else torch.float32
+        ctx = self.bind(params, atoms, dtype)
+        logabs, phase = ctx.logpsi(pos_t)
+        shape = pos_t.shape[:-1]
+        return phase.reshape(shape), logabs.reshape(shape)
+
+    def orbitals(self, params, pos, spins=None, atoms=None, charges=None):
+        raise NotImplementedError("the orbital matrix is internal to the HIP kernel; use apply()")
+
+
+def make_ai_net(nspins, charges, parallel_indices, antiparallel_indices, spin_up_indices, spin_down_indices,
+                n_parallel: int, n_antiparallel: int, ndim: int, natoms: int, nelectrons: int,
+                determinants: int = 1, bias_orbitals: bool = True, rescale_inputs: bool = False,
+                hidden_dims=DEFAULT_HIDDEN_DIMS, hidden_dims_Ynlm=DEFAULT_HIDDEN_DIMS_YNLM) -> Network:
+    """nn.py:511-553.  ``determinants`` is ignored exactly as in the reference (Q10)."""
+    del determinants
+    if not bias_orbitals:
+        raise NotImplementedError("bias_orbitals=False is not built (reference default True)")
+    if rescale_inputs:
+        raise NotImplementedError("rescale_inputs=True is not built (reference default False)")
+    if tuple(tuple(h) for h in hidden_dims) != DEFAULT_HIDDEN_DIMS or \
+            tuple(hidden_dims_Ynlm) != DEFAULT_HIDDEN_DIMS_YNLM:
+        raise NotImplementedError("only the default hidden dims are built")
+    net = AINet(nspins, charges, parallel_indices, antiparallel_indices, spin_up_indices, spin_down_indices,
+                n_parallel, n_antiparallel, ndim, natoms, nelectrons)
+    apply = net.apply
+    apply_fn = lambda *a, **k: apply(*a, **k)
+    apply_fn._aiqmc_network = net
+    return Network(init=net.init, apply=apply_fn, orbitals=net.orbitals)

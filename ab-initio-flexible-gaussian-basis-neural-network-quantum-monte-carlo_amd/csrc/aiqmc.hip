@@ -1,0 +1,351 @@
+// aiqmc.hip -- MI355X (gfx950) AIQMC VMC inner loop: kernels + C-ABI.
+//
+// Entry points are declared in include/aiqmc.h (which cites the reference
+// functions each one replaces).  Kernels:
+//   k_walker<T,N,A,MODE>  one wavefront per configuration (walker_kernel.h)
+//   k_taueff              device-batch reduction of |grad|^2 -> limdrift factor
+//   k_accept              Metropolis acceptance + move (VMCmcstep.py:84-106)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "aiqmc.h"
+#include "ctx.h"
+
+using namespace aq;
+
+// ============================================================================ small kernels
+
+// v2 = sum(x[0..n)) ; taueff = (sqrt(1 + 2 tau a v2) - 1)/(a v2), a = 0.25  (VMCmcstep.py:11-14)
+template <typename T>
+__global__ __launch_bounds__(256) void k_taueff(const T* __restrict__ x, int n, double tstep, double* out) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) s += (double)x[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double v2 = red[0];
+    const double a = 0.25;
+    T v2t = (T)v2;
+    T te = (sqrt((T)1 + (T)2 * (T)tstep * (T)a * v2t) - (T)1) / ((T)a * v2t);
+    *out = (double)te;
+  }
+}
+
+// ============================================================================ host side
+
+static thread_local std::string g_err;
+int aiqmc_fail(int code, const std::string& m) {
+  g_err = m;
+  return code;
+}
+static int fail(int code, const std::string& m) { return aiqmc_fail(code, m); }
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) return fail(AIQMC_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+static bool shape_ops(int N, int A, ShapeOps* ops) {
+#define AIQMC_CASE(n, a) \
+  if (N == n && A == a) return aiqmc_shape_ops_##n##_##a(ops);
+  AIQMC_SHAPE_LIST(AIQMC_CASE)
+#undef AIQMC_CASE
+  return false;
+}
+
+static void free_ws(aiqmc_ctx* c) {
+  void* ps[] = {c->d_grad, c->d_lp, c->d_sq, c->d_lpn, c->d_gown, c->d_sqn, c->d_taueff};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+  c->d_grad = c->d_lp = c->d_sq = c->d_lpn = c->d_gown = c->d_sqn = nullptr;
+  c->d_taueff = nullptr;
+  c->ws_B = 0;
+  c->ws_bytes = 0;
+}
+
+static int ensure_ws(aiqmc_ctx* c, int B) {
+  if (c->ws_B >= B) return 0;
+  free_ws(c);
+  const size_t s = c->dtype == AIQMC_F32 ? 4 : 8;
+  const size_t N = (size_t)c->N;
+  size_t bytes[6] = {B * 3 * N * s, B * s, B * s, B * N * s, B * N * 3 * s, B * N * s};
+  void** ptrs[6] = {&c->d_grad, &c->d_lp, &c->d_sq, &c->d_lpn, &c->d_gown, &c->d_sqn};
+  int64_t tot = 0;
+  for (int k = 0; k < 6; ++k) {
+    HIPCHK(hipMalloc(ptrs[k], bytes[k]));
+    tot += (int64_t)bytes[k];
+  }
+  HIPCHK(hipMalloc((void**)&c->d_taueff, 2 * sizeof(double)));
+  c->ws_B = B;
+  c->ws_bytes = tot + 16;
+  return 0;
+}
+
+// ============================================================================ C-ABI
+
+extern "C" {
+
+const char* aiqmc_last_error(void) { return g_err.c_str(); }
+
+const char* aiqmc_supported_shapes(void) {
+  static std::string s;
+  if (s.empty()) {
+#define AIQMC_NAME(n, a) s += (s.empty() ? "" : ",") + std::to_string(n) + ":" + std::to_string(a);
+    AIQMC_SHAPE_LIST(AIQMC_NAME)
+#undef AIQMC_NAME
+  }
+  return s.c_str();
+}
+
+int aiqmc_create(const aiqmc_cfg* cfg, aiqmc_ctx** out) {
+  if (!cfg || !out) return fail(AIQMC_EINVAL, "null argument");
+  *out = nullptr;
+  const int N = cfg->nelectrons, A = cfg->natoms;
+  if (N < 2 || N > 16) return fail(AIQMC_EUNSUPPORTED, "nelectrons must be in [2,16]");
+  if (cfg->nspins[0] <= 0 || cfg->nspins[1] <= 0 || cfg->nspins[0] + cfg->nspins[1] != N)
+    return fail(AIQMC_EUNSUPPORTED, "both spin channels must be occupied and sum to nelectrons");
+  for (int l = 0; l < 3; ++l)
+    if (cfg->hidden_dims[l][0] != NH || cfg->hidden_dims[l][1] != NH2 || cfg->hidden_dims_ynlm[l] != NYW)
+      return fail(AIQMC_EUNSUPPORTED, "only the default hidden dims ((4,4),(4,4),(4,4)) / (6,6,6) are built");
+  if (cfg->dtype != AIQMC_F32 && cfg->dtype != AIQMC_F64) return fail(AIQMC_EINVAL, "dtype");
+  ShapeOps ops;
+  if (!shape_ops(N, A, &ops))
+    return fail(AIQMC_EUNSUPPORTED, "no kernel instantiation for (N,A)=(" + std::to_string(N) + "," +
+                                        std::to_string(A) + "); supported: " + aiqmc_supported_shapes());
+  if (cfg->n_parallel + cfg->n_antiparallel != N * (N - 1) / 2)
+    return fail(AIQMC_EINVAL, "pair tables must cover all N(N-1)/2 pairs");
+  aiqmc_ctx* c = new (std::nothrow) aiqmc_ctx();
+  if (!c) return fail(AIQMC_EINVAL, "oom");
+  c->N = N;
+  c->A = A;
+  c->nup = cfg->nspins[0];
+  c->ndn = cfg->nspins[1];
+  c->dtype = cfg->dtype;
+  c->device = cfg->device;
+  c->npar = cfg->n_parallel;
+  c->nanti = cfg->n_antiparallel;
+  c->atoms.assign(cfg->atoms, cfg->atoms + 3 * A);
+  c->charges.assign(cfg->charges, cfg->charges + A);
+  c->up.assign(cfg->spin_up_indices, cfg->spin_up_indices + c->nup);
+  c->dn.assign(cfg->spin_down_indices, cfg->spin_down_indices + c->ndn);
+  c->par.assign(cfg->parallel_indices, cfg->parallel_indices + 2 * c->npar);
+  c->anti.assign(cfg->antiparallel_indices, cfg->antiparallel_indices + 2 * c->nanti);
+  for (int v : c->up)
+    if (v < 0 || v >= N) { delete c; return fail(AIQMC_EINVAL, "spin_up_indices out of range"); }
+  for (int v : c->dn)
+    if (v < 0 || v >= N) { delete c; return fail(AIQMC_EINVAL, "spin_down_indices out of range"); }
+  for (int v : c->par)
+    if (v < 0 || v >= N) { delete c; return fail(AIQMC_EINVAL, "parallel_indices out of range"); }
+  for (int v : c->anti)
+    if (v < 0 || v >= N) { delete c; return fail(AIQMC_EINVAL, "antiparallel_indices out of range"); }
+  c->ncanon = ops.ncanon(c->npar, c->nanti);
+  c->nkern = ops.nkern;
+  hipError_t e = hipSetDevice(c->device);
+  if (e != hipSuccess) { delete c; return fail(AIQMC_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(e)); }
+  int rc = ops.set_lds();
+  if (rc) { delete c; return rc; }
+  const size_t s = c->dtype == AIQMC_F32 ? 4 : 8;
+  e = hipMalloc(&c->d_prm, (size_t)c->nkern * s);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->d_rowsrc, 16 * sizeof(int));
+  if (e != hipSuccess) {
+    if (c->d_prm) (void)hipFree(c->d_prm);
+    delete c;
+    return fail(AIQMC_EHIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+  }
+  int rows[16] = {0};
+  for (int r = 0; r < c->nup; ++r) rows[r] = c->up[r];
+  for (int r = 0; r < c->ndn; ++r) rows[c->nup + r] = c->dn[r];
+  e = hipMemcpy(c->d_rowsrc, rows, sizeof(rows), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(c->d_prm);
+    (void)hipFree(c->d_rowsrc);
+    delete c;
+    return fail(AIQMC_EHIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
+  }
+  *out = c;
+  return AIQMC_OK;
+}
+
+int aiqmc_destroy(aiqmc_ctx* c) {
+  if (!c) return AIQMC_OK;
+  (void)hipSetDevice(c->device);
+  free_ws(c);
+  if (c->d_prm) (void)hipFree(c->d_prm);
+  if (c->d_rowsrc) (void)hipFree(c->d_rowsrc);
+  delete c;
+  return AIQMC_OK;
+}
+
+int64_t aiqmc_param_count(const aiqmc_ctx* c) { return c ? c->ncanon : -1; }
+int64_t aiqmc_workspace_bytes(const aiqmc_ctx* c) { return c ? c->ws_bytes : -1; }
+
+int aiqmc_set_params(aiqmc_ctx* c, const double* flat, int64_t n, void* stream) {
+  if (!c || !flat) return fail(AIQMC_EINVAL, "null argument");
+  if (n != c->ncanon)
+    return fail(AIQMC_EINVAL, "expected " + std::to_string(c->ncanon) + " parameters, got " + std::to_string(n));
+  ShapeOps ops;
+  shape_ops(c->N, c->A, &ops);
+  std::vector<double> lay;
+  ops.pack(c, flat, lay);
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (c->dtype == AIQMC_F32) {
+    std::vector<float> f(lay.begin(), lay.end());
+    HIPCHK(hipMemcpyAsync(c->d_prm, f.data(), f.size() * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+  } else {
+    HIPCHK(hipMemcpyAsync(c->d_prm, lay.data(), lay.size() * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  c->params_set = true;
+  return AIQMC_OK;
+}
+
+static KArgs base_args(const aiqmc_ctx* c) {
+  KArgs ka;
+  std::memset(&ka, 0, sizeof(ka));
+  ka.nup = c->nup;
+  ka.rowsrc = c->d_rowsrc;
+  ka.prm = c->d_prm;
+  return ka;
+}
+
+static int check_call(aiqmc_ctx* c, const void* pos, int B) {
+  if (!c) return fail(AIQMC_EINVAL, "null context");
+  if (!c->params_set) return fail(AIQMC_ESTATE, "aiqmc_set_params has not been called");
+  if (!pos) return fail(AIQMC_EINVAL, "null positions");
+  if (B < 0) return fail(AIQMC_EINVAL, "negative batch");
+  return 0;
+}
+
+int aiqmc_logpsi(aiqmc_ctx* c, const void* pos, int32_t B, void* logabs, void* phase, void* stream) {
+  int rc = check_call(c, pos, B);
+  if (rc) return rc;
+  if (B == 0) return AIQMC_OK;
+  ShapeOps ops;
+  shape_ops(c->N, c->A, &ops);
+  KArgs ka = base_args(c);
+  ka.nconf = B;
+  ka.pos = pos;
+  ka.logabs = logabs;
+  ka.phase = phase;
+  ops.walker(c->dtype, MODE_GRAD, ka, B, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_logpsi_grad(aiqmc_ctx* c, const void* pos, int32_t B, void* logabs, void* grad, void* stream) {
+  int rc = check_call(c, pos, B);
+  if (rc) return rc;
+  if (!grad) return fail(AIQMC_EINVAL, "null grad");
+  if (B == 0) return AIQMC_OK;
+  ShapeOps ops;
+  shape_ops(c->N, c->A, &ops);
+  KArgs ka = base_args(c);
+  ka.nconf = B;
+  ka.pos = pos;
+  ka.logabs = logabs;
+  ka.grad = grad;
+  ops.walker(c->dtype, MODE_GRAD, ka, B, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_local_energy(aiqmc_ctx* c, const void* pos, int32_t B, void* e_l, void* logabs, void* grad,
+                       void* stream) {
+  int rc = check_call(c, pos, B);
+  if (rc) return rc;
+  if (!e_l) return fail(AIQMC_EINVAL, "null e_l");
+  if (B == 0) return AIQMC_OK;
+  ShapeOps ops;
+  shape_ops(c->N, c->A, &ops);
+  KArgs ka = base_args(c);
+  ka.nconf = B;
+  ka.pos = pos;
+  ka.el = e_l;
+  ka.logabs = logabs;
+  ka.grad = grad;
+  ops.walker(c->dtype, MODE_LAP, ka, B, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tstep, int32_t rng_mode,
+                  const void* gauss1, const void* gauss2, const void* u, uint64_t seed, uint64_t offset,
+                  int32_t* accept_out, void* stream) {
+  int rc = check_call(c, pos, B);
+  if (rc) return rc;
+  if (nsteps < 0) return fail(AIQMC_EINVAL, "negative nsteps");
+  if (!(tstep > 0.0)) return fail(AIQMC_EINVAL, "tstep must be > 0");
+  if (rng_mode == AIQMC_RNG_HOST && (!gauss1 || !gauss2 || !u))
+    return fail(AIQMC_EINVAL, "AIQMC_RNG_HOST needs gauss1, gauss2 and u");
+  if (rng_mode != AIQMC_RNG_HOST && rng_mode != AIQMC_RNG_PHILOX) return fail(AIQMC_EINVAL, "rng_mode");
+  if (B == 0 || nsteps == 0) return AIQMC_OK;
+  HIPCHK(hipSetDevice(c->device));
+  rc = ensure_ws(c, B);
+  if (rc) return rc;
+  ShapeOps ops;
+  shape_ops(c->N, c->A, &ops);
+  hipStream_t s = (hipStream_t)stream;
+  const int N = c->N;
+  const size_t es = c->dtype == AIQMC_F32 ? 4 : 8;
+  for (int st = 0; st < nsteps; ++st) {
+    const uint64_t step = offset + (uint64_t)st;
+    const char* g1 = rng_mode == AIQMC_RNG_HOST ? (const char*)gauss1 + (size_t)st * B * 3 * N * es : nullptr;
+    const char* g2 = rng_mode == AIQMC_RNG_HOST ? (const char*)gauss2 + (size_t)st * B * N * 3 * es : nullptr;
+    const char* uu = rng_mode == AIQMC_RNG_HOST ? (const char*)u + (size_t)st * B * N * es : nullptr;
+    // (1) grad log|psi| at the walkers (VMCmcstep.py:41-53)
+    KArgs ka = base_args(c);
+    ka.nconf = B;
+    ka.pos = pos;
+    ka.logabs = c->d_lp;
+    ka.grad = c->d_grad;
+    ka.sumsq = c->d_sq;
+    ops.walker(c->dtype, MODE_GRAD, ka, B, s);
+    // (2) limdrift factor over the device batch (:60)
+    if (c->dtype == AIQMC_F32)
+      k_taueff<float><<<dim3(1), dim3(256), 0, s>>>((const float*)c->d_sq, B, tstep, c->d_taueff);
+    else
+      k_taueff<double><<<dim3(1), dim3(256), 0, s>>>((const double*)c->d_sq, B, tstep, c->d_taueff);
+    // (3) single-electron proposals x^(i): value + gradient (:55-79, :95-97)
+    KArgs kp = base_args(c);
+    kp.nconf = B * N;
+    kp.pos = pos;
+    kp.proposal = 1;
+    kp.pgrad = c->d_grad;
+    kp.gauss1 = g1;
+    kp.taueff = c->d_taueff;
+    kp.tstep = tstep;
+    kp.seed = seed;
+    kp.step = step;
+    kp.logabs = c->d_lpn;
+    kp.gown = c->d_gown;
+    kp.sumsq = c->d_sqn;
+    ops.walker(c->dtype, MODE_GRAD, kp, B * N, s);
+    // (4) limdrift factor of the proposal gradients over all B*N*3N entries (:80)
+    if (c->dtype == AIQMC_F32)
+      k_taueff<float><<<dim3(1), dim3(256), 0, s>>>((const float*)c->d_sqn, B * N, tstep,
+                         c->d_taueff + 1);
+    else
+      k_taueff<double><<<dim3(1), dim3(256), 0, s>>>((const double*)c->d_sqn, B * N, tstep,
+                         c->d_taueff + 1);
+    // (5) acceptance and move (:83-106)
+    ops.accept(c->dtype, pos, c->d_grad, c->d_gown, c->d_lp, c->d_lpn, g1, g2, uu, c->d_taueff, B, tstep, seed, step,
+               accept_out, s);
+  }
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,49 @@
+// ctx.h -- host-side context + per-shape dispatch table shared by the
+// C-ABI translation unit (aiqmc.hip) and the per-shape kernel TUs (shape.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "aiqmc.h"
+#include "walker_kernel.h"
+
+// (N, A) instantiations; the Makefile compiles shape.hip once per entry.
+#define AIQMC_SHAPE_LIST(X) X(2, 2) X(4, 1) X(6, 1) X(8, 1) X(10, 1) X(12, 2) X(14, 2)
+
+int aiqmc_fail(int code, const std::string& msg);
+using aq::KArgs;
+
+struct aiqmc_ctx {
+  int N = 0, A = 0, nup = 0, ndn = 0, dtype = 0, device = 0;
+  int npar = 0, nanti = 0;
+  std::vector<double> atoms, charges;
+  std::vector<int> up, dn, par, anti;
+  int64_t ncanon = 0, nkern = 0;
+  void* d_prm = nullptr;
+  int* d_rowsrc = nullptr;
+  bool params_set = false;
+  int ws_B = 0;
+  void *d_grad = nullptr, *d_lp = nullptr, *d_sq = nullptr, *d_lpn = nullptr, *d_gown = nullptr,
+       *d_sqn = nullptr;
+  double* d_taueff = nullptr;
+  int64_t ws_bytes = 0;
+};
+
+struct ShapeOps {
+  int (*set_lds)();
+  void (*walker)(int dtype, int mode, const KArgs& ka, int nconf, hipStream_t s);
+  void (*accept)(int dtype, void* pos, const void* grad, const void* gown, const void* lp, const void* lpn,
+                 const void* g1, const void* g2, const void* u, const double* te, int B, double tstep,
+                 uint64_t seed, uint64_t step, int32_t* acc, hipStream_t s);
+  int64_t nkern;
+  long (*ncanon)(int npar, int nanti);
+  void (*pack)(const aiqmc_ctx* c, const double* flat, std::vector<double>& out);
+};
+
+
+#define AIQMC_DECL(n, a) bool aiqmc_shape_ops_##n##_##a(ShapeOps* ops);
+AIQMC_SHAPE_LIST(AIQMC_DECL)
+#undef AIQMC_DECL

@@ -1,0 +1,207 @@
+// jets.h -- per-lane Taylor jets and wave primitives for the AIQMC walker kernels.
+//
+// Lane layout of one 64-wide wavefront that evaluates ONE electron
+// configuration (N <= 16 electrons):
+//
+//   lane l = 16*c + e      c = l >> 4 in {0,1,2,3},  e = l & 15
+//   c < 3, e < N : "direction lane" for the coordinate x_{e,c}
+//   c == 3       : "value row" (lanes 48..63)
+//
+// PJ<T>  {v, d1, d2}: every lane carries a value and the first/second
+//        derivative along its OWN direction (value-row lanes: direction 0).
+//        Used for per-electron and per-pair streams, whose values differ
+//        between lanes.
+// DJ<T>  {d1, d2}: a quantity shared by the whole wave.  Direction lanes hold
+//        the first/second directional derivative; value-row lanes hold the
+//        value in d1.  One VGPR (two with second derivatives) per scalar.
+//
+// The second derivative kept per lane is the diagonal Hessian entry along the
+// lane's coordinate, so the Laplacian is the sum over direction lanes (the
+// forward-Laplacian of the reference's jvp-of-grad loop,
+// Energy/hamiltonian.py:100-131).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace aq {
+
+template <typename T> __device__ __forceinline__ T f_sqrt(T x);
+template <> __device__ __forceinline__ float f_sqrt(float x) { return sqrtf(x); }
+template <> __device__ __forceinline__ double f_sqrt(double x) { return sqrt(x); }
+template <typename T> __device__ __forceinline__ T f_exp(T x);
+template <> __device__ __forceinline__ float f_exp(float x) { return expf(x); }
+template <> __device__ __forceinline__ double f_exp(double x) { return exp(x); }
+template <typename T> __device__ __forceinline__ T f_log(T x);
+template <> __device__ __forceinline__ float f_log(float x) { return logf(x); }
+template <> __device__ __forceinline__ double f_log(double x) { return log(x); }
+template <typename T> __device__ __forceinline__ T f_tanh(T x);
+template <> __device__ __forceinline__ float f_tanh(float x) { return tanhf(x); }
+template <> __device__ __forceinline__ double f_tanh(double x) { return tanh(x); }
+template <typename T> __device__ __forceinline__ T f_abs(T x);
+template <> __device__ __forceinline__ float f_abs(float x) { return fabsf(x); }
+template <> __device__ __forceinline__ double f_abs(double x) { return fabs(x); }
+template <typename T> __device__ __forceinline__ T f_hypot(T x, T y);
+template <> __device__ __forceinline__ float f_hypot(float x, float y) { return hypotf(x, y); }
+template <> __device__ __forceinline__ double f_hypot(double x, double y) { return hypot(x, y); }
+template <typename T> __device__ __forceinline__ T f_atan2(T y, T x);
+template <> __device__ __forceinline__ float f_atan2(float y, float x) { return atan2f(y, x); }
+template <> __device__ __forceinline__ double f_atan2(double y, double x) { return atan2(y, x); }
+
+// ---------------------------------------------------------------------------
+// PJ: univariate second-order Taylor jet along the lane's direction
+// ---------------------------------------------------------------------------
+template <typename T> struct PJ { T v, d1, d2; };
+
+template <typename T> __device__ __forceinline__ PJ<T> pjc(T c) { return PJ<T>{c, T(0), T(0)}; }
+template <typename T> __device__ __forceinline__ PJ<T> operator+(PJ<T> a, PJ<T> b) {
+  return PJ<T>{a.v + b.v, a.d1 + b.d1, a.d2 + b.d2};
+}
+template <typename T> __device__ __forceinline__ PJ<T> operator-(PJ<T> a, PJ<T> b) {
+  return PJ<T>{a.v - b.v, a.d1 - b.d1, a.d2 - b.d2};
+}
+template <typename T> __device__ __forceinline__ PJ<T> operator-(PJ<T> a) {
+  return PJ<T>{-a.v, -a.d1, -a.d2};
+}
+template <typename T> __device__ __forceinline__ PJ<T> operator*(PJ<T> a, PJ<T> b) {
+  return PJ<T>{a.v * b.v, a.d1 * b.v + a.v * b.d1, a.d2 * b.v + T(2) * a.d1 * b.d1 + a.v * b.d2};
+}
+template <typename T> __device__ __forceinline__ PJ<T> operator*(T s, PJ<T> a) {
+  return PJ<T>{s * a.v, s * a.d1, s * a.d2};
+}
+template <typename T> __device__ __forceinline__ PJ<T> operator+(PJ<T> a, T s) {
+  return PJ<T>{a.v + s, a.d1, a.d2};
+}
+template <typename T> __device__ __forceinline__ PJ<T> operator-(PJ<T> a, T s) {
+  return PJ<T>{a.v - s, a.d1, a.d2};
+}
+// a / b   (a = q b  =>  q' = (a' - q b')/b,  q'' = (a'' - 2 q' b' - q b'')/b)
+template <typename T> __device__ __forceinline__ PJ<T> operator/(PJ<T> a, PJ<T> b) {
+  const T q = a.v / b.v;
+  const T ib = T(1) / b.v;
+  const T q1 = (a.d1 - q * b.d1) * ib;
+  const T q2 = (a.d2 - T(2) * q1 * b.d1 - q * b.d2) * ib;
+  return PJ<T>{q, q1, q2};
+}
+template <typename T> __device__ __forceinline__ PJ<T> operator/(PJ<T> a, T s) {
+  return PJ<T>{a.v / s, a.d1 / s, a.d2 / s};
+}
+template <typename T> __device__ __forceinline__ PJ<T> pj_sqrt(PJ<T> a) {
+  const T s = f_sqrt(a.v);
+  const T h = T(0.5) / s;
+  const T s1 = a.d1 * h;
+  return PJ<T>{s, s1, (a.d2 - T(2) * s1 * s1) * h};
+}
+template <typename T> __device__ __forceinline__ PJ<T> pj_exp(PJ<T> a) {
+  const T e = f_exp(a.v);
+  return PJ<T>{e, e * a.d1, e * (a.d2 + a.d1 * a.d1)};
+}
+template <typename T> __device__ __forceinline__ PJ<T> pj_tanh(PJ<T> a) {
+  const T t = f_tanh(a.v);
+  const T s = T(1) - t * t;
+  return PJ<T>{t, s * a.d1, s * a.d2 - T(2) * t * s * a.d1 * a.d1};
+}
+template <typename T> __device__ __forceinline__ PJ<T> pj_sel(bool c, PJ<T> a, PJ<T> b) {
+  return PJ<T>{c ? a.v : b.v, c ? a.d1 : b.d1, c ? a.d2 : b.d2};
+}
+
+// ---------------------------------------------------------------------------
+// wave primitives
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float rdlane(float x, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
+}
+__device__ __forceinline__ double rdlane(double x, int l) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ int rdlane(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+
+template <int CTRL> __device__ __forceinline__ float dpp(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL> __device__ __forceinline__ double dpp(double x) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xF, 0xF, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// Sum over the 16 lanes of each DPP row; every lane of the row receives the
+// (bitwise identical) row total.  quad_perm[1,0,3,2], quad_perm[2,3,0,1],
+// row_half_mirror, row_mirror.
+template <typename T> __device__ __forceinline__ T rowsum16(T x) {
+  x += dpp<0xB1>(x);
+  x += dpp<0x4E>(x);
+  x += dpp<0x141>(x);
+  x += dpp<0x140>(x);
+  return x;
+}
+
+// Sum over all 64 lanes, uniform result.
+template <typename T> __device__ __forceinline__ T wave_sum(T x) {
+  x = rowsum16(x);
+  return (rdlane(x, 0) + rdlane(x, 16)) + (rdlane(x, 32) + rdlane(x, 48));
+}
+
+// ---------------------------------------------------------------------------
+// DJ: wave-shared jet (direction lanes: derivatives, value row: value in d1)
+// ---------------------------------------------------------------------------
+template <typename T> struct DJ { T d1, d2; };
+
+template <typename T> __device__ __forceinline__ DJ<T> dj_zero() { return DJ<T>{T(0), T(0)}; }
+template <typename T> __device__ __forceinline__ void dj_axpy(DJ<T>& acc, T w, DJ<T> x) {
+  acc.d1 += w * x.d1;
+  acc.d2 += w * x.d2;
+}
+// tanh of a wave-shared jet; the value is broadcast from lane 48.
+template <typename T> __device__ __forceinline__ DJ<T> dj_tanh(DJ<T> z, bool val) {
+  const T zv = rdlane(z.d1, 48);
+  const T t = f_tanh(zv);
+  const T s = T(1) - t * t;
+  DJ<T> o;
+  o.d1 = val ? t : s * z.d1;
+  o.d2 = s * z.d2 - T(2) * t * s * z.d1 * z.d1;
+  return o;
+}
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 counter-based RNG (production random draws)
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+    const uint32_t n1 = (uint32_t)p1;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    const uint32_t n3 = (uint32_t)p0;
+    c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+// 4 uniforms in (0,1] from (seed, step, stream id, kind)
+__device__ __forceinline__ void philox_uniform4(uint64_t seed, uint64_t step, uint32_t sid, uint32_t kind,
+                                                double u[4]) {
+  uint32_t c[4] = {sid, (uint32_t)step, (uint32_t)(step >> 32), kind};
+  philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) u[j] = ((double)c[j] + 1.0) * 2.3283064365386963e-10;   // (0,1]
+}
+// 3 standard normals (Box-Muller on 4 uniforms)
+template <typename T>
+__device__ __forceinline__ void philox_normal3(uint64_t seed, uint64_t step, uint32_t sid, uint32_t kind, T out[3]) {
+  double u[4];
+  philox_uniform4(seed, step, sid, kind, u);
+  const double r0 = sqrt(-2.0 * log(u[0])), r1 = sqrt(-2.0 * log(u[2]));
+  const double tp = 6.283185307179586;
+  out[0] = (T)(r0 * cos(tp * u[1]));
+  out[1] = (T)(r0 * sin(tp * u[1]));
+  out[2] = (T)(r1 * cos(tp * u[3]));
+}
+
+}  // namespace aq

@@ -1,0 +1,88 @@
+// layout.h -- kernel-side parameter layout for the AIQMC network (N electrons,
+// A atoms, two occupied spin channels, default hidden dims).
+//
+// The host repacks the canonical tree_flatten parameter vector (see
+// include/aiqmc.h) into this layout once per aiqmc_set_params; derived
+// quantities (row-normalised y coefficients nn.py:449-451, (2Z)^{3/4},
+// (2Z)^{1/4} Jastrow.py:95, e-e cusp/alpha tables Jastrow.py:23-41, V_nn)
+// are precomputed there in double precision.
+#pragma once
+
+namespace aq {
+
+constexpr int NH = 4;    // h-stream width  (hidden_dims[l][0], nn.py:525)
+constexpr int NH2 = 4;   // pair-stream width (hidden_dims[l][1])
+constexpr int NYW = 6;   // Ynlm-stream width (hidden_dims_Ynlm, nn.py:526)
+
+template <int N, int A>
+struct Lay {
+  // conv input widths: (nchannels+1)*d1 + nchannels*d2 with 2 channels (nn.py:209-210)
+  static constexpr int D0 = 3 * 4 * A + 2 * NH2;   // layer 0
+  static constexpr int D1 = 3 * NH + 2 * NH2;      // layers 1,2
+  static constexpr int Q0 = D0 / 4, Q1 = D1 / 4;
+  static constexpr int DY0 = 4 * A + 2;            // nn.py:220
+  // network_blocks.convolu_layer weights [N][D], bias [N][D/4]
+  static constexpr int conv_w0 = 0;
+  static constexpr int conv_b0 = conv_w0 + N * D0;
+  static constexpr int conv_w1 = conv_b0 + N * Q0;
+  static constexpr int conv_b1 = conv_w1 + N * D1;
+  static constexpr int conv_w2 = conv_b1 + N * Q1;
+  static constexpr int conv_b2 = conv_w2 + N * D1;
+  // single linear [Q][4], [4]
+  static constexpr int sng_w0 = conv_b2 + N * Q1;
+  static constexpr int sng_b0 = sng_w0 + Q0 * NH;
+  static constexpr int sng_w1 = sng_b0 + NH;
+  static constexpr int sng_b1 = sng_w1 + Q1 * NH;
+  static constexpr int sng_w2 = sng_b1 + NH;
+  static constexpr int sng_b2 = sng_w2 + Q1 * NH;
+  // double (pair) linear [4][4], [4], layers 0 and 1
+  static constexpr int dbl_w0 = sng_b2 + NH;
+  static constexpr int dbl_b0 = dbl_w0 + NH2 * NH2;
+  static constexpr int dbl_w1 = dbl_b0 + NH2;
+  static constexpr int dbl_b1 = dbl_w1 + NH2 * NH2;
+  // Ynlm stream [in][6], [6]
+  static constexpr int y_w0 = dbl_b1 + NH2;
+  static constexpr int y_b0 = y_w0 + DY0 * NYW;
+  static constexpr int y_w1 = y_b0 + NYW;
+  static constexpr int y_b1 = y_w1 + NYW * NYW;
+  static constexpr int y_w2 = y_b1 + NYW;
+  static constexpr int y_b2 = y_w2 + NYW * NYW;
+  // orbitals: W[spin][f][col][re,im], b[spin][col][re,im]  (nn.py:447,456)
+  static constexpr int orb_w = y_b2 + NYW;
+  static constexpr int orb_b = orb_w + 2 * NH * N * 2;
+  // normalised y coefficients [6][N]
+  static constexpr int wy = orb_b + 2 * N * 2;
+  // Jastrow e-e: cusp [N][N] (0.25 par / 0.5 anti / 0 diag), alpha [N][N]
+  static constexpr int jee_c = wy + NYW * N;
+  static constexpr int jee_a = jee_c + N * N;
+  // Jastrow e-n beta [N][A]
+  static constexpr int jae_b = jee_a + N * N;
+  // envelope per electron: alpha[N], xi[N], beta[N][A], pi[N][A][3], sigma[N][A][3]
+  static constexpr int env_alpha = jae_b + N * A;
+  static constexpr int env_xi = env_alpha + N;
+  static constexpr int env_beta = env_xi + N;
+  static constexpr int env_pi = env_beta + N * A;
+  static constexpr int env_sigma = env_pi + N * A * 3;
+  // system
+  static constexpr int atoms = env_sigma + N * A * 3;
+  static constexpr int charges = atoms + 3 * A;
+  static constexpr int c34 = charges + A;
+  static constexpr int c14 = c34 + A;
+  static constexpr int vnn = c14 + A;
+  static constexpr int total = vnn + 1;
+
+  // canonical (tree_flatten) parameter count
+  static constexpr long canon(int npar, int nanti) {
+    return (long)N * (2 + 12 * A)                       // envelope
+           + (long)N * A                                // jastrow_ae
+           + npar + nanti                               // jastrow_ee
+           + (N * Q0 + N * D0) + (NH2 + NH2 * NH2) + (NH + Q0 * NH)   // streams[0]
+           + (N * Q1 + N * D1) + (NH2 + NH2 * NH2) + (NH + Q1 * NH)   // streams[1]
+           + (N * Q1 + N * D1) + (NH + Q1 * NH)                        // streams[2]
+           + (NYW + DY0 * NYW) + 2 * (NYW + NYW * NYW)                 // streams_y
+           + 2 * (2 * N + NH * 2 * N)                                  // orbitals
+           + NYW * N;                                                  // y
+  }
+};
+
+}  // namespace aq

@@ -1,0 +1,243 @@
+// shape.hip -- kernels and host helpers for ONE (N, A) shape.  Compiled once
+// per entry of AIQMC_SHAPE_LIST with -DAQ_N=<N> -DAQ_A=<A> (parallel build).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+
+#include "ctx.h"
+
+using namespace aq;
+
+#ifndef AQ_N
+#error "compile with -DAQ_N=<electrons> -DAQ_A=<atoms>"
+#endif
+
+static int fail(int code, const std::string& m) { return aiqmc_fail(code, m); }
+
+// One thread per (walker b, electron i): t_pro (sum over xyz, Q6), acceptance
+// |exp(lp_i - lp)|^2 t_pro > u, move accepted electrons (VMCmcstep.py:80-106).
+template <typename T, int N>
+__global__ __launch_bounds__(256) void k_accept(T* __restrict__ pos, const T* __restrict__ grad,
+                                                const T* __restrict__ gown, const T* __restrict__ lp,
+                                                const T* __restrict__ lpn, const T* __restrict__ gauss1,
+                                                const T* __restrict__ gauss2, const T* __restrict__ u,
+                                                const double* __restrict__ taueff, int B, double tstep_d,
+                                                uint64_t seed, uint64_t step, int32_t* accept_count) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * N) return;
+  const int b = t / N, i = t - b * N;
+  const T tstep = (T)tstep_d;
+  const T sq = sqrt(tstep);
+  const T te1 = (T)taueff[0], te2 = (T)taueff[1];
+  T z1[3], z2[3];
+  T uu;
+  if (gauss1) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      z1[c] = gauss1[(size_t)b * 3 * N + 3 * i + c];
+      z2[c] = gauss2[((size_t)b * N + i) * 3 + c];
+    }
+    uu = u[(size_t)b * N + i];
+  } else {
+    philox_normal3<T>(seed, step, (uint32_t)(b * N + i), 0u, z1);
+    philox_normal3<T>(seed, step, (uint32_t)(b * N + i), 1u, z2);
+    double uv[4];
+    philox_uniform4(seed, step, (uint32_t)(b * N + i), 2u, uv);
+    uu = (T)(uv[0] - 2.3283064365386963e-10);   // [0,1)
+  }
+  T gmove[3];
+  T tp = T(0);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const T ge = grad[(size_t)b * 3 * N + 3 * i + c] * te1;      // grad_eff  (:60)
+    gmove[c] = ge * tstep + sq * z1[c];                          // g         (:62)
+    const T gn = gown[((size_t)b * N + i) * 3 + c] * te2;        // grad_new_eff (:80)
+    const T g2 = sq * z2[c];                                     // gauss2    (:83)
+    const T fw = g2 * g2;
+    const T bwv = g2 + (ge + gn) * tstep;
+    tp += exp((fw - bwv * bwv) / (T(2) * tstep));                // :84-94
+  }
+  const T e = exp(lpn[(size_t)b * N + i] - lp[b]);
+  const T acc = e * e * tp;                                      // |exp(.)|^2 t_pro  (:100)
+  if (acc > uu) {                                                // :18-25
+#pragma unroll
+    for (int c = 0; c < 3; ++c) pos[(size_t)b * 3 * N + 3 * i + c] += gmove[c];
+    if (accept_count) atomicAdd(&accept_count[b], 1);
+  }
+}
+
+template <int N, int A>
+static void pack_params(const aiqmc_ctx* c, const double* flat, std::vector<double>& out) {
+  using Ly = Lay<N, A>;
+  out.assign(Ly::total, 0.0);
+  const double* p = flat;
+  auto take = [&](int n) {
+    const double* q = p;
+    p += n;
+    return q;
+  };
+  // envelope[i]: alpha, beta, eplion, mu, nu, pi, sigma, xi (sorted keys)
+  for (int i = 0; i < N; ++i) {
+    const double* alpha = take(1);
+    const double* beta = take(A);
+    take(3 * A);   // eplion (unused by envelope.apply)
+    take(A);       // mu
+    take(A);       // nu
+    const double* pi = take(3 * A);
+    const double* sigma = take(3 * A);
+    const double* xi = take(1);
+    out[Ly::env_alpha + i] = alpha[0];
+    out[Ly::env_xi + i] = xi[0];
+    for (int a = 0; a < A; ++a) {
+      out[Ly::env_beta + i * A + a] = beta[a];
+      for (int d = 0; d < 3; ++d) {
+        out[Ly::env_pi + (i * A + a) * 3 + d] = pi[a * 3 + d];
+        out[Ly::env_sigma + (i * A + a) * 3 + d] = sigma[a * 3 + d];
+      }
+    }
+  }
+  const double* jae = take(N * A);
+  for (int k = 0; k < N * A; ++k) out[Ly::jae_b + k] = jae[k];
+  const double* ee_anti = take(c->nanti);
+  const double* ee_par = take(c->npar);
+  for (int q = 0; q < c->npar; ++q) {
+    const int i = c->par[q], j = c->par[c->npar + q];
+    out[Ly::jee_c + i * N + j] = out[Ly::jee_c + j * N + i] = 0.25;
+    out[Ly::jee_a + i * N + j] = out[Ly::jee_a + j * N + i] = ee_par[q];
+  }
+  for (int q = 0; q < c->nanti; ++q) {
+    const int i = c->anti[q], j = c->anti[c->nanti + q];
+    out[Ly::jee_c + i * N + j] = out[Ly::jee_c + j * N + i] = 0.5;
+    out[Ly::jee_a + i * N + j] = out[Ly::jee_a + j * N + i] = ee_anti[q];
+  }
+  // layers.input = {} ; layers.streams[l] = {convolutional{b,w}, double{b,w}, single{b,w}}
+  const int D[3] = {Ly::D0, Ly::D1, Ly::D1};
+  const int Q[3] = {Ly::Q0, Ly::Q1, Ly::Q1};
+  const int cw[3] = {Ly::conv_w0, Ly::conv_w1, Ly::conv_w2};
+  const int cb[3] = {Ly::conv_b0, Ly::conv_b1, Ly::conv_b2};
+  const int sw[3] = {Ly::sng_w0, Ly::sng_w1, Ly::sng_w2};
+  const int sb[3] = {Ly::sng_b0, Ly::sng_b1, Ly::sng_b2};
+  const int dw[2] = {Ly::dbl_w0, Ly::dbl_w1};
+  const int db[2] = {Ly::dbl_b0, Ly::dbl_b1};
+  for (int l = 0; l < 3; ++l) {
+    const double* b = take(N * Q[l]);
+    const double* w = take(N * D[l]);
+    for (int k = 0; k < N * Q[l]; ++k) out[cb[l] + k] = b[k];
+    for (int k = 0; k < N * D[l]; ++k) out[cw[l] + k] = w[k];
+    if (l < 2) {
+      const double* bb = take(NH2);
+      const double* ww = take(NH2 * NH2);
+      for (int k = 0; k < NH2; ++k) out[db[l] + k] = bb[k];
+      for (int k = 0; k < NH2 * NH2; ++k) out[dw[l] + k] = ww[k];
+    }
+    const double* sbp = take(NH);
+    const double* swp = take(Q[l] * NH);
+    for (int k = 0; k < NH; ++k) out[sb[l] + k] = sbp[k];
+    for (int k = 0; k < Q[l] * NH; ++k) out[sw[l] + k] = swp[k];
+  }
+  // layers.streams_y[l].single_Ynlm {b, w}
+  const int yin[3] = {Ly::DY0, NYW, NYW};
+  const int yw[3] = {Ly::y_w0, Ly::y_w1, Ly::y_w2};
+  const int yb[3] = {Ly::y_b0, Ly::y_b1, Ly::y_b2};
+  for (int l = 0; l < 3; ++l) {
+    const double* b = take(NYW);
+    const double* w = take(yin[l] * NYW);
+    for (int k = 0; k < NYW; ++k) out[yb[l] + k] = b[k];
+    for (int k = 0; k < yin[l] * NYW; ++k) out[yw[l] + k] = w[k];
+  }
+  // orbitals[s] {b [2N], w [4][2N]} ; complex = even + i odd (nn.py:456)
+  for (int s = 0; s < 2; ++s) {
+    const double* b = take(2 * N);
+    const double* w = take(NH * 2 * N);
+    for (int col = 0; col < N; ++col) {
+      out[Ly::orb_b + (s * N + col) * 2 + 0] = b[2 * col];
+      out[Ly::orb_b + (s * N + col) * 2 + 1] = b[2 * col + 1];
+      for (int f = 0; f < NH; ++f) {
+        out[Ly::orb_w + ((s * NH + f) * N + col) * 2 + 0] = w[f * 2 * N + 2 * col];
+        out[Ly::orb_w + ((s * NH + f) * N + col) * 2 + 1] = w[f * 2 * N + 2 * col + 1];
+      }
+    }
+  }
+  // y[0].w [6][N], row-normalised (nn.py:449-451)
+  const double* wy = take(NYW * N);
+  for (int m = 0; m < NYW; ++m) {
+    double nrm = 0.0;
+    for (int col = 0; col < N; ++col) nrm += wy[m * N + col] * wy[m * N + col];
+    nrm = std::sqrt(nrm);
+    for (int col = 0; col < N; ++col) out[Ly::wy + m * N + col] = wy[m * N + col] / nrm;
+  }
+  // system constants
+  for (int a = 0; a < A; ++a) {
+    for (int d = 0; d < 3; ++d) out[Ly::atoms + a * 3 + d] = c->atoms[a * 3 + d];
+    out[Ly::charges + a] = c->charges[a];
+    out[Ly::c34 + a] = std::pow(2.0 * c->charges[a], 0.75);
+    out[Ly::c14 + a] = std::pow(2.0 * c->charges[a], 0.25);
+  }
+  double vnn = 0.0;
+  for (int a = 0; a < A; ++a)
+    for (int b = a + 1; b < A; ++b) {
+      double r2 = 0.0;
+      for (int d = 0; d < 3; ++d) {
+        const double t = c->atoms[a * 3 + d] - c->atoms[b * 3 + d];
+        r2 += t * t;
+      }
+      vnn += c->charges[a] * c->charges[b] / std::sqrt(r2);
+    }
+  out[Ly::vnn] = vnn;
+}
+
+template <int N, int A>
+static int set_lds_impl() {
+  const int sizes[4] = {Smem<float, N, false>::bytes, Smem<float, N, true>::bytes, Smem<double, N, false>::bytes,
+                        Smem<double, N, true>::bytes};
+  const void* fns[4] = {(const void*)&k_walker<float, N, A, MODE_GRAD>, (const void*)&k_walker<float, N, A, MODE_LAP>,
+                        (const void*)&k_walker<double, N, A, MODE_GRAD>, (const void*)&k_walker<double, N, A, MODE_LAP>};
+  for (int k = 0; k < 4; ++k) {
+    if (sizes[k] > 65536) {
+      hipError_t e = hipFuncSetAttribute(fns[k], hipFuncAttributeMaxDynamicSharedMemorySize, sizes[k]);
+      if (e != hipSuccess) return fail(AIQMC_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+    }
+  }
+  return 0;
+}
+
+template <int N, int A>
+static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStream_t s) {
+  if (dtype == AIQMC_F32) {
+    if (mode == MODE_LAP)
+      k_walker<float, N, A, MODE_LAP><<<dim3(nconf), dim3(64), Smem<float, N, true>::bytes, s>>>(ka);
+    else
+      k_walker<float, N, A, MODE_GRAD><<<dim3(nconf), dim3(64), Smem<float, N, false>::bytes, s>>>(ka);
+  } else {
+    if (mode == MODE_LAP)
+      k_walker<double, N, A, MODE_LAP><<<dim3(nconf), dim3(64), Smem<double, N, true>::bytes, s>>>(ka);
+    else
+      k_walker<double, N, A, MODE_GRAD><<<dim3(nconf), dim3(64), Smem<double, N, false>::bytes, s>>>(ka);
+  }
+}
+
+template <int N, int A>
+static void accept_impl(int dtype, void* pos, const void* grad, const void* gown, const void* lp, const void* lpn,
+                        const void* g1, const void* g2, const void* u, const double* te, int B, double tstep,
+                        uint64_t seed, uint64_t step, int32_t* acc, hipStream_t s) {
+  const int nt = B * N;
+  const int nb = (nt + 255) / 256;
+  if (dtype == AIQMC_F32)
+    k_accept<float, N><<<dim3(nb), dim3(256), 0, s>>>((float*)pos, (const float*)grad, (const float*)gown, (const float*)lp, (const float*)lpn, (const float*)g1, (const float*)g2, (const float*)u, te, B, tstep, seed, step, acc);
+  else
+    k_accept<double, N><<<dim3(nb), dim3(256), 0, s>>>((double*)pos, (const double*)grad, (const double*)gown, (const double*)lp, (const double*)lpn, (const double*)g1, (const double*)g2, (const double*)u, te, B, tstep, seed, step, acc);
+}
+
+
+#define AQ_CAT2(a, b, c) aiqmc_shape_ops_##a##_##b##c
+#define AQ_CAT(a, b) AQ_CAT2(a, b, )
+bool AQ_CAT(AQ_N, AQ_A)(ShapeOps* ops) {
+  ops->set_lds = &set_lds_impl<AQ_N, AQ_A>;
+  ops->walker = &walker_impl<AQ_N, AQ_A>;
+  ops->accept = &accept_impl<AQ_N, AQ_A>;
+  ops->nkern = Lay<AQ_N, AQ_A>::total;
+  ops->ncanon = &Lay<AQ_N, AQ_A>::canon;
+  ops->pack = &pack_params<AQ_N, AQ_A>;
+  return true;
+}

@@ -1,0 +1,683 @@
+// walker_kernel.h -- one wavefront evaluates log|psi|, its gradient and
+// (MODE == MODE_LAP) its Laplacian for ONE electron configuration of the AIQMC
+// wavefunction (AIQMCrelease3/wavefunction_Ynlm/nn.py:106-553), then the local
+// energy (Energy/hamiltonian.py:236-260, complex_output=False).
+//
+// Derivatives are forward-mode: direction lane (c,e) propagates the first and
+// diagonal-second derivative along x_{e,c} (see jets.h).  Sparsity is used
+// structurally: per-electron quantities (ae features, Ylm stream, envelope,
+// e-n Jastrow) depend on x_e only and are computed as PJ jets by the lanes of
+// electron e; pair quantities h2[k,i] (never mixed across pairs, nn.py:305-309)
+// depend on x_k, x_i only.  Only the mean-field h stream is carried as dense
+// wave-shared DJ jets, stored lane-private in LDS between layers.
+//
+// Determinant derivatives use the low-rank structure of the orbital matrix
+//   A[r,c] = Phi[r,c] * Yt[r,c],   Phi[r,:] = H[r,:] W_{s(r)} + b_{s(r)}  (complex)
+//   Yt[r,c] = env_r * Y[r,c]  (real, depends on x_r only),
+// with B = A^{-1}, Q_f = P_f B, P_f[r,c] = W_{s(r)}[f,c] Yt[r,c]:
+//   d_k log|det A| = sum_{r,f} U[r,f] Re Q_f[r,r] + Re(w.b_e)
+//   d2_k log|det A| = Re[ sum U2 Q_f[r,r] + (2 dPhi_e.Yt' + Phi_e.Yt'') b_e
+//                       - sum_{r,s} S_rs S_sr - 2 sum_{r,f} U z Q_f[r,e] - (w.b_e)^2 ]
+// where U = d_k H, U2 = d2_k H, S = sum_f diag(U_f) Q_f, w = Phi[e,:] * d_k Yt[e,:],
+// z = B^T w, b_e = B[:,e], e = electron of direction k.  The Jastrow factors
+// scale every element (Q11) and enter log|psi| additively.
+#pragma once
+#include "jets.h"
+#include "layout.h"
+
+namespace aq {
+
+constexpr int MODE_GRAD = 1;
+constexpr int MODE_LAP = 2;
+
+struct KArgs {
+  int nconf;
+  int nup;
+  const int* rowsrc;      // [N]: electron feeding determinant row r (up rows then down rows)
+  const void* prm;        // kernel parameter layout (Lay<N,A>)
+  const void* pos;        // direct: [nconf][3N]; proposal: walkers [B][3N]
+  // proposal mode: configuration conf = b*N + i is walker b with electron i moved
+  // by  grad_eff*tstep + sqrt(tstep)*gauss1  (VMCmcstep.py:58-78)
+  int proposal;
+  const void* pgrad;      // [B][3N] grad log|psi| at the walkers
+  const void* gauss1;     // [B][3N] standard normals (host rng) or nullptr (philox)
+  const double* taueff;   // device scalar: limdrift factor of pgrad (VMCmcstep.py:11-14)
+  double tstep;
+  uint64_t seed, step;
+  // outputs (nullable)
+  void* logabs;           // [nconf]
+  void* phase;            // [nconf]
+  void* grad;             // [nconf][3N]
+  void* el;               // [nconf]
+  void* sumsq;            // [nconf] |grad|^2
+  void* gown;             // [nconf][3]  proposal: gradient components of the moved electron
+};
+
+template <typename T, int N, bool LAP>
+struct Smem {
+  static constexpr int NC = LAP ? 2 : 1;
+  static constexpr int xs = 0;
+  static constexpr int hb = 48;
+  static constexpr int yv = hb + N * 4 * NC * 64;
+  static constexpr int ph = yv + N * N;
+  static constexpr int mx = ph + N * N * 2;
+  static constexpr int fac = mx + N * 2 * N * 2;
+  static constexpr int qs = fac + N * 2;
+  static constexpr int end = qs + (LAP ? N * N * 8 : N * 8);
+  static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
+};
+
+template <typename T, int N, int A, bool LAP, int L>
+__device__ __forceinline__ void h_layer(const T* __restrict__ P, const T* xs, T* hb, const PJ<T>* hf,
+                                        int lane, int lc, int er, int le, bool val, bool dir, bool live,
+                                        int nup, T& jd1, T& jd2, T& jv, T& vv) {
+  using Ly = Lay<N, A>;
+  constexpr int NC = LAP ? 2 : 1;
+  constexpr int DIN = (L == 0) ? 4 * A : NH;
+  constexpr int DF = 3 * DIN + 2 * NH2;
+  constexpr int Q = DF / 4;
+  const T* convw = P + (L == 0 ? Ly::conv_w0 : (L == 1 ? Ly::conv_w1 : Ly::conv_w2));
+  const T* convb = P + (L == 0 ? Ly::conv_b0 : (L == 1 ? Ly::conv_b1 : Ly::conv_b2));
+  const T* sngw = P + (L == 0 ? Ly::sng_w0 : (L == 1 ? Ly::sng_w1 : Ly::sng_w2));
+  const T* sngb = P + (L == 0 ? Ly::sng_b0 : (L == 1 ? Ly::sng_b1 : Ly::sng_b2));
+  const int glo[2] = {0, nup};
+  const int ghi[2] = {nup, N};
+  const T ginv[2] = {T(1) / T(nup), T(1) / T(N - nup)};
+  const T SQ2 = T(1.4142135623730951);
+
+  // ---- g1: spin-group means of h (construct_symmetric_features, nn.py:142-150)
+  DJ<T> g1[2][DIN];
+#pragma unroll
+  for (int G = 0; G < 2; ++G) {
+    const bool inG = live && er >= glo[G] && er < ghi[G];
+    if constexpr (L == 0) {
+#pragma unroll
+      for (int m = 0; m < DIN; ++m) {
+        const T S = rowsum16((val && inG) ? hf[m].v : T(0));
+        g1[G][m].d1 = val ? S * ginv[G] : ((dir && inG) ? hf[m].d1 * ginv[G] : T(0));
+        g1[G][m].d2 = (dir && inG) ? hf[m].d2 * ginv[G] : T(0);
+      }
+    } else {
+#pragma unroll
+      for (int m = 0; m < DIN; ++m) g1[G][m] = dj_zero<T>();
+      for (int k = glo[G]; k < ghi[G]; ++k) {
+#pragma unroll
+        for (int m = 0; m < DIN; ++m) {
+          g1[G][m].d1 += hb[((k * 4 + m) * NC + 0) * 64 + lane];
+          if constexpr (LAP) g1[G][m].d2 += hb[((k * 4 + m) * NC + 1) * 64 + lane];
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < DIN; ++m) {
+        g1[G][m].d1 *= ginv[G];
+        g1[G][m].d2 *= ginv[G];
+      }
+    }
+  }
+
+  // ---- column loop: electron i's new h (nn.py:280-311)
+#pragma unroll 1
+  for (int i = 0; i < N; ++i) {
+    // pair (le, i): ee[le,i] = x_i - x_le, r_ee (nn.py:111-115); lane direction is x_{le,lc}
+    const bool diag = (er == i);
+    PJ<T> d[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) d[c] = PJ<T>{xs[i * 3 + c] - xs[le * 3 + c], (lc == c) ? T(-1) : T(0), T(0)};
+    PJ<T> r2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+    r2 = pj_sel(diag, pjc(T(1)), r2);
+    const PJ<T> r = pj_sqrt(r2);
+    PJ<T> p[4];
+    p[0] = pj_sel(diag, pjc(T(0)), r);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) p[1 + c] = pj_sel(diag, pjc(T(0)), d[c]);
+
+    if constexpr (L == 0) {
+      // Pade e-e Jastrow pair term r*cusp/(1+alpha r) (Jastrow.py:51-52) and V_ee (hamiltonian.py:177-187)
+      const T cusp = P[Ly::jee_c + le * N + i];
+      const T al = P[Ly::jee_a + le * N + i];
+      const PJ<T> fj = (cusp * r) / (al * r + T(1));
+      if (dir && !diag) {
+        jd1 += fj.d1;
+        jd2 += fj.d2;
+      }
+      if (val && live && er < i) {
+        jv += fj.v;
+        vv += T(1) / r.v;
+      }
+    }
+    // pair stream: L double layers, tanh + residual (nn.py:305-309)
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const T* dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
+      const T* db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
+      PJ<T> q[4];
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        PJ<T> s = dw[0 * 4 + o] * p[0];
+#pragma unroll
+        for (int m = 1; m < 4; ++m) s = s + dw[m * 4 + o] * p[m];
+        q[o] = pj_tanh(s + db[o]);
+      }
+#pragma unroll
+      for (int o = 0; o < 4; ++o) p[o] = (p[o] + q[o]) / SQ2;
+    }
+    // g2: column means of h2 over spin groups (nn.py:151)
+    DJ<T> g2[2][4];
+#pragma unroll
+    for (int G = 0; G < 2; ++G) {
+      const bool inG = live && er >= glo[G] && er < ghi[G];
+      const bool mp = inG && !diag;
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const T X = val ? (inG ? p[f].v : T(0)) : (mp ? p[f].d1 : T(0));
+        const T S = rowsum16(X);
+        g2[G][f].d1 = val ? S * ginv[G] : ((diag && dir) ? -S * ginv[G] : ((mp && dir) ? p[f].d1 * ginv[G] : T(0)));
+        if constexpr (LAP) {
+          const T S2 = rowsum16((!val && mp) ? p[f].d2 : T(0));
+          g2[G][f].d2 = val ? T(0) : ((diag && dir) ? S2 * ginv[G] : ((mp && dir) ? p[f].d2 * ginv[G] : T(0)));
+        } else {
+          g2[G][f].d2 = T(0);
+        }
+      }
+    }
+    // h_i as wave-shared jets
+    DJ<T> hi[DIN];
+    if constexpr (L == 0) {
+#pragma unroll
+      for (int m = 0; m < DIN; ++m) {
+        const T hv = rdlane(hf[m].v, 48 + i);
+        hi[m].d1 = val ? hv : ((diag && dir) ? hf[m].d1 : T(0));
+        hi[m].d2 = (diag && dir) ? hf[m].d2 : T(0);
+      }
+    } else {
+#pragma unroll
+      for (int m = 0; m < DIN; ++m) {
+        hi[m].d1 = hb[((i * 4 + m) * NC + 0) * 64 + lane];
+        hi[m].d2 = LAP ? hb[((i * 4 + m) * NC + (LAP ? 1 : 0)) * 64 + lane] : T(0);
+      }
+    }
+    // convolutional layer: tanh(mean_4(f * w) + b)  (network_blocks.py:106-116)
+    DJ<T> cq[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      DJ<T> z = dj_zero<T>();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int idx = 4 * q + s;
+        DJ<T> F;
+        if (idx < DIN) F = hi[idx];
+        else if (idx < 2 * DIN) F = g1[0][idx - DIN];
+        else if (idx < 3 * DIN) F = g1[1][idx - 2 * DIN];
+        else if (idx < 3 * DIN + 4) F = g2[0][idx - 3 * DIN];
+        else F = g2[1][idx - 3 * DIN - 4];
+        dj_axpy(z, convw[i * DF + idx] * T(0.25), F);
+      }
+      if (val) z.d1 += convb[i * Q + q];
+      cq[q] = dj_tanh(z, val);
+    }
+    // single linear + tanh + residual (nn.py:296-300)
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      DJ<T> s = dj_zero<T>();
+#pragma unroll
+      for (int q = 0; q < Q; ++q) dj_axpy(s, sngw[q * 4 + f], cq[q]);
+      if (val) s.d1 += sngb[f];
+      s = dj_tanh(s, val);
+      DJ<T> nh;
+      if constexpr (DIN == NH) {
+        nh.d1 = (hi[f].d1 + s.d1) / SQ2;
+        nh.d2 = (hi[f].d2 + s.d2) / SQ2;
+      } else {
+        nh = s;
+      }
+      hb[((i * 4 + f) * NC + 0) * 64 + lane] = nh.d1;
+      if constexpr (LAP) hb[((i * 4 + f) * NC + 1) * 64 + lane] = nh.d2;
+    }
+  }
+}
+
+template <typename T, int N, int A, int MODE>
+__global__ __launch_bounds__(64) void k_walker(KArgs ka) {
+  constexpr bool LAP = (MODE == MODE_LAP);
+  using Ly = Lay<N, A>;
+  using SM = Smem<T, N, LAP>;
+  constexpr int NC = SM::NC;
+  constexpr int N2 = 2 * N;
+  const T* __restrict__ P = (const T*)ka.prm;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  T* sm = (T*)smem_raw;
+  T* xs = sm + SM::xs;
+  T* hb = sm + SM::hb;
+  T* Yv = sm + SM::yv;
+  T* Ph = sm + SM::ph;
+  T* Mx = sm + SM::mx;
+  T* fac = sm + SM::fac;
+  T* Qs = sm + SM::qs;
+
+  const int conf = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int lc = lane >> 4;
+  const int er = lane & 15;
+  const int le = er < N ? er : N - 1;
+  const bool val = (lc == 3);
+  const bool live = er < N;
+  const bool dir = (lc < 3) && live;
+  const int nup = ka.nup;
+  const T tstep = (T)ka.tstep;
+
+  // ------------------------------------------------------------------ positions
+  int pb = conf, pi = -1;
+  if (ka.proposal) {
+    pb = conf / N;
+    pi = conf - pb * N;
+  }
+  if (lane < 3 * N) {
+    T x = ((const T*)ka.pos)[(size_t)pb * 3 * N + lane];
+    if (ka.proposal && lane / 3 == pi) {
+      T z;
+      if (ka.gauss1) {
+        z = ((const T*)ka.gauss1)[(size_t)pb * 3 * N + lane];
+      } else {
+        T g3[3];
+        philox_normal3<T>(ka.seed, ka.step, (uint32_t)(pb * N + pi), 0u, g3);
+        const int c = lane - 3 * pi;
+        z = c == 0 ? g3[0] : (c == 1 ? g3[1] : g3[2]);
+      }
+      const T ge = ((const T*)ka.pgrad)[(size_t)pb * 3 * N + lane] * (T)(*ka.taueff);
+      x = x + (ge * tstep + f_sqrt(tstep) * z);
+    }
+    xs[lane] = x;
+  }
+  __syncthreads();
+
+  // ------------------------------------------------------------------ per-electron stage (lanes of electron le)
+  PJ<T> xe[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) xe[c] = PJ<T>{xs[le * 3 + c], (lc == c) ? T(1) : T(0), T(0)};
+  PJ<T> hf[4 * A];
+  PJ<T> yin[4 * A + 2];
+  PJ<T> ra[A];
+  PJ<T> aev[A][3];
+  PJ<T> hisum = pjc(T(0)), spsum = pjc(T(0));
+  T vv = T(0);
+  {
+    const T PI = T(3.141592653589793);
+    const T c0 = T(0.5) * f_sqrt(T(1) / PI), c1 = f_sqrt(T(3) / (T(4) * PI));
+    const T k15h = T(0.5) * f_sqrt(T(15) / PI), k5q = T(0.25) * f_sqrt(T(5) / PI);
+    const T k15q = T(0.25) * f_sqrt(T(15) / PI), k35 = T(0.25) * f_sqrt(T(35) / (T(2) * PI));
+    const T k105h = T(0.5) * f_sqrt(T(105) / PI), k21 = T(0.25) * f_sqrt(T(21) / (T(2) * PI));
+    const T k7 = T(0.25) * f_sqrt(T(7) / PI), k105q = T(0.25) * f_sqrt(T(105) / PI);
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      PJ<T> ae[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) ae[c] = xe[c] - P[Ly::atoms + a * 3 + c];   // nn.py:111
+      const PJ<T> r = pj_sqrt(ae[0] * ae[0] + ae[1] * ae[1] + ae[2] * ae[2]);   // nn.py:113
+      ra[a] = r;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) aev[a][c] = ae[c];
+      hf[4 * a] = r;                                                       // nn.py:134-136
+#pragma unroll
+      for (int c = 0; c < 3; ++c) hf[4 * a + 1 + c] = ae[c];
+      const PJ<T> x0 = ae[0] / r, x1 = ae[1] / r, x2 = ae[2] / r;          // nn.py:327
+      yin[4 * a + 0] = pjc(c0);                                            // nn.py:164-167
+      yin[4 * a + 1] = c1 * x0;
+      yin[4 * a + 2] = c1 * x1;
+      yin[4 * a + 3] = c1 * x2;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) spsum = spsum + yin[4 * a + m];
+      // nn.py:182-193 with y = r and x[3] -> x[2] (Q3)
+      const PJ<T> y2 = r * r, y3 = y2 * r;
+      const PJ<T> x00 = x0 * x0, x11 = x1 * x1, x22 = x2 * x2;
+      hisum = hisum + k15h * (x0 * x1 / y2);
+      hisum = hisum + k15h * (x1 * x2 / y2);
+      hisum = hisum + k5q * ((T(3) * x22 - y2) / y2);
+      hisum = hisum + k15h * (x0 * x2 / y2);
+      hisum = hisum + k15q * ((x00 - x11) / y2);
+      hisum = hisum + k35 * ((x1 * (T(3) * x00 - x11)) / y3);
+      hisum = hisum + k105h * (x0 * x1 * x2 / y3);
+      hisum = hisum + k21 * ((x1 * (T(5) * x22 - y2)) / y3);
+      hisum = hisum + k7 * ((T(5) * (x22 * x2) - T(3) * x2 * y2) / y3);
+      hisum = hisum + k21 * ((x0 * (T(5) * x22 - y2)) / y3);
+      hisum = hisum + k105q * (((x00 - x11) * x2) / y3);
+      hisum = hisum + k35 * ((x0 * (x00 - T(3) * x11)) / y3);
+      vv += (val && live) ? -P[Ly::charges + a] / r.v : T(0);             // hamiltonian.py:190-198
+    }
+  }
+  yin[4 * A] = hisum / T(12 * A);                                          // nn.py:336-339
+  yin[4 * A + 1] = spsum / T(4 * A);
+  // Ynlm stream (nn.py:313-319, 340-341)
+  PJ<T> yst[NYW];
+  {
+    constexpr int DY0 = Ly::DY0;
+#pragma unroll
+    for (int o = 0; o < NYW; ++o) {
+      PJ<T> s = P[Ly::y_w0 + o] * yin[0];
+#pragma unroll
+      for (int m = 1; m < DY0; ++m) s = s + P[Ly::y_w0 + m * NYW + o] * yin[m];
+      yst[o] = pj_tanh(s + P[Ly::y_b0 + o]);
+      if constexpr (DY0 == NYW) yst[o] = (yin[o] + yst[o]) / T(1.4142135623730951);
+    }
+#pragma unroll
+    for (int l = 1; l < 3; ++l) {
+      const int wo = l == 1 ? Ly::y_w1 : Ly::y_w2;
+      const int bo = l == 1 ? Ly::y_b1 : Ly::y_b2;
+      PJ<T> nx[NYW];
+#pragma unroll
+      for (int o = 0; o < NYW; ++o) {
+        PJ<T> s = P[wo + o] * yst[0];
+#pragma unroll
+        for (int m = 1; m < NYW; ++m) s = s + P[wo + m * NYW + o] * yst[m];
+        nx[o] = pj_tanh(s + P[bo + o]);
+      }
+#pragma unroll
+      for (int o = 0; o < NYW; ++o) yst[o] = (yst[o] + nx[o]) / T(1.4142135623730951);
+    }
+  }
+  // envelope of electron le (envelope.py:26-30, Q1) and e-n Jastrow (Jastrow.py:84-93)
+  PJ<T> env = pjc(T(0)), jae = pjc(T(0));
+  {
+    const T alpha = P[Ly::env_alpha + le], xi = P[Ly::env_xi + le];
+    PJ<T> s1 = pjc(T(0)), s2 = pjc(T(0));
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      const T beta = P[Ly::env_beta + le * A + a];
+      s1 = s1 + alpha * pj_exp(-beta * (ra[a] * ra[a]));
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const T pi_ = P[Ly::env_pi + (le * A + a) * 3 + c];
+        const T sg = P[Ly::env_sigma + (le * A + a) * 3 + c];
+        s2 = s2 + (sg * xi) * pj_exp(-pi_ * aev[a][c]);
+      }
+      const T bj = P[Ly::jae_b + le * A + a];
+      const T c34 = P[Ly::c34 + a], c14 = P[Ly::c14 + a];
+      const PJ<T> ex = pj_exp(-(c14 * bj) * ra[a]);
+      jae = jae + (-c34 * (pjc(T(1)) - ex)) / (T(2) * bj);
+    }
+    env = s1 + s2;
+  }
+  // Yt row of electron le: env * (y . What)   (nn.py:449-452, 479-485)
+  T Yd1[N], Yd2[N];
+#pragma unroll
+  for (int col = 0; col < N; ++col) {
+    PJ<T> s = P[Ly::wy + col] * yst[0];
+#pragma unroll
+    for (int m = 1; m < NYW; ++m) s = s + P[Ly::wy + m * N + col] * yst[m];
+    const PJ<T> yt = env * s;
+    Yd1[col] = yt.d1;
+    Yd2[col] = yt.d2;
+    if (val && live) Yv[er * N + col] = yt.v;
+  }
+  T jd1 = dir ? jae.d1 : T(0);
+  T jd2 = dir ? jae.d2 : T(0);
+  T jv = (val && live) ? jae.v : T(0);
+
+  // ------------------------------------------------------------------ h stream (3 layers)
+  h_layer<T, N, A, LAP, 0>(P, xs, hb, hf, lane, lc, er, le, val, dir, live, nup, jd1, jd2, jv, vv);
+  h_layer<T, N, A, LAP, 1>(P, xs, hb, hf, lane, lc, er, le, val, dir, live, nup, jd1, jd2, jv, vv);
+  h_layer<T, N, A, LAP, 2>(P, xs, hb, hf, lane, lc, er, le, val, dir, live, nup, jd1, jd2, jv, vv);
+  __syncthreads();
+
+  // ------------------------------------------------------------------ orbital matrix A = Phi * Yt, [A | I]
+  const int* rowsrc = ka.rowsrc;
+  for (int idx = lane; idx < N * N; idx += 64) {
+    const int r = idx / N, col = idx - r * N;
+    const int src = rowsrc[r];
+    const int sp = r < nup ? 0 : 1;
+    T re = T(0), im = T(0);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const T hv = hb[((src * 4 + f) * NC + 0) * 64 + 48];
+      re += hv * P[Ly::orb_w + ((sp * 4 + f) * N + col) * 2 + 0];
+      im += hv * P[Ly::orb_w + ((sp * 4 + f) * N + col) * 2 + 1];
+    }
+    re += P[Ly::orb_b + (sp * N + col) * 2 + 0];
+    im += P[Ly::orb_b + (sp * N + col) * 2 + 1];
+    Ph[idx * 2 + 0] = re;
+    Ph[idx * 2 + 1] = im;
+    const T yv = Yv[idx];
+    Mx[(r * N2 + col) * 2 + 0] = re * yv;
+    Mx[(r * N2 + col) * 2 + 1] = im * yv;
+    Mx[(r * N2 + N + col) * 2 + 0] = (r == col) ? T(1) : T(0);
+    Mx[(r * N2 + N + col) * 2 + 1] = T(0);
+  }
+  __syncthreads();
+
+  // ------------------------------------------------------------------ Gauss-Jordan with partial pivoting
+  // (replaces jnp.linalg.slogdet, network_blocks.py:156; pivot = first max |re|+|im| as LAPACK izamax)
+  T logdet = T(0), phr = T(1), phi = T(0);
+  for (int k = 0; k < N; ++k) {
+    T key = T(-1);
+    int kid = lane;
+    if (lane >= k && lane < N) key = f_abs(Mx[(lane * N2 + k) * 2]) + f_abs(Mx[(lane * N2 + k) * 2 + 1]);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const T ok = __shfl_xor(key, off);
+      const int oi = __shfl_xor(kid, off);
+      if (ok > key || (ok == key && oi < kid)) {
+        key = ok;
+        kid = oi;
+      }
+    }
+    const int p = __builtin_amdgcn_readfirstlane(kid);
+    if (p != k) {
+      if (lane < 2 * N2) {
+        const T a = Mx[k * N2 * 2 + lane];
+        const T b = Mx[p * N2 * 2 + lane];
+        Mx[k * N2 * 2 + lane] = b;
+        Mx[p * N2 * 2 + lane] = a;
+      }
+      phr = -phr;
+      phi = -phi;
+    }
+    __syncthreads();
+    const T pr = Mx[(k * N2 + k) * 2], pim = Mx[(k * N2 + k) * 2 + 1];
+    const T mag = f_hypot(pr, pim);
+    logdet += f_log(mag);
+    {
+      const T ur = pr / mag, ui = pim / mag;
+      const T nr = phr * ur - phi * ui, ni = phr * ui + phi * ur;
+      phr = nr;
+      phi = ni;
+    }
+    const T den = pr * pr + pim * pim;
+    const T ir = pr / den, ii = -pim / den;
+    if (lane < N) {
+      fac[lane * 2 + 0] = Mx[(lane * N2 + k) * 2 + 0];
+      fac[lane * 2 + 1] = Mx[(lane * N2 + k) * 2 + 1];
+    }
+    __syncthreads();
+    if (lane < N2) {
+      const T mr = Mx[(k * N2 + lane) * 2], mi = Mx[(k * N2 + lane) * 2 + 1];
+      Mx[(k * N2 + lane) * 2] = mr * ir - mi * ii;
+      Mx[(k * N2 + lane) * 2 + 1] = mr * ii + mi * ir;
+    }
+    __syncthreads();
+    for (int idx = lane; idx < N * N2; idx += 64) {
+      const int j = idx / N2, col = idx - j * N2;
+      if (j != k) {
+        const T fr = fac[j * 2], fi = fac[j * 2 + 1];
+        const T kr = Mx[(k * N2 + col) * 2], ki = Mx[(k * N2 + col) * 2 + 1];
+        Mx[(j * N2 + col) * 2] -= fr * kr - fi * ki;
+        Mx[(j * N2 + col) * 2 + 1] -= fr * ki + fi * kr;
+      }
+    }
+    __syncthreads();
+  }
+#define BINV_RE(c, s) Mx[((c) * N2 + N + (s)) * 2]
+#define BINV_IM(c, s) Mx[((c) * N2 + N + (s)) * 2 + 1]
+
+  // ------------------------------------------------------------------ Q_f = P_f B  (diagonal only for gradients)
+  if constexpr (LAP) {
+    for (int idx = lane; idx < 4 * N * N; idx += 64) {
+      const int f = idx / (N * N);
+      const int rs = idx - f * N * N;
+      const int r = rs / N, s = rs - r * N;
+      const int sp = r < nup ? 0 : 1;
+      T qr = T(0), qi = T(0);
+      for (int c = 0; c < N; ++c) {
+        const T yv = Yv[r * N + c];
+        const T wr = P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2] * yv;
+        const T wi = P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 1] * yv;
+        const T br = BINV_RE(c, s), bi = BINV_IM(c, s);
+        qr += wr * br - wi * bi;
+        qi += wr * bi + wi * br;
+      }
+      Qs[((r * N + s) * 4 + f) * 2] = qr;
+      Qs[((r * N + s) * 4 + f) * 2 + 1] = qi;
+    }
+  } else {
+    if (lane < 4 * N) {
+      const int f = lane / N, r = lane - f * N;
+      const int sp = r < nup ? 0 : 1;
+      T qr = T(0), qi = T(0);
+      for (int c = 0; c < N; ++c) {
+        const T yv = Yv[r * N + c];
+        const T wr = P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2] * yv;
+        const T wi = P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 1] * yv;
+        const T br = BINV_RE(c, r), bi = BINV_IM(c, r);
+        qr += wr * br - wi * bi;
+        qi += wr * bi + wi * br;
+      }
+      Qs[(r * 4 + f) * 2] = qr;
+      Qs[(r * 4 + f) * 2 + 1] = qi;
+    }
+  }
+  __syncthreads();
+  auto qdiag_re = [&](int r, int f) -> T {
+    return LAP ? Qs[((r * N + r) * 4 + f) * 2] : Qs[(r * 4 + f) * 2];
+  };
+
+  // ------------------------------------------------------------------ per-direction contractions
+  // gradient: sum_{r,f} U Re Q_f[r,r] + Re(w . b_e) + Jastrow
+  T g = jd1;
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+    const int src = rowsrc[r];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) g += hb[((src * 4 + f) * NC + 0) * 64 + lane] * qdiag_re(r, f);
+  }
+  T wbr = T(0), wbi = T(0);
+#pragma unroll
+  for (int col = 0; col < N; ++col) {
+    const T pr = Ph[(le * N + col) * 2], pim = Ph[(le * N + col) * 2 + 1];
+    const T wr = pr * Yd1[col], wi = pim * Yd1[col];
+    const T br = BINV_RE(col, le), bi = BINV_IM(col, le);
+    wbr += wr * br - wi * bi;
+    wbi += wr * bi + wi * br;
+  }
+  g += wbr;
+
+  T lap = T(0);
+  if constexpr (LAP) {
+    // t1 = sum U2 Re Q_f[r,r]
+    T t1 = T(0);
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      const int src = rowsrc[r];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) t1 += hb[((src * 4 + f) * NC + 1) * 64 + lane] * qdiag_re(r, f);
+    }
+    // U of row le (this direction's electron row of the matrix)
+    T Ue[4];
+    {
+      const int src = rowsrc[le];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) Ue[f] = hb[((src * 4 + f) * NC + 0) * 64 + lane];
+    }
+    const int spe = le < nup ? 0 : 1;
+    // t2 = Re sum_col (2 dPhi[e,col] Yt'[col] + Phi[e,col] Yt''[col]) B[col,e]
+    T t2 = T(0);
+#pragma unroll
+    for (int col = 0; col < N; ++col) {
+      T dpr = T(0), dpi = T(0);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        dpr += Ue[f] * P[Ly::orb_w + ((spe * 4 + f) * N + col) * 2];
+        dpi += Ue[f] * P[Ly::orb_w + ((spe * 4 + f) * N + col) * 2 + 1];
+      }
+      const T pr = Ph[(le * N + col) * 2], pim = Ph[(le * N + col) * 2 + 1];
+      const T xr = T(2) * dpr * Yd1[col] + pr * Yd2[col];
+      const T xi = T(2) * dpi * Yd1[col] + pim * Yd2[col];
+      t2 += xr * BINV_RE(col, le) - xi * BINV_IM(col, le);
+    }
+    // cross = Re sum_r z[r] sum_f U[r,f] Q_f[r,e]  with z = B^T w ;  ss = Re sum_{r,s} S_rs S_sr
+    T cross = T(0), ss = T(0);
+#pragma unroll 1
+    for (int r = 0; r < N; ++r) {
+      T ur[4];
+      {
+        const int src = rowsrc[r];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) ur[f] = hb[((src * 4 + f) * NC + 0) * 64 + lane];
+      }
+      T zr = T(0), zi = T(0);
+#pragma unroll
+      for (int col = 0; col < N; ++col) {
+        const T pr = Ph[(le * N + col) * 2], pim = Ph[(le * N + col) * 2 + 1];
+        const T wr = pr * Yd1[col], wi = pim * Yd1[col];
+        const T br = BINV_RE(col, r), bi = BINV_IM(col, r);
+        zr += br * wr - bi * wi;
+        zi += br * wi + bi * wr;
+      }
+      {
+        T sr = T(0), si = T(0);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          sr += ur[f] * Qs[((r * N + le) * 4 + f) * 2];
+          si += ur[f] * Qs[((r * N + le) * 4 + f) * 2 + 1];
+        }
+        cross += zr * sr - zi * si;
+      }
+      {
+        T sr = T(0), si = T(0);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          sr += ur[f] * Qs[((r * N + r) * 4 + f) * 2];
+          si += ur[f] * Qs[((r * N + r) * 4 + f) * 2 + 1];
+        }
+        ss += sr * sr - si * si;
+      }
+#pragma unroll 1
+      for (int s = r + 1; s < N; ++s) {
+        const int srcs = rowsrc[s];
+        T ar = T(0), ai = T(0), br = T(0), bi = T(0);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const T us = hb[((srcs * 4 + f) * NC + 0) * 64 + lane];
+          ar += ur[f] * Qs[((r * N + s) * 4 + f) * 2];
+          ai += ur[f] * Qs[((r * N + s) * 4 + f) * 2 + 1];
+          br += us * Qs[((s * N + r) * 4 + f) * 2];
+          bi += us * Qs[((s * N + r) * 4 + f) * 2 + 1];
+        }
+        ss += T(2) * (ar * br - ai * bi);
+      }
+    }
+    lap = t1 + t2 - (ss + T(2) * cross + (wbr * wbr - wbi * wbi)) + jd2;
+  }
+#undef BINV_RE
+#undef BINV_IM
+
+  // ------------------------------------------------------------------ reductions + outputs
+  const T gd = dir ? g : T(0);
+  const T sumsq = wave_sum(gd * gd);
+  const T lpsi = logdet + wave_sum(jv);
+  if (ka.grad && dir) ((T*)ka.grad)[(size_t)conf * 3 * N + 3 * le + lc] = g;
+  if (ka.gown && dir && le == pi) ((T*)ka.gown)[(size_t)conf * 3 + lc] = g;
+  T el = T(0);
+  if constexpr (LAP) {
+    const T kin = T(-0.5) * wave_sum(dir ? (lap + g * g) : T(0));    // hamiltonian.py:126-127
+    const T pot = wave_sum(vv) + P[Ly::vnn];
+    el = pot + kin;
+  }
+  if (lane == 0) {
+    if (ka.logabs) ((T*)ka.logabs)[conf] = lpsi;
+    if (ka.phase) ((T*)ka.phase)[conf] = f_atan2(phi, phr);
+    if (ka.sumsq) ((T*)ka.sumsq)[conf] = sumsq;
+    if constexpr (LAP) {
+      if (ka.el) ((T*)ka.el)[conf] = el;
+    }
+  }
+}
+
+}  // namespace aq

@@ -1,0 +1,118 @@
+/*
+ * aiqmc.h -- C-ABI of the MI355X-native AIQMC VMC inner loop.
+ *
+ * The reference (Yongda1/AIQMC, AIQMCrelease3) is pure Python/JAX and has no
+ * FFI; the entry points below replace the JAX-traced hot path one for one:
+ *
+ *   aiqmc_logpsi        <- network.apply / signed_network, vmapped
+ *                          (AIQMCrelease3/wavefunction_Ynlm/nn.py:545-551,
+ *                           network_blocks.py:161-206)
+ *   aiqmc_logpsi_grad   <- vmap(jax.grad(logabs_f))   (VMC/VMCmcstep.py:41-53)
+ *   aiqmc_local_energy  <- vmap(hamiltonian.local_energy(...)) with
+ *                          complex_output=False (Energy/hamiltonian.py:236-260,
+ *                          kinetic part :77-132)
+ *   aiqmc_mc_step       <- VMCmcstep.main_monte_carlo(...) -> mc_step
+ *                          (VMC/VMCmcstep.py:121-140, walkers_update :28-111)
+ *   aiqmc_set_params    <- the params pytree passed to all of the above;
+ *                          `flat` is its jax.tree_util.tree_flatten order
+ *                          (dict keys sorted, lists in order, C-order leaves),
+ *                          i.e. jax.flatten_util.ravel_pytree(params)[0].
+ *
+ * Conventions: every array pointer passed to a compute entry point is a DEVICE
+ * pointer (HIP) of the context's dtype (float for AIQMC_F32, double for
+ * AIQMC_F64); `stream` is a hipStream_t (NULL = default stream).  Host
+ * pointers appear only in aiqmc_cfg and aiqmc_set_params.  Functions return
+ * 0 on success and a negative AIQMC_E* code on failure; the message is in
+ * aiqmc_last_error() (thread-local).  No C++ exception crosses the ABI.
+ * A context is bound to one device and is not re-entrant.
+ */
+#ifndef AIQMC_H_
+#define AIQMC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AIQMC_F32 0
+#define AIQMC_F64 1
+
+#define AIQMC_OK 0
+#define AIQMC_EINVAL (-1)
+#define AIQMC_EUNSUPPORTED (-2)
+#define AIQMC_EHIP (-3)
+#define AIQMC_ESTATE (-4)
+
+/* rng_mode of aiqmc_mc_step */
+#define AIQMC_RNG_HOST 0    /* gauss1/gauss2/u supplied by the caller (parity mode) */
+#define AIQMC_RNG_PHILOX 1  /* drawn on device from (seed, offset)                 */
+
+typedef struct aiqmc_ctx aiqmc_ctx;
+
+/* System + network configuration (make_ai_net arguments, nn.py:511-526). */
+typedef struct aiqmc_cfg {
+  int32_t nelectrons;            /* N  (2 <= N <= 16)                          */
+  int32_t natoms;                /* A                                          */
+  int32_t nspins[2];             /* (n_up, n_down); both > 0                   */
+  int32_t dtype;                 /* AIQMC_F32 | AIQMC_F64                      */
+  int32_t device;                /* HIP device ordinal                         */
+  const double* atoms;           /* [A*3] bohr                                 */
+  const double* charges;         /* [A]   (Jastrow e-n + potential charges)    */
+  const int32_t* spin_up_indices;   /* [n_up]   spin_indices.py:38-45          */
+  const int32_t* spin_down_indices; /* [n_down]                                */
+  const int32_t* parallel_indices;  /* [2*n_parallel] row-major (2,n_par)      */
+  int32_t n_parallel;               /* spin_indices.py:5-19                    */
+  const int32_t* antiparallel_indices; /* [2*n_antiparallel]                   */
+  int32_t n_antiparallel;
+  int32_t hidden_dims[3][2];     /* must be ((4,4),(4,4),(4,4)) (nn.py:525)   */
+  int32_t hidden_dims_ynlm[3];   /* must be (6,6,6)             (nn.py:526)   */
+} aiqmc_cfg;
+
+int aiqmc_create(const aiqmc_cfg* cfg, aiqmc_ctx** out);
+int aiqmc_destroy(aiqmc_ctx* ctx);
+
+/* Number of doubles aiqmc_set_params expects (2381 for N2 with defaults). */
+int64_t aiqmc_param_count(const aiqmc_ctx* ctx);
+
+/* flat: HOST pointer, `n` doubles in tree_flatten order. Synchronous upload. */
+int aiqmc_set_params(aiqmc_ctx* ctx, const double* flat, int64_t n, void* stream);
+
+/* pos[B*3N] -> logabs[B], phase[B] (phase may be NULL). */
+int aiqmc_logpsi(aiqmc_ctx* ctx, const void* pos, int32_t B, void* logabs, void* phase,
+                 void* stream);
+
+/* pos[B*3N] -> logabs[B] (may be NULL), grad[B*3N] = d log|psi| / d pos. */
+int aiqmc_logpsi_grad(aiqmc_ctx* ctx, const void* pos, int32_t B, void* logabs, void* grad,
+                      void* stream);
+
+/* pos[B*3N] -> e_l[B]; logabs[B] and grad[B*3N] optional (NULL to skip). */
+int aiqmc_local_energy(aiqmc_ctx* ctx, const void* pos, int32_t B, void* e_l, void* logabs,
+                       void* grad, void* stream);
+
+/* nsteps drift-diffusion Metropolis steps on pos_inout[B*3N] (in place; the
+ * donate_argnums=1 analogue).  B is the per-device batch: limdrift's v2 is
+ * summed over exactly these B walkers (VMCmcstep.py:12).
+ * AIQMC_RNG_HOST: gauss1[nsteps*B*3N] and gauss2[nsteps*B*N*3] standard
+ * normals (gauss2 = the electron-diagonal blocks of the reference's
+ * [B,N,3N] draw, the only entries it reads, VMCmcstep.py:87-94) and
+ * u[nsteps*B*N] uniforms in [0,1).  AIQMC_RNG_PHILOX: the three may be NULL;
+ * draws come from Philox4x32-10 keyed by seed, counter offset+step.
+ * accept_out (optional, int32[B]) accumulates accepted single-electron moves. */
+int aiqmc_mc_step(aiqmc_ctx* ctx, void* pos_inout, int32_t B, int32_t nsteps, double tstep,
+                  int32_t rng_mode, const void* gauss1, const void* gauss2, const void* u,
+                  uint64_t seed, uint64_t offset, int32_t* accept_out, void* stream);
+
+/* Bytes of device workspace the context holds (for memory planning). */
+int64_t aiqmc_workspace_bytes(const aiqmc_ctx* ctx);
+
+const char* aiqmc_last_error(void);
+
+/* Compile-time list of supported (N, A) shapes, as "N:A,N:A,...". */
+const char* aiqmc_supported_shapes(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AIQMC_H_ */
