@@ -25,7 +25,12 @@ EXPORTED_SYMBOLS = (
     "aiqmc_create", "aiqmc_destroy", "aiqmc_param_count", "aiqmc_set_params",
     "aiqmc_logpsi", "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_mc_step",
     "aiqmc_workspace_bytes", "aiqmc_last_error", "aiqmc_supported_shapes",
+    "aiqmc_profile_enable", "aiqmc_profile_read",
 )
+
+PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
+PROF_MC_WALKER = 1     # walker gradient launches of aiqmc_mc_step
+PROF_LOCAL_ENERGY = 2  # aiqmc_local_energy launches
 
 
 class AiqmcCfg(ctypes.Structure):
@@ -74,10 +79,13 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_local_energy.argtypes = [vp, vp, i32, vp, vp, vp, vp]
     lib.aiqmc_mc_step.argtypes = [vp, vp, i32, i32, ctypes.c_double, i32, vp, vp, vp,
                                   ctypes.c_uint64, ctypes.c_uint64, vp, vp]
+    lib.aiqmc_profile_enable.argtypes = [vp, i32]
+    lib.aiqmc_profile_read.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64)]
     lib.aiqmc_last_error.restype = ctypes.c_char_p
     lib.aiqmc_supported_shapes.restype = ctypes.c_char_p
     for name in ("aiqmc_create", "aiqmc_destroy", "aiqmc_set_params", "aiqmc_logpsi",
-                 "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_mc_step"):
+                 "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_mc_step", "aiqmc_profile_enable",
+                 "aiqmc_profile_read"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib
@@ -165,6 +173,21 @@ class Context:
             except Exception:
                 pass
             self._h = None
+
+    # -- kernel timing (HIP events on the launch stream) -------------------
+    def profile(self, on: bool = True):
+        check(self._lib.aiqmc_profile_enable(self._h, 1 if on else 0), "aiqmc_profile_enable")
+
+    def profile_read(self, slot: int):
+        """(summed kernel ms, launches) recorded in `slot` since the last read."""
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        check(self._lib.aiqmc_profile_read(self._h, int(slot), ctypes.byref(ms), ctypes.byref(n)),
+              "aiqmc_profile_read")
+        return ms.value, n.value
+
+    def workspace_bytes(self) -> int:
+        return int(self._lib.aiqmc_workspace_bytes(self._h))
 
     # -- helpers ---------------------------------------------------------
     def _pos(self, pos: torch.Tensor) -> torch.Tensor:

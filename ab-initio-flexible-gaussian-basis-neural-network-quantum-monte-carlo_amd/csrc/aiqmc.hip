@@ -64,6 +64,35 @@ static bool shape_ops(int N, int A, ShapeOps* ops) {
   return false;
 }
 
+static hipEvent_t ev_get(aiqmc_ctx* c) {
+  if (!c->ev_free.empty()) {
+    hipEvent_t e = c->ev_free.back();
+    c->ev_free.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Launch `fn` on stream s; when profiling, bracket it with a pair of events in `slot`.
+template <typename F>
+static void timed(aiqmc_ctx* c, int slot, hipStream_t s, F&& fn) {
+  if (!c->prof) {
+    fn();
+    return;
+  }
+  hipEvent_t a = ev_get(c), b = ev_get(c);
+  if (!a || !b) {
+    fn();
+    return;
+  }
+  (void)hipEventRecord(a, s);
+  fn();
+  (void)hipEventRecord(b, s);
+  c->ev_used[slot].push_back({a, b});
+}
+
 static void free_ws(aiqmc_ctx* c) {
   void* ps[] = {c->d_grad, c->d_lp, c->d_sq, c->d_lpn, c->d_gown, c->d_sqn, c->d_taueff};
   for (void* p : ps)
@@ -181,6 +210,12 @@ int aiqmc_destroy(aiqmc_ctx* c) {
   if (!c) return AIQMC_OK;
   (void)hipSetDevice(c->device);
   free_ws(c);
+  for (auto& v : c->ev_used)
+    for (auto& p : v) {
+      (void)hipEventDestroy(p.first);
+      (void)hipEventDestroy(p.second);
+    }
+  for (hipEvent_t e : c->ev_free) (void)hipEventDestroy(e);
   if (c->d_prm) (void)hipFree(c->d_prm);
   if (c->d_rowsrc) (void)hipFree(c->d_rowsrc);
   delete c;
@@ -276,7 +311,7 @@ int aiqmc_local_energy(aiqmc_ctx* c, const void* pos, int32_t B, void* e_l, void
   ka.el = e_l;
   ka.logabs = logabs;
   ka.grad = grad;
-  ops.walker(c->dtype, MODE_LAP, ka, B, (hipStream_t)stream);
+  timed(c, 2, (hipStream_t)stream, [&] { ops.walker(c->dtype, MODE_LAP, ka, B, (hipStream_t)stream); });
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
 }
@@ -312,7 +347,7 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
     ka.logabs = c->d_lp;
     ka.grad = c->d_grad;
     ka.sumsq = c->d_sq;
-    ops.walker(c->dtype, MODE_GRAD, ka, B, s);
+    timed(c, 1, s, [&] { ops.walker(c->dtype, MODE_GRAD, ka, B, s); });
     // (2) limdrift factor over the device batch (:60)
     if (c->dtype == AIQMC_F32)
       k_taueff<float><<<dim3(1), dim3(256), 0, s>>>((const float*)c->d_sq, B, tstep, c->d_taueff);
@@ -332,7 +367,7 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
     kp.logabs = c->d_lpn;
     kp.gown = c->d_gown;
     kp.sumsq = c->d_sqn;
-    ops.walker(c->dtype, MODE_GRAD, kp, B * N, s);
+    timed(c, 0, s, [&] { ops.walker(c->dtype, MODE_GRAD, kp, B * N, s); });
     // (4) limdrift factor of the proposal gradients over all B*N*3N entries (:80)
     if (c->dtype == AIQMC_F32)
       k_taueff<float><<<dim3(1), dim3(256), 0, s>>>((const float*)c->d_sqn, B * N, tstep,
@@ -345,6 +380,31 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
                accept_out, s);
   }
   HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_profile_enable(aiqmc_ctx* c, int32_t on) {
+  if (!c) return fail(AIQMC_EINVAL, "null context");
+  c->prof = on != 0;
+  return AIQMC_OK;
+}
+
+int aiqmc_profile_read(aiqmc_ctx* c, int32_t slot, double* total_ms, int64_t* launches) {
+  if (!c || slot < 0 || slot >= AIQMC_PROF_SLOTS || !total_ms || !launches) return fail(AIQMC_EINVAL, "bad argument");
+  double tot = 0.0;
+  int64_t n = 0;
+  for (auto& p : c->ev_used[slot]) {
+    HIPCHK(hipEventSynchronize(p.second));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, p.first, p.second));
+    tot += ms;
+    ++n;
+    c->ev_free.push_back(p.first);
+    c->ev_free.push_back(p.second);
+  }
+  c->ev_used[slot].clear();
+  *total_ms = tot;
+  *launches = n;
   return AIQMC_OK;
 }
 

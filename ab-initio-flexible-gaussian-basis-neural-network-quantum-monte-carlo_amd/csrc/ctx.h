@@ -15,6 +15,8 @@
 
 int aiqmc_fail(int code, const std::string& msg);
 using aq::KArgs;
+#include <utility>
+#define AIQMC_PROF_SLOTS 3
 
 struct aiqmc_ctx {
   int N = 0, A = 0, nup = 0, ndn = 0, dtype = 0, device = 0;
@@ -30,6 +32,10 @@ struct aiqmc_ctx {
        *d_sqn = nullptr;
   double* d_taueff = nullptr;
   int64_t ws_bytes = 0;
+  // optional per-kernel HIP-event timing (aiqmc_profile_*): slot -> recorded (start, stop) pairs
+  bool prof = false;
+  std::vector<hipEvent_t> ev_free;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used[AIQMC_PROF_SLOTS];
 };
 
 struct ShapeOps {

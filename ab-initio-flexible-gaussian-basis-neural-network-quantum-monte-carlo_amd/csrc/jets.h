@@ -25,17 +25,31 @@
 
 namespace aq {
 
+// Scalar math.  float uses the hardware approximations (v_sqrt_f32, v_rcp_f32,
+// v_exp_f32: ~1 ulp), which is well inside the fp32 parity tolerance of the
+// reference's own float32 arithmetic; double keeps the correctly rounded
+// library functions (the fp64 parity mode).
 template <typename T> __device__ __forceinline__ T f_sqrt(T x);
-template <> __device__ __forceinline__ float f_sqrt(float x) { return sqrtf(x); }
+template <> __device__ __forceinline__ float f_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 template <> __device__ __forceinline__ double f_sqrt(double x) { return sqrt(x); }
+template <typename T> __device__ __forceinline__ T f_rcp(T x);
+template <> __device__ __forceinline__ float f_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+template <> __device__ __forceinline__ double f_rcp(double x) { return 1.0 / x; }
+template <typename T> __device__ __forceinline__ T f_div(T a, T b);
+template <> __device__ __forceinline__ float f_div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+template <> __device__ __forceinline__ double f_div(double a, double b) { return a / b; }
 template <typename T> __device__ __forceinline__ T f_exp(T x);
-template <> __device__ __forceinline__ float f_exp(float x) { return expf(x); }
+template <> __device__ __forceinline__ float f_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 template <> __device__ __forceinline__ double f_exp(double x) { return exp(x); }
 template <typename T> __device__ __forceinline__ T f_log(T x);
 template <> __device__ __forceinline__ float f_log(float x) { return logf(x); }
 template <> __device__ __forceinline__ double f_log(double x) { return log(x); }
+// tanh(x) = 1 - 2/(1 + e^{2x}); saturates correctly at +-inf (abs. error ~1e-7 in float)
 template <typename T> __device__ __forceinline__ T f_tanh(T x);
-template <> __device__ __forceinline__ float f_tanh(float x) { return tanhf(x); }
+template <> __device__ __forceinline__ float f_tanh(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + e);
+}
 template <> __device__ __forceinline__ double f_tanh(double x) { return tanh(x); }
 template <typename T> __device__ __forceinline__ T f_abs(T x);
 template <> __device__ __forceinline__ float f_abs(float x) { return fabsf(x); }
@@ -68,6 +82,9 @@ template <typename T> __device__ __forceinline__ PJ<T> operator*(PJ<T> a, PJ<T> 
 template <typename T> __device__ __forceinline__ PJ<T> operator*(T s, PJ<T> a) {
   return PJ<T>{s * a.v, s * a.d1, s * a.d2};
 }
+template <typename T> __device__ __forceinline__ PJ<T> operator*(PJ<T> a, T s) {
+  return PJ<T>{s * a.v, s * a.d1, s * a.d2};
+}
 template <typename T> __device__ __forceinline__ PJ<T> operator+(PJ<T> a, T s) {
   return PJ<T>{a.v + s, a.d1, a.d2};
 }
@@ -76,18 +93,19 @@ template <typename T> __device__ __forceinline__ PJ<T> operator-(PJ<T> a, T s) {
 }
 // a / b   (a = q b  =>  q' = (a' - q b')/b,  q'' = (a'' - 2 q' b' - q b'')/b)
 template <typename T> __device__ __forceinline__ PJ<T> operator/(PJ<T> a, PJ<T> b) {
-  const T q = a.v / b.v;
-  const T ib = T(1) / b.v;
+  const T ib = f_rcp(b.v);
+  const T q = f_div(a.v, b.v);
   const T q1 = (a.d1 - q * b.d1) * ib;
   const T q2 = (a.d2 - T(2) * q1 * b.d1 - q * b.d2) * ib;
   return PJ<T>{q, q1, q2};
 }
 template <typename T> __device__ __forceinline__ PJ<T> operator/(PJ<T> a, T s) {
-  return PJ<T>{a.v / s, a.d1 / s, a.d2 / s};
+  const T is = f_rcp(s);
+  return PJ<T>{f_div(a.v, s), a.d1 * is, a.d2 * is};
 }
 template <typename T> __device__ __forceinline__ PJ<T> pj_sqrt(PJ<T> a) {
   const T s = f_sqrt(a.v);
-  const T h = T(0.5) / s;
+  const T h = T(0.5) * f_rcp(s);
   const T s1 = a.d1 * h;
   return PJ<T>{s, s1, (a.d2 - T(2) * s1 * s1) * h};
 }
@@ -137,6 +155,18 @@ template <typename T> __device__ __forceinline__ T rowsum16(T x) {
   x += dpp<0x141>(x);
   x += dpp<0x140>(x);
   return x;
+}
+
+// K independent row sums, interleaved so the DPP read-after-write hazards overlap.
+template <typename T, int K> __device__ __forceinline__ void rowsum16_multi(T* x) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) x[k] += dpp<0xB1>(x[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) x[k] += dpp<0x4E>(x[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) x[k] += dpp<0x141>(x[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) x[k] += dpp<0x140>(x[k]);
 }
 
 // Sum over all 64 lanes, uniform result.

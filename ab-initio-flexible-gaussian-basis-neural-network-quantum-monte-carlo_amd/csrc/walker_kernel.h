@@ -83,7 +83,7 @@ __device__ __forceinline__ void h_layer(const T* __restrict__ P, const T* xs, T*
   const int glo[2] = {0, nup};
   const int ghi[2] = {nup, N};
   const T ginv[2] = {T(1) / T(nup), T(1) / T(N - nup)};
-  const T SQ2 = T(1.4142135623730951);
+  const T RSQ2 = T(0.70710678118654752);  // residual (x+y)/sqrt(2), nn.py:284
 
   // ---- g1: spin-group means of h (construct_symmetric_features, nn.py:142-150)
   DJ<T> g1[2][DIN];
@@ -119,7 +119,9 @@ __device__ __forceinline__ void h_layer(const T* __restrict__ P, const T* xs, T*
 #pragma unroll 1
   for (int i = 0; i < N; ++i) {
     // pair (le, i): ee[le,i] = x_i - x_le, r_ee (nn.py:111-115); lane direction is x_{le,lc}
-    const bool diag = (er == i);
+    // dead lanes (er >= N) compute the clamped pair (N-1, i) and treat it as diagonal when i == N-1,
+    // so no lane ever evaluates sqrt'(0)
+    const bool diag = (le == i);
     PJ<T> d[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) d[c] = PJ<T>{xs[i * 3 + c] - xs[le * 3 + c], (lc == c) ? T(-1) : T(0), T(0)};
@@ -136,14 +138,12 @@ __device__ __forceinline__ void h_layer(const T* __restrict__ P, const T* xs, T*
       const T cusp = P[Ly::jee_c + le * N + i];
       const T al = P[Ly::jee_a + le * N + i];
       const PJ<T> fj = (cusp * r) / (al * r + T(1));
-      if (dir && !diag) {
-        jd1 += fj.d1;
-        jd2 += fj.d2;
-      }
-      if (val && live && er < i) {
-        jv += fj.v;
-        vv += T(1) / r.v;
-      }
+      const bool pd = dir && !diag;
+      jd1 += pd ? fj.d1 : T(0);
+      jd2 += pd ? fj.d2 : T(0);
+      const bool pv = val && live && er < i;
+      jv += pv ? fj.v : T(0);
+      vv += pv ? f_rcp(r.v) : T(0);
     }
     // pair stream: L double layers, tanh + residual (nn.py:305-309)
 #pragma unroll
@@ -159,35 +159,48 @@ __device__ __forceinline__ void h_layer(const T* __restrict__ P, const T* xs, T*
         q[o] = pj_tanh(s + db[o]);
       }
 #pragma unroll
-      for (int o = 0; o < 4; ++o) p[o] = (p[o] + q[o]) / SQ2;
+      for (int o = 0; o < 4; ++o) p[o] = (p[o] + q[o]) * RSQ2;
     }
-    // g2: column means of h2 over spin groups (nn.py:151)
+    // g2: column means of h2 over spin groups (nn.py:151); 8 (16) independent row sums interleaved
     DJ<T> g2[2][4];
+    {
+      T X[8], X2[8];
+      bool inGs[2], mps[2];
 #pragma unroll
-    for (int G = 0; G < 2; ++G) {
-      const bool inG = live && er >= glo[G] && er < ghi[G];
-      const bool mp = inG && !diag;
+      for (int G = 0; G < 2; ++G) {
+        inGs[G] = live && er >= glo[G] && er < ghi[G];
+        mps[G] = inGs[G] && !diag;
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        const T X = val ? (inG ? p[f].v : T(0)) : (mp ? p[f].d1 : T(0));
-        const T S = rowsum16(X);
-        g2[G][f].d1 = val ? S * ginv[G] : ((diag && dir) ? -S * ginv[G] : ((mp && dir) ? p[f].d1 * ginv[G] : T(0)));
-        if constexpr (LAP) {
-          const T S2 = rowsum16((!val && mp) ? p[f].d2 : T(0));
-          g2[G][f].d2 = val ? T(0) : ((diag && dir) ? S2 * ginv[G] : ((mp && dir) ? p[f].d2 * ginv[G] : T(0)));
-        } else {
-          g2[G][f].d2 = T(0);
+        for (int f = 0; f < 4; ++f) {
+          X[G * 4 + f] = val ? (inGs[G] ? p[f].v : T(0)) : (mps[G] ? p[f].d1 : T(0));
+          X2[G * 4 + f] = (!val && mps[G]) ? p[f].d2 : T(0);
+        }
+      }
+      rowsum16_multi<T, 8>(X);
+      if constexpr (LAP) rowsum16_multi<T, 8>(X2);
+      // d1 = cS * S + cP * p.d1  (value row: S/|G|; electron i's lanes: -S/|G|; other members: p.d1/|G|)
+#pragma unroll
+      for (int G = 0; G < 2; ++G) {
+        const T cS = val ? ginv[G] : ((diag && dir) ? -ginv[G] : T(0));
+        const T cS2 = (diag && dir) ? ginv[G] : T(0);
+        const T cP = (mps[G] && dir) ? ginv[G] : T(0);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          g2[G][f].d1 = cS * X[G * 4 + f] + cP * p[f].d1;
+          g2[G][f].d2 = LAP ? (cS2 * X2[G * 4 + f] + cP * p[f].d2) : T(0);
         }
       }
     }
     // h_i as wave-shared jets
     DJ<T> hi[DIN];
     if constexpr (L == 0) {
+      const T cD = (diag && dir) ? T(1) : T(0);
+      const T cV = val ? T(1) : T(0);
 #pragma unroll
       for (int m = 0; m < DIN; ++m) {
         const T hv = rdlane(hf[m].v, 48 + i);
-        hi[m].d1 = val ? hv : ((diag && dir) ? hf[m].d1 : T(0));
-        hi[m].d2 = (diag && dir) ? hf[m].d2 : T(0);
+        hi[m].d1 = cD * hf[m].d1 + cV * hv;
+        hi[m].d2 = cD * hf[m].d2;
       }
     } else {
 #pragma unroll
@@ -212,7 +225,8 @@ __device__ __forceinline__ void h_layer(const T* __restrict__ P, const T* xs, T*
         else F = g2[1][idx - 3 * DIN - 4];
         dj_axpy(z, convw[i * DF + idx] * T(0.25), F);
       }
-      if (val) z.d1 += convb[i * Q + q];
+      const T bq = convb[i * Q + q];
+      z.d1 += val ? bq : T(0);
       cq[q] = dj_tanh(z, val);
     }
     // single linear + tanh + residual (nn.py:296-300)
@@ -221,12 +235,13 @@ __device__ __forceinline__ void h_layer(const T* __restrict__ P, const T* xs, T*
       DJ<T> s = dj_zero<T>();
 #pragma unroll
       for (int q = 0; q < Q; ++q) dj_axpy(s, sngw[q * 4 + f], cq[q]);
-      if (val) s.d1 += sngb[f];
+      const T bf = sngb[f];
+      s.d1 += val ? bf : T(0);
       s = dj_tanh(s, val);
       DJ<T> nh;
       if constexpr (DIN == NH) {
-        nh.d1 = (hi[f].d1 + s.d1) / SQ2;
-        nh.d2 = (hi[f].d2 + s.d2) / SQ2;
+        nh.d1 = (hi[f].d1 + s.d1) * RSQ2;
+        nh.d2 = (hi[f].d2 + s.d2) * RSQ2;
       } else {
         nh = s;
       }
@@ -356,7 +371,7 @@ __global__ __launch_bounds__(64) void k_walker(KArgs ka) {
 #pragma unroll
       for (int m = 1; m < DY0; ++m) s = s + P[Ly::y_w0 + m * NYW + o] * yin[m];
       yst[o] = pj_tanh(s + P[Ly::y_b0 + o]);
-      if constexpr (DY0 == NYW) yst[o] = (yin[o] + yst[o]) / T(1.4142135623730951);
+      if constexpr (DY0 == NYW) yst[o] = T(0.70710678118654752) * (yin[o] + yst[o]);
     }
 #pragma unroll
     for (int l = 1; l < 3; ++l) {
@@ -371,7 +386,7 @@ __global__ __launch_bounds__(64) void k_walker(KArgs ka) {
         nx[o] = pj_tanh(s + P[bo + o]);
       }
 #pragma unroll
-      for (int o = 0; o < NYW; ++o) yst[o] = (yst[o] + nx[o]) / T(1.4142135623730951);
+      for (int o = 0; o < NYW; ++o) yst[o] = T(0.70710678118654752) * (yst[o] + nx[o]);
     }
   }
   // envelope of electron le (envelope.py:26-30, Q1) and e-n Jastrow (Jastrow.py:84-93)

@@ -1,0 +1,247 @@
+#!/usr/bin/env python3
+"""VMC inner-loop benchmark: N2 (14 e-), 4096 walkers per GPU, MI355X.
+
+One benchmark "step" = one VMC iteration of the reference driver's sampling
+loop (main_all_electrons_adam_muti_GPU.py:177-197 / VMC/VMCmain.py:83-91):
+  mc_step with nsteps drift-diffusion Metropolis sweeps (VMCmcstep.py:121-140),
+  local energy of every walker (hamiltonian.local_energy, complex_output=False),
+  energy statistics pmean (loss.py:206-208) as ONE all-reduce over RCCL.
+Walkers are sharded: each rank owns --walkers walkers (weak scaling); only the
+statistics cross ranks.
+
+Usage: python bench.py [--gpus N --steps K --warmup W]; for N>1 launch with
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N --steps K --warmup W
+Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "ab-initio-flexible-gaussian-basis-neural-network-quantum-monte-carlo_amd")
+sys.path.insert(0, PKG)
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+
+# Algorithmic FLOP model of SURVEY.md 8(d) (N2, hand-counted from the nn.py layer dims)
+F_FWD_N2 = 4.9e4                 # one wavefunction forward, FLOP/config
+F_VG_N2 = 3 * F_FWD_N2           # value + gradient (bwd ~ 2x fwd), FLOP/config
+F_MC_N2 = 2.2e6                  # one walker-step = (N+1) value+gradient passes
+F_EL_N2 = 2.55e6                 # one local-energy evaluation
+PEAK_FP32_TFLOPS = 157.3         # MI355X FP32 vector peak (MI355X_MICROARCH.md)
+PEAK_FP64_TFLOPS = 78.6          # FP64 vector peak (spec)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--walkers", type=int, default=4096, help="walkers per GPU")
+    ap.add_argument("--nsteps", type=int, default=10, help="Metropolis sweeps per iteration")
+    ap.add_argument("--tstep", type=float, default=0.05)
+    ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
+    ap.add_argument("--system", default="N2")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-walkers", type=int, default=8)
+    return ap.parse_args()
+
+
+def system_def(name):
+    if name == "N2":
+        return np.array([[0.0, 0.0, -1.0372], [0.0, 0.0, 1.0372]]), np.array([7.0, 7.0])
+    if name == "Be":
+        return np.zeros((1, 3)), np.array([4.0])
+    if name == "Ne":
+        return np.zeros((1, 3)), np.array([10.0])
+    if name == "H2":
+        return np.array([[0.0, 0.0, -0.7], [0.0, 0.0, 0.7]]), np.array([1.0, 1.0])
+    raise KeyError(name)
+
+
+def build(name, dtype, device):
+    from aiqmc import spin_indices
+    from aiqmc.wavefunction_Ynlm import nn
+    atoms, charges = system_def(name)
+    n = int(charges.sum())
+    spins = np.array([1.0 if i % 2 == 0 else -1.0 for i in range(n)])
+    par, anti, npar, nanti = spin_indices.jastrow_indices_ee(spins, n)
+    up, dn = spin_indices.spin_indices_h(spins)
+    nup = int((spins > 0).sum())
+    network = nn.make_ai_net(nspins=(nup, n - nup), charges=charges, parallel_indices=par,
+                             antiparallel_indices=anti, spin_up_indices=up, spin_down_indices=dn,
+                             n_parallel=npar, n_antiparallel=nanti, ndim=3, natoms=len(atoms), nelectrons=n)
+    params = network.init(1)
+    net = network.apply._aiqmc_network
+    ctx = net.bind(params, atoms, dtype, device)
+    return atoms, charges, spins, network, params, ctx
+
+
+def cpu_baseline(name, params, atoms, charges, nsteps_unused, tstep, sample_walkers):
+    """Time the float64 oracle (reference algorithms) on host cores on a bounded sample."""
+    sys.path.insert(0, ROOT)
+    from oracle import hamiltonian, mcstep, network, system
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    s = system.make_system(name)
+    net = network.Network(s)
+    pt = network.to_torch(params)
+    rng = np.random.default_rng(5)
+    B = sample_walkers
+    N = s.nelectrons
+    x = torch.tensor(system.init_electrons(rng, s.atoms, s.charges, B, 1.0))
+    g1 = torch.tensor(rng.standard_normal((B, 3 * N)))
+    g2 = torch.tensor(rng.standard_normal((B, N, 3 * N)))
+    u = torch.tensor(rng.uniform(size=(B, N)))
+    t0 = time.perf_counter()
+    mcstep.walkers_update(net, pt, x, g1, g2, u, tstep)
+    t_mc = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    hamiltonian.batch_local_energy(net, pt, x[:max(1, B // 2)])
+    t_el = time.perf_counter() - t0
+    return {
+        "value": B / t_mc, "unit": "walker*steps/s", "cores": threads, "kind": "port",
+        "local_energy_evals_per_s": max(1, B // 2) / t_el,
+        "sample": f"float64 oracle (torch CPU, jvp-of-grad Laplacian, per-electron-config MH) on {name}: "
+                  f"1 Metropolis sweep of {B} walkers ({t_mc:.1f}s) + local energy of {max(1, B // 2)} "
+                  f"walkers ({t_el:.1f}s)",
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dtype = torch.float32 if args.dtype == "f32" else torch.float64
+    from aiqmc import constants, _lib
+    from aiqmc.initial_electrons_positions.init import init_electrons
+
+    atoms, charges, spins, network, params, ctx = build(args.system, dtype, local_rank)
+    N = int(charges.sum())
+    B = args.walkers
+    pos0, _ = init_electrons(1000 + rank, None, atoms, charges, spins, B, 1.0)
+    pos = pos0.to(dev, dtype).contiguous()
+    el = torch.empty(B, dtype=dtype, device=dev)
+    seed = 12345 + rank
+    offset = 0
+
+    def iteration(record=None):
+        nonlocal offset
+        if record is not None:
+            record[0].record()
+        ctx.mc_step(pos, args.nsteps, args.tstep, seed=seed, offset=offset)
+        offset += args.nsteps
+        if record is not None:
+            record[1].record()
+        ctx.local_energy(pos, out=el)
+        if record is not None:
+            record[2].record()
+        return constants.pmean_stats(el)
+
+    for _ in range(args.warmup):
+        iteration()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ctx.profile(True)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    stats = None
+    for k in range(args.steps):
+        stats = iteration(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_local = time.perf_counter() - t0
+    ctx.profile(False)
+    mc_ms = sum(e[0].elapsed_time(e[1]) for e in evs)
+    el_ms = sum(e[1].elapsed_time(e[2]) for e in evs)
+    prop_ms, prop_n = ctx.profile_read(_lib.PROF_MC_PROPOSAL)
+    walk_ms, walk_n = ctx.profile_read(_lib.PROF_MC_WALKER)
+    lap_ms, lap_n = ctx.profile_read(_lib.PROF_LOCAL_ENERGY)
+    tt = torch.tensor([t_local, mc_ms, el_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    t_job, mc_ms_max, el_ms_max = tt.tolist()
+    mean_e, var_e = (float(stats[0]), float(stats[1]))
+    finite = bool(torch.isfinite(pos).all().item()) and math.isfinite(mean_e)
+
+    if rank == 0:
+        total_walkers = world * B
+        value = total_walkers * args.nsteps * args.steps / t_job
+        peak = PEAK_FP32_TFLOPS if dtype == torch.float32 else PEAK_FP64_TFLOPS
+        prop_avg_ms = prop_ms / max(prop_n, 1)
+        flop_prop = B * N * F_VG_N2 if args.system == "N2" else None
+        achieved = (flop_prop / (prop_avg_ms * 1e-3) / 1e12) if flop_prop else None
+        lap_avg_ms = lap_ms / max(lap_n, 1)
+        achieved_el = (B * F_EL_N2 / (lap_avg_ms * 1e-3) / 1e12) if args.system == "N2" else None
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get("k_walker_grad_proposal_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "walker*steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * t_job / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" if dtype == torch.float32 else "f64",
+            "data": "synthetic (init_electrons walkers, random-init network of the reference architecture)",
+            "config": {"workload": f"{args.system} VMC iteration: {args.nsteps} Metropolis sweeps + local energy "
+                                   f"+ energy-stat all-reduce", "system": args.system, "electrons": N,
+                       "walkers_per_gpu": B, "global_walkers": total_walkers, "nsteps": args.nsteps,
+                       "tstep": args.tstep, "parallelism": f"walker-sharded dp{world}"},
+            "local_energy_evals_per_s": total_walkers * args.steps / (el_ms_max * 1e-3),
+            "mc_walker_steps_per_s": total_walkers * args.nsteps * args.steps / (mc_ms_max * 1e-3),
+            "roofline": {
+                "kernel": "k_walker<float,14,2,GRAD> proposal launch (B*N value+gradient configs)",
+                "bound": "mfma", "compute_unit": "VALU (fp32 dense peak = VALU peak)", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                "frac": (achieved / peak) if achieved else None, "traffic": traffic,
+                "avg_launch_ms": prop_avg_ms, "launches": prop_n,
+                "flop_per_launch": flop_prop,
+                "flop_model": "B*N*3*F_fwd, F_fwd=4.9e4 (SURVEY 8d)"},
+            "roofline_local_energy": {
+                "kernel": "k_walker<float,14,2,LAP>", "achieved": achieved_el, "peak": peak, "unit": "TFLOP/s",
+                "frac": (achieved_el / peak) if achieved_el else None, "avg_launch_ms": lap_avg_ms,
+                "launches": lap_n, "flop_model": "B*2.55e6 (SURVEY 8d)"},
+            "walker_grad_avg_ms": walk_ms / max(walk_n, 1),
+            "mean_energy": mean_e, "energy_variance": var_e, "finite": finite,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(args.system, params, atoms, charges, args.nsteps, args.tstep,
+                                                   args.cpu_sample_walkers)
+            except Exception as e:  # the baseline is a report, never a failure of the bench
+                out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -104,6 +104,15 @@ int aiqmc_mc_step(aiqmc_ctx* ctx, void* pos_inout, int32_t B, int32_t nsteps, do
                   int32_t rng_mode, const void* gauss1, const void* gauss2, const void* u,
                   uint64_t seed, uint64_t offset, int32_t* accept_out, void* stream);
 
+/* Optional HIP-event timing of the hot kernels, recorded on the caller's
+ * stream around each launch while enabled.  Slots: 0 = proposal
+ * value+gradient launches of aiqmc_mc_step, 1 = walker gradient launches of
+ * aiqmc_mc_step, 2 = aiqmc_local_energy launches.  aiqmc_profile_read waits
+ * for the recorded events, returns the summed kernel time in ms and the launch
+ * count of one slot, and clears it. */
+int aiqmc_profile_enable(aiqmc_ctx* ctx, int32_t on);
+int aiqmc_profile_read(aiqmc_ctx* ctx, int32_t slot, double* total_ms, int64_t* launches);
+
 /* Bytes of device workspace the context holds (for memory planning). */
 int64_t aiqmc_workspace_bytes(const aiqmc_ctx* ctx);
 

@@ -196,3 +196,23 @@ def map_tree(fn, tree):
     if isinstance(tree, tuple):
         return tuple(map_tree(fn, v) for v in tree)
     return fn(tree)
+
+
+def unflatten_params(template, flat: np.ndarray):
+    """Inverse of flatten_params for a tree with the template's structure/shapes."""
+    flat = np.asarray(flat, dtype=np.float64)
+    pos = [0]
+
+    def build(tree):
+        if isinstance(tree, dict):
+            return {k: build(tree[k]) for k in sorted(tree.keys())}
+        if isinstance(tree, (list, tuple)):
+            return [build(v) for v in tree]
+        a = np.asarray(tree)
+        out = flat[pos[0]:pos[0] + a.size].reshape(a.shape)
+        pos[0] += a.size
+        return out
+    out = build(template)
+    if pos[0] != flat.size:
+        raise ValueError(f"flat vector has {flat.size} entries, template needs {pos[0]}")
+    return out
