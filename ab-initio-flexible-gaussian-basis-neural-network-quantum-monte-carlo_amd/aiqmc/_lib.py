@@ -25,7 +25,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_create", "aiqmc_destroy", "aiqmc_param_count", "aiqmc_set_params",
     "aiqmc_logpsi", "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_mc_step",
     "aiqmc_workspace_bytes", "aiqmc_last_error", "aiqmc_supported_shapes",
-    "aiqmc_profile_enable", "aiqmc_profile_read",
+    "aiqmc_profile_enable", "aiqmc_profile_read", "aiqmc_debug_logpsi_grad_forward",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -79,6 +79,8 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_local_energy.argtypes = [vp, vp, i32, vp, vp, vp, vp]
     lib.aiqmc_mc_step.argtypes = [vp, vp, i32, i32, ctypes.c_double, i32, vp, vp, vp,
                                   ctypes.c_uint64, ctypes.c_uint64, vp, vp]
+    lib.aiqmc_debug_logpsi_grad_forward.argtypes = [vp, vp, i32, vp, vp, vp]
+    lib.aiqmc_debug_logpsi_grad_forward.restype = ctypes.c_int
     lib.aiqmc_profile_enable.argtypes = [vp, i32]
     lib.aiqmc_profile_read.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64)]
     lib.aiqmc_last_error.restype = ctypes.c_char_p
@@ -222,6 +224,16 @@ class Context:
         grad = torch.empty_like(p)
         check(self._lib.aiqmc_logpsi_grad(self._h, _ptr(p), B, _ptr(logabs), _ptr(grad), _stream(self.device)),
               "aiqmc_logpsi_grad")
+        return logabs, grad
+
+    def logpsi_grad_forward_mode(self, pos: torch.Tensor):
+        """Diagnostics: the same quantity through the forward-mode kernel (cross-check)."""
+        p = self._pos(pos)
+        B = p.shape[0]
+        logabs = torch.empty(B, dtype=self.dtype, device=self.device)
+        grad = torch.empty_like(p)
+        check(self._lib.aiqmc_debug_logpsi_grad_forward(self._h, _ptr(p), B, _ptr(logabs), _ptr(grad),
+                                                        _stream(self.device)), "aiqmc_debug_logpsi_grad_forward")
         return logabs, grad
 
     def local_energy(self, pos: torch.Tensor, want_logabs: bool = False, want_grad: bool = False,

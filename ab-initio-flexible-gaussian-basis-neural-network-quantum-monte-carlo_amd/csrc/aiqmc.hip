@@ -259,8 +259,8 @@ static KArgs base_args(const aiqmc_ctx* c) {
 static int check_call(aiqmc_ctx* c, const void* pos, int B) {
   if (!c) return fail(AIQMC_EINVAL, "null context");
   if (!c->params_set) return fail(AIQMC_ESTATE, "aiqmc_set_params has not been called");
-  if (!pos) return fail(AIQMC_EINVAL, "null positions");
   if (B < 0) return fail(AIQMC_EINVAL, "negative batch");
+  if (!pos && B > 0) return fail(AIQMC_EINVAL, "null positions");
   return 0;
 }
 
@@ -283,8 +283,8 @@ int aiqmc_logpsi(aiqmc_ctx* c, const void* pos, int32_t B, void* logabs, void* p
 int aiqmc_logpsi_grad(aiqmc_ctx* c, const void* pos, int32_t B, void* logabs, void* grad, void* stream) {
   int rc = check_call(c, pos, B);
   if (rc) return rc;
-  if (!grad) return fail(AIQMC_EINVAL, "null grad");
   if (B == 0) return AIQMC_OK;
+  if (!grad) return fail(AIQMC_EINVAL, "null grad");
   ShapeOps ops;
   shape_ops(c->N, c->A, &ops);
   KArgs ka = base_args(c);
@@ -301,8 +301,8 @@ int aiqmc_local_energy(aiqmc_ctx* c, const void* pos, int32_t B, void* e_l, void
                        void* stream) {
   int rc = check_call(c, pos, B);
   if (rc) return rc;
-  if (!e_l) return fail(AIQMC_EINVAL, "null e_l");
   if (B == 0) return AIQMC_OK;
+  if (!e_l) return fail(AIQMC_EINVAL, "null e_l");
   ShapeOps ops;
   shape_ops(c->N, c->A, &ops);
   KArgs ka = base_args(c);
@@ -405,6 +405,24 @@ int aiqmc_profile_read(aiqmc_ctx* c, int32_t slot, double* total_ms, int64_t* la
   c->ev_used[slot].clear();
   *total_ms = tot;
   *launches = n;
+  return AIQMC_OK;
+}
+
+int aiqmc_debug_logpsi_grad_forward(aiqmc_ctx* c, const void* pos, int32_t B, void* logabs, void* grad,
+                                     void* stream) {
+  int rc = check_call(c, pos, B);
+  if (rc) return rc;
+  if (B == 0) return AIQMC_OK;
+  if (!grad) return fail(AIQMC_EINVAL, "null grad");
+  ShapeOps ops;
+  shape_ops(c->N, c->A, &ops);
+  KArgs ka = base_args(c);
+  ka.nconf = B;
+  ka.pos = pos;
+  ka.logabs = logabs;
+  ka.grad = grad;
+  ops.walker(c->dtype, MODE_GRAD_FWD, ka, B, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
   return AIQMC_OK;
 }
 

@@ -6,6 +6,7 @@
 #include <cstring>
 
 #include "ctx.h"
+#include "walker_rev.h"
 
 using namespace aq;
 
@@ -189,11 +190,12 @@ static void pack_params(const aiqmc_ctx* c, const double* flat, std::vector<doub
 
 template <int N, int A>
 static int set_lds_impl() {
-  const int sizes[4] = {Smem<float, N, false>::bytes, Smem<float, N, true>::bytes, Smem<double, N, false>::bytes,
-                        Smem<double, N, true>::bytes};
-  const void* fns[4] = {(const void*)&k_walker<float, N, A, MODE_GRAD>, (const void*)&k_walker<float, N, A, MODE_LAP>,
-                        (const void*)&k_walker<double, N, A, MODE_GRAD>, (const void*)&k_walker<double, N, A, MODE_LAP>};
-  for (int k = 0; k < 4; ++k) {
+  const int sizes[6] = {Smem<float, N, false>::bytes,  Smem<float, N, true>::bytes,  Smem<double, N, false>::bytes,
+                        Smem<double, N, true>::bytes,  SmemRev<float, N, A>::bytes, SmemRev<double, N, A>::bytes};
+  const void* fns[6] = {(const void*)&k_walker<float, N, A, MODE_GRAD>,  (const void*)&k_walker<float, N, A, MODE_LAP>,
+                        (const void*)&k_walker<double, N, A, MODE_GRAD>, (const void*)&k_walker<double, N, A, MODE_LAP>,
+                        (const void*)&k_walker_rev<float, N, A>,         (const void*)&k_walker_rev<double, N, A>};
+  for (int k = 0; k < 6; ++k) {
     if (sizes[k] > 65536) {
       hipError_t e = hipFuncSetAttribute(fns[k], hipFuncAttributeMaxDynamicSharedMemorySize, sizes[k]);
       if (e != hipSuccess) return fail(AIQMC_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
@@ -202,16 +204,22 @@ static int set_lds_impl() {
   return 0;
 }
 
+// MODE_GRAD -> reverse-mode value+gradient kernel (walker_rev.h); MODE_LAP -> forward
+// Laplacian kernel (walker_kernel.h); MODE_GRAD_FWD -> forward-mode gradient (diagnostics).
 template <int N, int A>
 static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStream_t s) {
   if (dtype == AIQMC_F32) {
     if (mode == MODE_LAP)
       k_walker<float, N, A, MODE_LAP><<<dim3(nconf), dim3(64), Smem<float, N, true>::bytes, s>>>(ka);
+    else if (mode == MODE_GRAD)
+      k_walker_rev<float, N, A><<<dim3(nconf), dim3(64), SmemRev<float, N, A>::bytes, s>>>(ka);
     else
       k_walker<float, N, A, MODE_GRAD><<<dim3(nconf), dim3(64), Smem<float, N, false>::bytes, s>>>(ka);
   } else {
     if (mode == MODE_LAP)
       k_walker<double, N, A, MODE_LAP><<<dim3(nconf), dim3(64), Smem<double, N, true>::bytes, s>>>(ka);
+    else if (mode == MODE_GRAD)
+      k_walker_rev<double, N, A><<<dim3(nconf), dim3(64), SmemRev<double, N, A>::bytes, s>>>(ka);
     else
       k_walker<double, N, A, MODE_GRAD><<<dim3(nconf), dim3(64), Smem<double, N, false>::bytes, s>>>(ka);
   }

@@ -29,6 +29,7 @@ namespace aq {
 
 constexpr int MODE_GRAD = 1;
 constexpr int MODE_LAP = 2;
+constexpr int MODE_GRAD_FWD = 3;   // forward-mode gradient (diagnostics / cross-check)
 
 struct KArgs {
   int nconf;

@@ -1,0 +1,601 @@
+// walker_rev.h -- reverse-mode value + gradient of log|psi| for ONE configuration
+// per wavefront (the Metropolis hot path: VMCmcstep.py:41-53 and :79 evaluate
+// jax.grad(logabs) at the walkers and at all B*N single-electron proposals).
+//
+// Forward pass (values) with lanes over work items, intermediates in LDS:
+//   F1 per-electron stage as forward jets along the lane's own coordinate
+//      (direction lanes keep d(features)/dx_e and d(Yt row)/dx_e in registers:
+//      these sub-Jacobians are local to electron e);
+//   F2 pair stream h2[k,i] for all N^2 pairs (lanes over pairs), J_ee, V_ee;
+//   F3 spin-group column means g2 (nn.py:151); F4 three h-stream layers
+//      (lanes over (electron, unit)); F5 Phi, A = Phi * Yt, Gauss-Jordan -> B.
+// Backward pass:
+//   B1 dL/dH[r,f] = Re Q_f[r,r] = Re sum_c W_{s(r)}[f,c] Yt[r,c] B[c,r],
+//      dL/dYt[r,c] = Re(B[c,r] Phi[r,c]);
+//   B2 back through the three h-stream layers (tanh, conv quads, group means);
+//   B3 back through each pair's two double layers to d = x_i - x_k (+ J_ee);
+//   B4 direction lane (c,e) assembles dlogpsi/dx_{e,c} from pair adjoints and
+//      its electron-local sub-Jacobians (Yt row, ae features, J_ae).
+#pragma once
+#include "jets.h"
+#include "layout.h"
+#include "walker_kernel.h"
+
+namespace aq {
+
+template <typename T, int N, int A>
+struct SmemRev {
+  static constexpr int D0 = 4 * A;               // layer-0 h width
+  static constexpr int DFM = 3 * D0 + 8;         // widest conv input (layer 0)
+  static constexpr int QM = DFM / 4;
+  static constexpr int xs = 0;                   // 48
+  static constexpr int hl = 48;                  // h^0 [N][D0], h^1..h^3 [N][4]
+  static constexpr int hl_n = N * D0 + 3 * N * 4;
+  static constexpr int g1 = hl + hl_n;           // [3][2][D0]
+  static constexpr int cq = g1 + 3 * 2 * D0;     // [3][N][QM]
+  static constexpr int sv = cq + 3 * N * QM;     // [3][N][4]
+  static constexpr int p2 = sv + 3 * N * 4;      // [3][N][N][4] pair values
+  static constexpr int g2 = p2 + 3 * N * N * 4;  // [3][2][N][4]
+  static constexpr int yv = g2 + 3 * 2 * N * 4;  // [N][N]
+  static constexpr int ph = yv + N * N;          // [N][N][2]
+  static constexpr int mx = ph + N * N * 2;      // [N][2N][2]
+  static constexpr int fac = mx + N * 2 * N * 2; // [N][2]
+  static constexpr int ybar = fac + N * 2;       // [N][N]
+  static constexpr int hbar = ybar + N * N;      // adjoints of h^0..h^3 (same layout as hl)
+  static constexpr int zsb = hbar + hl_n;        // [N][4]
+  static constexpr int fbar = zsb + N * 4;       // [N][DFM]
+  static constexpr int gsum = fbar + N * DFM;    // [2][D0]
+  static constexpr int g2b = gsum + 2 * D0;      // [3][2][N][4]
+  static constexpr int dbar = g2b + 3 * 2 * N * 4;  // [N][N][3]
+  static constexpr int red = dbar + N * N * 3;   // 64 scratch
+  static constexpr int end = red + 64;
+  static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
+  // offset of h^l inside the hl / hbar blocks
+  static constexpr int hoff(int l) { return l == 0 ? 0 : N * D0 + (l - 1) * N * 4; }
+};
+
+template <typename T, int N, int A>
+__global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
+  using Ly = Lay<N, A>;
+  using SM = SmemRev<T, N, A>;
+  constexpr int D0 = SM::D0;
+  constexpr int N2 = 2 * N;
+  const T* __restrict__ P = (const T*)ka.prm;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  T* sm = (T*)smem_raw;
+  T* xs = sm + SM::xs;
+
+  const int conf = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int lc = lane >> 4;
+  const int er = lane & 15;
+  const int le = er < N ? er : N - 1;
+  const bool val = (lc == 3);
+  const bool live = er < N;
+  const bool dir = (lc < 3) && live;
+  const int nup = ka.nup;
+  const T tstep = (T)ka.tstep;
+  const T RSQ2 = T(0.70710678118654752);
+  const T ginv0 = T(1) / T(nup), ginv1 = T(1) / T(N - nup);
+  const int* rowsrc = ka.rowsrc;
+
+  // ------------------------------------------------------------------ F0 positions (as k_walker)
+  int pb = conf, pi = -1;
+  if (ka.proposal) {
+    pb = conf / N;
+    pi = conf - pb * N;
+  }
+  if (lane < 3 * N) {
+    T x = ((const T*)ka.pos)[(size_t)pb * 3 * N + lane];
+    if (ka.proposal && lane / 3 == pi) {
+      T z;
+      if (ka.gauss1) {
+        z = ((const T*)ka.gauss1)[(size_t)pb * 3 * N + lane];
+      } else {
+        T g3[3];
+        philox_normal3<T>(ka.seed, ka.step, (uint32_t)(pb * N + pi), 0u, g3);
+        const int c = lane - 3 * pi;
+        z = c == 0 ? g3[0] : (c == 1 ? g3[1] : g3[2]);
+      }
+      const T ge = ((const T*)ka.pgrad)[(size_t)pb * 3 * N + lane] * (T)(*ka.taueff);
+      x = x + (ge * tstep + f_sqrt(tstep) * z);
+    }
+    xs[lane] = x;
+  }
+  __syncthreads();
+
+  // ------------------------------------------------------------------ F1 per-electron stage (forward jets)
+  PJ<T> xe[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) xe[c] = PJ<T>{xs[le * 3 + c], (lc == c) ? T(1) : T(0), T(0)};
+  PJ<T> hf[D0];
+  PJ<T> yin[4 * A + 2];
+  PJ<T> ra[A];
+  PJ<T> aev[A][3];
+  PJ<T> hisum = pjc(T(0)), spsum = pjc(T(0));
+  {
+    const T PI = T(3.141592653589793);
+    const T c0 = T(0.5) * f_sqrt(T(1) / PI), c1 = f_sqrt(T(3) / (T(4) * PI));
+    const T k15h = T(0.5) * f_sqrt(T(15) / PI), k5q = T(0.25) * f_sqrt(T(5) / PI);
+    const T k15q = T(0.25) * f_sqrt(T(15) / PI), k35 = T(0.25) * f_sqrt(T(35) / (T(2) * PI));
+    const T k105h = T(0.5) * f_sqrt(T(105) / PI), k21 = T(0.25) * f_sqrt(T(21) / (T(2) * PI));
+    const T k7 = T(0.25) * f_sqrt(T(7) / PI), k105q = T(0.25) * f_sqrt(T(105) / PI);
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      PJ<T> ae[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) ae[c] = xe[c] - P[Ly::atoms + a * 3 + c];
+      const PJ<T> r = pj_sqrt(ae[0] * ae[0] + ae[1] * ae[1] + ae[2] * ae[2]);
+      ra[a] = r;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) aev[a][c] = ae[c];
+      hf[4 * a] = r;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) hf[4 * a + 1 + c] = ae[c];
+      const PJ<T> x0 = ae[0] / r, x1 = ae[1] / r, x2 = ae[2] / r;
+      yin[4 * a + 0] = pjc(c0);
+      yin[4 * a + 1] = c1 * x0;
+      yin[4 * a + 2] = c1 * x1;
+      yin[4 * a + 3] = c1 * x2;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) spsum = spsum + yin[4 * a + m];
+      const PJ<T> y2 = r * r, y3 = y2 * r;
+      const PJ<T> x00 = x0 * x0, x11 = x1 * x1, x22 = x2 * x2;
+      hisum = hisum + k15h * (x0 * x1 / y2);
+      hisum = hisum + k15h * (x1 * x2 / y2);
+      hisum = hisum + k5q * ((T(3) * x22 - y2) / y2);
+      hisum = hisum + k15h * (x0 * x2 / y2);
+      hisum = hisum + k15q * ((x00 - x11) / y2);
+      hisum = hisum + k35 * ((x1 * (T(3) * x00 - x11)) / y3);
+      hisum = hisum + k105h * (x0 * x1 * x2 / y3);
+      hisum = hisum + k21 * ((x1 * (T(5) * x22 - y2)) / y3);
+      hisum = hisum + k7 * ((T(5) * (x22 * x2) - T(3) * x2 * y2) / y3);
+      hisum = hisum + k21 * ((x0 * (T(5) * x22 - y2)) / y3);
+      hisum = hisum + k105q * (((x00 - x11) * x2) / y3);
+      hisum = hisum + k35 * ((x0 * (x00 - T(3) * x11)) / y3);
+    }
+  }
+  yin[4 * A] = hisum / T(12 * A);
+  yin[4 * A + 1] = spsum / T(4 * A);
+  PJ<T> yst[NYW];
+  {
+    constexpr int DY0 = Ly::DY0;
+#pragma unroll
+    for (int o = 0; o < NYW; ++o) {
+      PJ<T> s = P[Ly::y_w0 + o] * yin[0];
+#pragma unroll
+      for (int m = 1; m < DY0; ++m) s = s + P[Ly::y_w0 + m * NYW + o] * yin[m];
+      yst[o] = pj_tanh(s + P[Ly::y_b0 + o]);
+      if constexpr (DY0 == NYW) yst[o] = T(0.70710678118654752) * (yin[o] + yst[o]);
+    }
+#pragma unroll
+    for (int l = 1; l < 3; ++l) {
+      const int wo = l == 1 ? Ly::y_w1 : Ly::y_w2;
+      const int bo = l == 1 ? Ly::y_b1 : Ly::y_b2;
+      PJ<T> nx[NYW];
+#pragma unroll
+      for (int o = 0; o < NYW; ++o) {
+        PJ<T> s = P[wo + o] * yst[0];
+#pragma unroll
+        for (int m = 1; m < NYW; ++m) s = s + P[wo + m * NYW + o] * yst[m];
+        nx[o] = pj_tanh(s + P[bo + o]);
+      }
+#pragma unroll
+      for (int o = 0; o < NYW; ++o) yst[o] = T(0.70710678118654752) * (yst[o] + nx[o]);
+    }
+  }
+  PJ<T> env = pjc(T(0)), jae = pjc(T(0));
+  {
+    const T alpha = P[Ly::env_alpha + le], xi = P[Ly::env_xi + le];
+    PJ<T> s1 = pjc(T(0)), s2 = pjc(T(0));
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      const T beta = P[Ly::env_beta + le * A + a];
+      s1 = s1 + alpha * pj_exp(-beta * (ra[a] * ra[a]));
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const T pi_ = P[Ly::env_pi + (le * A + a) * 3 + c];
+        const T sg = P[Ly::env_sigma + (le * A + a) * 3 + c];
+        s2 = s2 + (sg * xi) * pj_exp(-pi_ * aev[a][c]);
+      }
+      const T bj = P[Ly::jae_b + le * A + a];
+      const T c34 = P[Ly::c34 + a], c14 = P[Ly::c14 + a];
+      const PJ<T> ex = pj_exp(-(c14 * bj) * ra[a]);
+      jae = jae + (-c34 * (pjc(T(1)) - ex)) / (T(2) * bj);
+    }
+    env = s1 + s2;
+  }
+  T* Yv = sm + SM::yv;
+  T Yd1[N];
+#pragma unroll
+  for (int col = 0; col < N; ++col) {
+    PJ<T> s = P[Ly::wy + col] * yst[0];
+#pragma unroll
+    for (int m = 1; m < NYW; ++m) s = s + P[Ly::wy + m * N + col] * yst[m];
+    const PJ<T> yt = env * s;
+    Yd1[col] = yt.d1;
+    if (val && live) Yv[er * N + col] = yt.v;
+  }
+  T hfd1[D0];
+#pragma unroll
+  for (int m = 0; m < D0; ++m) {
+    hfd1[m] = hf[m].d1;
+    if (val && live) sm[SM::hl + er * D0 + m] = hf[m].v;
+  }
+  T jv = (val && live) ? jae.v : T(0);
+  T jd1 = dir ? jae.d1 : T(0);
+  __syncthreads();
+
+  // ------------------------------------------------------------------ F2 pair stream values (all N^2 pairs)
+  T* p2 = sm + SM::p2;
+  for (int it = lane; it < N * N; it += 64) {
+    const int k = it / N, i = it - k * N;
+    T p[4];
+    if (k == i) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) p[f] = T(0);
+    } else {
+      T d[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) d[c] = xs[i * 3 + c] - xs[k * 3 + c];
+      const T r = f_sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+      p[0] = r;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) p[1 + c] = d[c];
+      if (k < i) {
+        const T cusp = P[Ly::jee_c + k * N + i], al = P[Ly::jee_a + k * N + i];
+        jv += f_div(cusp * r, al * r + T(1));
+      }
+    }
+#pragma unroll
+    for (int f = 0; f < 4; ++f) p2[((0 * N + k) * N + i) * 4 + f] = p[f];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const T* dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
+      const T* db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
+      T q[4];
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        T s = db[o];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) s += p[m] * dw[m * 4 + o];
+        q[o] = f_tanh(s);
+      }
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        p[o] = (p[o] + q[o]) * RSQ2;
+        p2[(((j + 1) * N + k) * N + i) * 4 + o] = p[o];
+      }
+    }
+  }
+  __syncthreads();
+
+  // ------------------------------------------------------------------ F3 g2[l][G][i][f] = mean_{k in G} h2^l[k,i,f]
+  T* g2 = sm + SM::g2;
+  for (int it = lane; it < 3 * 2 * N * 4; it += 64) {
+    const int f = it & 3;
+    const int i = (it >> 2) % N;
+    const int G = ((it >> 2) / N) & 1;
+    const int l = (it >> 2) / (2 * N);
+    const int k0 = G ? nup : 0, k1 = G ? N : nup;
+    T s = T(0);
+    for (int k = k0; k < k1; ++k) s += p2[((l * N + k) * N + i) * 4 + f];
+    g2[it] = s * (G ? ginv1 : ginv0);
+  }
+  __syncthreads();
+
+  // ------------------------------------------------------------------ F4 h-stream layers (values)
+  T* hl = sm + SM::hl;
+  T* g1 = sm + SM::g1;
+  T* cqv = sm + SM::cq;
+  T* sv = sm + SM::sv;
+#pragma unroll
+  for (int l = 0; l < 3; ++l) {
+    const int d1 = l == 0 ? D0 : NH;
+    const int DF = 3 * d1 + 8;
+    const int Q = DF / 4;
+    const T* hin = hl + SM::hoff(l);
+    T* hout = hl + SM::hoff(l + 1);
+    const T* convw = P + (l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2));
+    const T* convb = P + (l == 0 ? Ly::conv_b0 : (l == 1 ? Ly::conv_b1 : Ly::conv_b2));
+    const T* sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
+    const T* sngb = P + (l == 0 ? Ly::sng_b0 : (l == 1 ? Ly::sng_b1 : Ly::sng_b2));
+    T* g1l = g1 + l * 2 * D0;
+    if (lane < 2 * d1) {
+      const int G = lane / d1, m = lane - G * d1;
+      const int k0 = G ? nup : 0, k1 = G ? N : nup;
+      T s = T(0);
+      for (int k = k0; k < k1; ++k) s += hin[k * d1 + m];
+      g1l[G * d1 + m] = s * (G ? ginv1 : ginv0);
+    }
+    __syncthreads();
+    for (int it = lane; it < N * Q; it += 64) {
+      const int i = it / Q, q = it - i * Q;
+      T z = T(0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int j = 4 * q + s;
+        T F;
+        if (j < d1) F = hin[i * d1 + j];
+        else if (j < 3 * d1) F = g1l[j - d1];
+        else F = g2[((l * 2 + (j - 3 * d1) / 4) * N + i) * 4 + ((j - 3 * d1) & 3)];
+        z += F * convw[i * DF + j];
+      }
+      cqv[(l * N + i) * SM::QM + q] = f_tanh(z * T(0.25) + convb[i * Q + q]);
+    }
+    __syncthreads();
+    if (lane < N * 4) {
+      const int i = lane >> 2, f = lane & 3;
+      T z = sngb[f];
+      for (int q = 0; q < Q; ++q) z += cqv[(l * N + i) * SM::QM + q] * sngw[q * 4 + f];
+      const T s = f_tanh(z);
+      sv[(l * N + i) * 4 + f] = s;
+      hout[i * 4 + f] = (d1 == NH) ? (hin[i * d1 + f] + s) * RSQ2 : s;
+    }
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------------ F5 Phi, A = Phi * Yt, Gauss-Jordan -> B = A^{-1}
+  T* Ph = sm + SM::ph;
+  T* Mx = sm + SM::mx;
+  T* fac = sm + SM::fac;
+  const T* H3 = hl + SM::hoff(3);
+  for (int idx = lane; idx < N * N; idx += 64) {
+    const int r = idx / N, col = idx - r * N;
+    const int src = rowsrc[r];
+    const int sp = r < nup ? 0 : 1;
+    T re = T(0), im = T(0);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const T hv = H3[src * 4 + f];
+      re += hv * P[Ly::orb_w + ((sp * 4 + f) * N + col) * 2 + 0];
+      im += hv * P[Ly::orb_w + ((sp * 4 + f) * N + col) * 2 + 1];
+    }
+    re += P[Ly::orb_b + (sp * N + col) * 2 + 0];
+    im += P[Ly::orb_b + (sp * N + col) * 2 + 1];
+    Ph[idx * 2 + 0] = re;
+    Ph[idx * 2 + 1] = im;
+    const T yv = Yv[idx];
+    Mx[(r * N2 + col) * 2 + 0] = re * yv;
+    Mx[(r * N2 + col) * 2 + 1] = im * yv;
+    Mx[(r * N2 + N + col) * 2 + 0] = (r == col) ? T(1) : T(0);
+    Mx[(r * N2 + N + col) * 2 + 1] = T(0);
+  }
+  __syncthreads();
+  T logdet = T(0), phr = T(1), phi = T(0);
+  for (int k = 0; k < N; ++k) {
+    T key = T(-1);
+    int kid = lane;
+    if (lane >= k && lane < N) key = f_abs(Mx[(lane * N2 + k) * 2]) + f_abs(Mx[(lane * N2 + k) * 2 + 1]);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const T ok = __shfl_xor(key, off);
+      const int oi = __shfl_xor(kid, off);
+      if (ok > key || (ok == key && oi < kid)) {
+        key = ok;
+        kid = oi;
+      }
+    }
+    const int p = __builtin_amdgcn_readfirstlane(kid);
+    if (p != k) {
+      if (lane < 2 * N2) {
+        const T a = Mx[k * N2 * 2 + lane];
+        const T b = Mx[p * N2 * 2 + lane];
+        Mx[k * N2 * 2 + lane] = b;
+        Mx[p * N2 * 2 + lane] = a;
+      }
+      phr = -phr;
+      phi = -phi;
+    }
+    __syncthreads();
+    const T pr = Mx[(k * N2 + k) * 2], pim = Mx[(k * N2 + k) * 2 + 1];
+    const T mag = f_hypot(pr, pim);
+    logdet += f_log(mag);
+    {
+      const T ur = pr / mag, ui = pim / mag;
+      const T nr = phr * ur - phi * ui, ni = phr * ui + phi * ur;
+      phr = nr;
+      phi = ni;
+    }
+    const T den = pr * pr + pim * pim;
+    const T ir = pr / den, ii = -pim / den;
+    if (lane < N) {
+      fac[lane * 2 + 0] = Mx[(lane * N2 + k) * 2 + 0];
+      fac[lane * 2 + 1] = Mx[(lane * N2 + k) * 2 + 1];
+    }
+    __syncthreads();
+    if (lane < N2) {
+      const T mr = Mx[(k * N2 + lane) * 2], mi = Mx[(k * N2 + lane) * 2 + 1];
+      Mx[(k * N2 + lane) * 2] = mr * ir - mi * ii;
+      Mx[(k * N2 + lane) * 2 + 1] = mr * ii + mi * ir;
+    }
+    __syncthreads();
+    for (int idx = lane; idx < N * N2; idx += 64) {
+      const int j = idx / N2, col = idx - j * N2;
+      if (j != k) {
+        const T fr = fac[j * 2], fi = fac[j * 2 + 1];
+        const T kr = Mx[(k * N2 + col) * 2], ki = Mx[(k * N2 + col) * 2 + 1];
+        Mx[(j * N2 + col) * 2] -= fr * kr - fi * ki;
+        Mx[(j * N2 + col) * 2 + 1] -= fr * ki + fi * kr;
+      }
+    }
+    __syncthreads();
+  }
+#define BRE(c, s) Mx[((c) * N2 + N + (s)) * 2]
+#define BIM(c, s) Mx[((c) * N2 + N + (s)) * 2 + 1]
+
+  // ------------------------------------------------------------------ B1 adjoints of H (= h^3) and Yt
+  T* hbar = sm + SM::hbar;
+  T* ybar = sm + SM::ybar;
+  if (lane < 4 * N) {
+    const int r = lane >> 2, f = lane & 3;
+    const int sp = r < nup ? 0 : 1;
+    T q = T(0);
+    for (int c = 0; c < N; ++c) {
+      const T yv = Yv[r * N + c];
+      const T wr = P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2] * yv;
+      const T wi = P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 1] * yv;
+      q += wr * BRE(c, r) - wi * BIM(c, r);
+    }
+    hbar[SM::hoff(3) + rowsrc[r] * 4 + f] = q;
+  }
+  for (int idx = lane; idx < N * N; idx += 64) {
+    const int r = idx / N, c = idx - r * N;
+    ybar[idx] = BRE(c, r) * Ph[idx * 2] - BIM(c, r) * Ph[idx * 2 + 1];
+  }
+#undef BRE
+#undef BIM
+  __syncthreads();
+
+  // ------------------------------------------------------------------ B2 back through the h-stream layers
+  T* zsb = sm + SM::zsb;
+  T* fbar = sm + SM::fbar;
+  T* gsum = sm + SM::gsum;
+  T* g2b = sm + SM::g2b;
+#pragma unroll
+  for (int l = 2; l >= 0; --l) {
+    const int d1 = l == 0 ? D0 : NH;
+    const int DF = 3 * d1 + 8;
+    const int Q = DF / 4;
+    const T* convw = P + (l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2));
+    const T* sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
+    const T* hbo = hbar + SM::hoff(l + 1);
+    T* hbi = hbar + SM::hoff(l);
+    // single: s = tanh(c Ws + b), h_out = res(h_in, s)
+    if (lane < N * 4) {
+      const int i = lane >> 2, f = lane & 3;
+      const T s = sv[(l * N + i) * 4 + f];
+      const T ho = hbo[i * 4 + f];
+      const T sb = (d1 == NH) ? ho * RSQ2 : ho;
+      zsb[i * 4 + f] = sb * (T(1) - s * s);
+    }
+    __syncthreads();
+    // conv: c = tanh(0.25 sum F w + b)
+    for (int it = lane; it < N * Q; it += 64) {
+      const int i = it / Q, q = it - i * Q;
+      T cb = T(0);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) cb += zsb[i * 4 + f] * sngw[q * 4 + f];
+      const T c = cqv[(l * N + i) * SM::QM + q];
+      const T zc = cb * (T(1) - c * c) * T(0.25);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) fbar[i * SM::DFM + 4 * q + s] = zc * convw[i * DF + 4 * q + s];
+    }
+    __syncthreads();
+    // group-mean adjoints: gsum[G][m] = sum_i fbar[i][d1*(1+G)+m]; g2 adjoints
+    if (lane < 2 * d1) {
+      const int G = lane / d1, m = lane - G * d1;
+      T s = T(0);
+      for (int i = 0; i < N; ++i) s += fbar[i * SM::DFM + d1 * (1 + G) + m];
+      gsum[G * d1 + m] = s * (G ? ginv1 : ginv0);
+    }
+    for (int it = lane; it < 2 * N * 4; it += 64) {
+      const int f = it & 3, i = (it >> 2) % N, G = (it >> 2) / N;
+      g2b[((l * 2 + G) * N + i) * 4 + f] = fbar[i * SM::DFM + 3 * d1 + 4 * G + f];
+    }
+    __syncthreads();
+    for (int it = lane; it < N * d1; it += 64) {
+      const int k = it / d1, m = it - k * d1;
+      T v = fbar[k * SM::DFM + m] + gsum[(k >= nup ? 1 : 0) * d1 + m];
+      if (d1 == NH) v += hbo[k * 4 + m] * RSQ2;
+      hbi[k * d1 + m] = v;
+    }
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------------ B3 pair adjoints d(logpsi)/d(x_i - x_k)
+  T* dbar = sm + SM::dbar;
+  for (int it = lane; it < N * (N - 1); it += 64) {
+    const int k = it / (N - 1);
+    const int jj = it - k * (N - 1);
+    const int i = jj + (jj >= k ? 1 : 0);
+    const int G = k >= nup ? 1 : 0;
+    const T gw = G ? ginv1 : ginv0;
+    T d[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) d[c] = xs[i * 3 + c] - xs[k * 3 + c];
+    const T r = f_sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    T p0[4] = {r, d[0], d[1], d[2]};
+    // recompute the two double layers (values)
+    T t1[4], p1[4], t2[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      T s = P[Ly::dbl_b0 + o];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) s += p0[m] * P[Ly::dbl_w0 + m * 4 + o];
+      t1[o] = f_tanh(s);
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) p1[o] = (p0[o] + t1[o]) * RSQ2;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      T s = P[Ly::dbl_b1 + o];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) s += p1[m] * P[Ly::dbl_w1 + m * 4 + o];
+      t2[o] = f_tanh(s);
+    }
+    // adjoints: output of layer l feeds g2[l][G][i] with weight 1/|G|
+    T pb2[4], pb1[4], pb0[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) pb2[f] = g2b[((2 * 2 + G) * N + i) * 4 + f] * gw;
+    T z2[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) z2[o] = pb2[o] * RSQ2 * (T(1) - t2[o] * t2[o]);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      T s = g2b[((1 * 2 + G) * N + i) * 4 + m] * gw + pb2[m] * RSQ2;
+#pragma unroll
+      for (int o = 0; o < 4; ++o) s += z2[o] * P[Ly::dbl_w1 + m * 4 + o];
+      pb1[m] = s;
+    }
+    T z1[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) z1[o] = pb1[o] * RSQ2 * (T(1) - t1[o] * t1[o]);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      T s = g2b[((0 * 2 + G) * N + i) * 4 + m] * gw + pb1[m] * RSQ2;
+#pragma unroll
+      for (int o = 0; o < 4; ++o) s += z1[o] * P[Ly::dbl_w0 + m * 4 + o];
+      pb0[m] = s;
+    }
+    // p0 = [r, d]; Pade e-e Jastrow once per unordered pair (k < i)
+    T rb = pb0[0];
+    if (k < i) {
+      const T cusp = P[Ly::jee_c + k * N + i], al = P[Ly::jee_a + k * N + i];
+      const T den = al * r + T(1);
+      rb += cusp * f_rcp(den * den);
+    }
+    const T ir = f_rcp(r);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) dbar[(k * N + i) * 3 + c] = pb0[1 + c] + rb * d[c] * ir;
+  }
+  __syncthreads();
+
+  // ------------------------------------------------------------------ B4 gradient per direction lane (c, e)
+  T g = jd1;
+  {
+    const int c = lc < 3 ? lc : 0;
+    for (int k = 0; k < N; ++k) {
+      if (k == le) continue;
+      g += dbar[(k * N + le) * 3 + c] - dbar[(le * N + k) * 3 + c];
+    }
+#pragma unroll
+    for (int col = 0; col < N; ++col) g += ybar[le * N + col] * Yd1[col];
+#pragma unroll
+    for (int m = 0; m < D0; ++m) g += hbar[le * D0 + m] * hfd1[m];
+  }
+
+  // ------------------------------------------------------------------ outputs
+  const T gd = dir ? g : T(0);
+  const T sumsq = wave_sum(gd * gd);
+  const T lpsi = logdet + wave_sum(jv);
+  if (ka.grad && dir) ((T*)ka.grad)[(size_t)conf * 3 * N + 3 * le + lc] = g;
+  if (ka.gown && dir && le == pi) ((T*)ka.gown)[(size_t)conf * 3 + lc] = g;
+  if (lane == 0) {
+    if (ka.logabs) ((T*)ka.logabs)[conf] = lpsi;
+    if (ka.phase) ((T*)ka.phase)[conf] = f_atan2(phi, phr);
+    if (ka.sumsq) ((T*)ka.sumsq)[conf] = sumsq;
+  }
+}
+
+}  // namespace aq

@@ -113,6 +113,12 @@ int aiqmc_mc_step(aiqmc_ctx* ctx, void* pos_inout, int32_t B, int32_t nsteps, do
 int aiqmc_profile_enable(aiqmc_ctx* ctx, int32_t on);
 int aiqmc_profile_read(aiqmc_ctx* ctx, int32_t slot, double* total_ms, int64_t* launches);
 
+/* Diagnostics: aiqmc_logpsi_grad through the forward-mode kernel (the
+ * production gradient is reverse mode); used to cross-check the two
+ * derivative implementations at full batch size. */
+int aiqmc_debug_logpsi_grad_forward(aiqmc_ctx* ctx, const void* pos, int32_t B, void* logabs, void* grad,
+                                    void* stream);
+
 /* Bytes of device workspace the context holds (for memory planning). */
 int64_t aiqmc_workspace_bytes(const aiqmc_ctx* ctx);
 

@@ -1,0 +1,76 @@
+"""Multi-rank host logic over torch.distributed gloo (CPU, world_size 2 and 4).
+
+The data path shards walkers with no collective (VMCmcstep has none);
+the only exchange is the energy-statistics pmean (loss.py:206-208), done by
+aiqmc.constants.pmean_stats as ONE all-reduce.  These tests check it equals the
+single-process statistics of the concatenated walker set, and that
+psum/pmean/all_gather follow the reference's constants.py semantics.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    from conftest import PKG
+    sys.path.insert(0, PKG)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from aiqmc import constants
+    rng = np.random.default_rng(rank)
+    e = torch.tensor(rng.normal(-109.0, 3.0, size=64))
+    mean, var = constants.pmean_stats(e)
+    x = torch.tensor([float(rank + 1)])
+    s = constants.psum(x)
+    m = constants.pmean(x)
+    g = constants.all_gather(x)
+    q.put((rank, e.numpy(), float(mean), float(var), float(s), float(m), g.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_pmean_stats_matches_global(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort(key=lambda t: t[0])
+    allE = np.concatenate([r[1] for r in res])
+    for r in res:
+        np.testing.assert_allclose(r[2], allE.mean(), rtol=1e-12)
+        np.testing.assert_allclose(r[3], allE.var(), rtol=1e-9)
+        assert r[4] == sum(range(1, world + 1))
+        np.testing.assert_allclose(r[5], sum(range(1, world + 1)) / world)
+        np.testing.assert_array_equal(r[6].reshape(-1), np.arange(1, world + 1))
+
+
+def test_single_process_collectives_are_identity():
+    from aiqmc import constants
+    x = torch.tensor([1.0, 2.0])
+    assert torch.equal(constants.pmean(x), x)
+    assert torch.equal(constants.psum(x), x)
+    assert constants.all_gather(x).shape == (1, 2)
+    m, v = constants.pmean_stats(torch.tensor([1.0, 3.0]))
+    assert float(m) == 2.0 and float(v) == 1.0

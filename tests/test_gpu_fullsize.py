@@ -1,0 +1,113 @@
+"""Full-size (4096-walker N2) GPU checks through size-independent properties.
+
+The oracle is too slow for 4096 walkers, so at the benchmark size we check:
+  * reverse-mode gradient kernel == forward-mode gradient kernel (two
+    independent derivative implementations) on every walker;
+  * the gradient returned by the Laplacian kernel == both of them;
+  * float32 kernels == float64 kernels (relative, on identical walkers);
+  * log|psi| from all four kernels agree;
+  * Metropolis with on-device Philox draws: finite, deterministic per
+    (seed, offset), acceptance rate in (0, 1).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(name, dtype, params_seed=5):
+    from oracle import system
+    from aiqmc import _lib
+    s = system.make_system(name)
+    t = s.tables()
+    ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
+                       t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"], dtype=dtype,
+                       device=0)
+    p = system.init_params(np.random.default_rng(params_seed), s, randomize_aux=True)
+    ctx.set_params(system.flatten_params(p))
+    return s, ctx
+
+
+def _walkers(s, B, seed=0):
+    from oracle import system
+    return system.init_electrons(np.random.default_rng(seed), s.atoms, s.charges, B, 1.0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_reverse_vs_forward_gradient_4096(dtype):
+    s, ctx = _ctx("N2", dtype)
+    pos = torch.tensor(_walkers(s, 4096), dtype=dtype, device="cuda")
+    la_r, g_r = ctx.logpsi_grad(pos)
+    la_f, g_f = ctx.logpsi_grad_forward_mode(pos)
+    el, la_l, g_l = ctx.local_energy(pos, want_logabs=True, want_grad=True)
+    torch.cuda.synchronize()
+    tol = 1e-9 if dtype == torch.float64 else 2e-3
+    scale = g_f.abs().amax(dim=1, keepdim=True) + 1.0
+    assert torch.all((g_r - g_f).abs() <= tol * scale), float(((g_r - g_f).abs() / scale).max())
+    assert torch.all((g_l - g_f).abs() <= tol * scale)
+    lt = 1e-10 if dtype == torch.float64 else 1e-4
+    assert torch.allclose(la_r, la_f, rtol=lt, atol=lt)
+    assert torch.allclose(la_l, la_f, rtol=lt, atol=lt)
+    assert torch.isfinite(el).all()
+
+
+def test_float32_matches_float64_4096():
+    s, c64 = _ctx("N2", torch.float64)
+    _, c32 = _ctx("N2", torch.float32)
+    x = _walkers(s, 4096, seed=3)
+    e64, l64, g64 = c64.local_energy(torch.tensor(x, device="cuda"), want_logabs=True, want_grad=True)
+    e32, l32, g32 = c32.local_energy(torch.tensor(x, dtype=torch.float32, device="cuda"), want_logabs=True,
+                                     want_grad=True)
+    torch.cuda.synchronize()
+    l64, l32 = l64.cpu().numpy(), l32.double().cpu().numpy()
+    np.testing.assert_allclose(l32, l64, rtol=1e-4, atol=1e-3)
+    e64, e32 = e64.cpu().numpy(), e32.double().cpu().numpy()
+    rel = np.abs(e32 - e64) / (np.abs(e64) + 1.0)
+    # fp32 forward Laplacian: median relative error ~1e-6, worst case near nodes larger
+    assert np.median(rel) < 1e-4, np.median(rel)
+    assert np.mean(rel < 1e-2) > 0.99
+
+
+def test_philox_mc_is_deterministic_and_sane():
+    s, ctx = _ctx("N2", torch.float32)
+    x0 = torch.tensor(_walkers(s, 4096, seed=4), dtype=torch.float32, device="cuda")
+    a = x0.clone().contiguous()
+    b = x0.clone().contiguous()
+    acc_a = ctx.mc_step(a, 3, 0.05, seed=7, offset=11, count_accepts=True)
+    ctx.mc_step(b, 3, 0.05, seed=7, offset=11)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert torch.isfinite(a).all()
+    moved = (a - x0).abs().reshape(4096, 14, 3).amax(-1) > 0
+    rate = float(acc_a.sum()) / (4096 * 14 * 3)
+    assert 0.05 < rate < 1.0, rate
+    assert 0.05 < float(moved.float().mean()) <= 1.0
+    c = x0.clone().contiguous()
+    ctx.mc_step(c, 3, 0.05, seed=8, offset=11)
+    assert not torch.equal(a, c)
+
+
+@pytest.mark.parametrize("B", [0, 1, 3, 65, 1000])
+def test_ragged_batches_match_full_batch(B):
+    s, ctx = _ctx("N2", torch.float64)
+    x = torch.tensor(_walkers(s, 1000, seed=6), device="cuda")
+    e_full, l_full, g_full = ctx.local_energy(x, want_logabs=True, want_grad=True)
+    e, l, g = ctx.local_energy(x[:B], want_logabs=True, want_grad=True)
+    la, gr = ctx.logpsi_grad(x[:B])
+    torch.cuda.synchronize()
+    assert e.shape == (B,)
+    if B:
+        assert torch.equal(e, e_full[:B]) and torch.equal(l, l_full[:B]) and torch.equal(g, g_full[:B])
+        assert torch.allclose(gr, g_full[:B], rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("name", ["H2", "Be", "C", "Ne", "C2"])
+def test_other_shapes_reverse_vs_forward(name):
+    s, ctx = _ctx(name, torch.float64)
+    pos = torch.tensor(_walkers(s, 256), device="cuda")
+    la_r, g_r = ctx.logpsi_grad(pos)
+    la_f, g_f = ctx.logpsi_grad_forward_mode(pos)
+    torch.cuda.synchronize()
+    assert torch.allclose(g_r, g_f, rtol=1e-8, atol=1e-8)
+    assert torch.allclose(la_r, la_f, rtol=1e-10, atol=1e-10)
