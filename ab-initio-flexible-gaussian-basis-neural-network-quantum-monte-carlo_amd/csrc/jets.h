@@ -42,7 +42,7 @@ template <typename T> __device__ __forceinline__ T f_exp(T x);
 template <> __device__ __forceinline__ float f_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 template <> __device__ __forceinline__ double f_exp(double x) { return exp(x); }
 template <typename T> __device__ __forceinline__ T f_log(T x);
-template <> __device__ __forceinline__ float f_log(float x) { return logf(x); }
+template <> __device__ __forceinline__ float f_log(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
 template <> __device__ __forceinline__ double f_log(double x) { return log(x); }
 // tanh(x) = 1 - 2/(1 + e^{2x}); saturates correctly at +-inf (abs. error ~1e-7 in float)
 template <typename T> __device__ __forceinline__ T f_tanh(T x);

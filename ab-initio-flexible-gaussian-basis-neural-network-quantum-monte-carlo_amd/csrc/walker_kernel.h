@@ -24,6 +24,7 @@
 #pragma once
 #include "jets.h"
 #include "layout.h"
+#include "gj.h"
 
 namespace aq {
 
@@ -62,7 +63,7 @@ struct Smem {
   static constexpr int yv = hb + N * 4 * NC * 64;
   static constexpr int ph = yv + N * N;
   static constexpr int mx = ph + N * N * 2;
-  static constexpr int fac = mx + N * 2 * N * 2;
+  static constexpr int fac = mx + N * N * 2;
   static constexpr int qs = fac + N * 2;
   static constexpr int end = qs + (LAP ? N * N * 8 : N * 8);
   static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
@@ -258,7 +259,6 @@ __global__ __launch_bounds__(64) void k_walker(KArgs ka) {
   using Ly = Lay<N, A>;
   using SM = Smem<T, N, LAP>;
   constexpr int NC = SM::NC;
-  constexpr int N2 = 2 * N;
   const T* __restrict__ P = (const T*)ka.prm;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   T* sm = (T*)smem_raw;
@@ -267,7 +267,6 @@ __global__ __launch_bounds__(64) void k_walker(KArgs ka) {
   T* Yv = sm + SM::yv;
   T* Ph = sm + SM::ph;
   T* Mx = sm + SM::mx;
-  T* fac = sm + SM::fac;
   T* Qs = sm + SM::qs;
 
   const int conf = blockIdx.x;
@@ -451,77 +450,16 @@ __global__ __launch_bounds__(64) void k_walker(KArgs ka) {
     im += P[Ly::orb_b + (sp * N + col) * 2 + 1];
     Ph[idx * 2 + 0] = re;
     Ph[idx * 2 + 1] = im;
-    const T yv = Yv[idx];
-    Mx[(r * N2 + col) * 2 + 0] = re * yv;
-    Mx[(r * N2 + col) * 2 + 1] = im * yv;
-    Mx[(r * N2 + N + col) * 2 + 0] = (r == col) ? T(1) : T(0);
-    Mx[(r * N2 + N + col) * 2 + 1] = T(0);
   }
   __syncthreads();
 
   // ------------------------------------------------------------------ Gauss-Jordan with partial pivoting
   // (replaces jnp.linalg.slogdet, network_blocks.py:156; pivot = first max |re|+|im| as LAPACK izamax)
-  T logdet = T(0), phr = T(1), phi = T(0);
-  for (int k = 0; k < N; ++k) {
-    T key = T(-1);
-    int kid = lane;
-    if (lane >= k && lane < N) key = f_abs(Mx[(lane * N2 + k) * 2]) + f_abs(Mx[(lane * N2 + k) * 2 + 1]);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const T ok = __shfl_xor(key, off);
-      const int oi = __shfl_xor(kid, off);
-      if (ok > key || (ok == key && oi < kid)) {
-        key = ok;
-        kid = oi;
-      }
-    }
-    const int p = __builtin_amdgcn_readfirstlane(kid);
-    if (p != k) {
-      if (lane < 2 * N2) {
-        const T a = Mx[k * N2 * 2 + lane];
-        const T b = Mx[p * N2 * 2 + lane];
-        Mx[k * N2 * 2 + lane] = b;
-        Mx[p * N2 * 2 + lane] = a;
-      }
-      phr = -phr;
-      phi = -phi;
-    }
-    __syncthreads();
-    const T pr = Mx[(k * N2 + k) * 2], pim = Mx[(k * N2 + k) * 2 + 1];
-    const T mag = f_hypot(pr, pim);
-    logdet += f_log(mag);
-    {
-      const T ur = pr / mag, ui = pim / mag;
-      const T nr = phr * ur - phi * ui, ni = phr * ui + phi * ur;
-      phr = nr;
-      phi = ni;
-    }
-    const T den = pr * pr + pim * pim;
-    const T ir = pr / den, ii = -pim / den;
-    if (lane < N) {
-      fac[lane * 2 + 0] = Mx[(lane * N2 + k) * 2 + 0];
-      fac[lane * 2 + 1] = Mx[(lane * N2 + k) * 2 + 1];
-    }
-    __syncthreads();
-    if (lane < N2) {
-      const T mr = Mx[(k * N2 + lane) * 2], mi = Mx[(k * N2 + lane) * 2 + 1];
-      Mx[(k * N2 + lane) * 2] = mr * ir - mi * ii;
-      Mx[(k * N2 + lane) * 2 + 1] = mr * ii + mi * ir;
-    }
-    __syncthreads();
-    for (int idx = lane; idx < N * N2; idx += 64) {
-      const int j = idx / N2, col = idx - j * N2;
-      if (j != k) {
-        const T fr = fac[j * 2], fi = fac[j * 2 + 1];
-        const T kr = Mx[(k * N2 + col) * 2], ki = Mx[(k * N2 + col) * 2 + 1];
-        Mx[(j * N2 + col) * 2] -= fr * kr - fi * ki;
-        Mx[(j * N2 + col) * 2 + 1] -= fr * ki + fi * kr;
-      }
-    }
-    __syncthreads();
-  }
-#define BINV_RE(c, s) Mx[((c) * N2 + N + (s)) * 2]
-#define BINV_IM(c, s) Mx[((c) * N2 + N + (s)) * 2 + 1]
+  T logdet, phr, phi;
+  gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi);   // Mx now holds B = A^{-1} [N][N][2]
+  __syncthreads();
+#define BINV_RE(c, s) Mx[((c) * N + (s)) * 2]
+#define BINV_IM(c, s) Mx[((c) * N + (s)) * 2 + 1]
 
   // ------------------------------------------------------------------ Q_f = P_f B  (diagonal only for gradients)
   if constexpr (LAP) {
