@@ -29,29 +29,29 @@ struct SmemRev {
   static constexpr int D0 = 4 * A;               // layer-0 h width
   static constexpr int DFM = 3 * D0 + 8;         // widest conv input (layer 0)
   static constexpr int QM = DFM / 4;
+  static constexpr int hl_n = N * D0 + 3 * N * 4;
+  static constexpr int cmax(int a, int b) { return a > b ? a : b; }
   static constexpr int xs = 0;                   // 48
   static constexpr int hl = 48;                  // h^0 [N][D0], h^1..h^3 [N][4]
-  static constexpr int hl_n = N * D0 + 3 * N * 4;
   static constexpr int g1 = hl + hl_n;           // [3][2][D0]
-  static constexpr int cq = g1 + 3 * 2 * D0;     // [3][N][QM]
-  static constexpr int sv = cq + 3 * N * QM;     // [3][N][4]
-  static constexpr int p2 = sv + 3 * N * 4;      // [3][N][N][4] pair values
-  static constexpr int g2 = p2 + 3 * N * N * 4;  // [3][2][N][4]
-  static constexpr int yv = g2 + 3 * 2 * N * 4;  // [N][N]
-  static constexpr int ph = yv + N * N;          // [N][N][2]
-  static constexpr int mx = ph + N * N * 2;      // B = A^{-1} [N][N][2]
-  static constexpr int fac = mx + N * N * 2;     // (unused)
-  static constexpr int ybar = fac + N * 2;       // [N][N]
-  static constexpr int hbar = ybar + N * N;      // adjoints of h^0..h^3 (same layout as hl)
+  static constexpr int cq = g1 + 3 * 2 * D0;     // [3][N][QM]  conv outputs (kept for backward)
+  static constexpr int sv = cq + 3 * N * QM;     // [3][N][4]   single outputs
+  static constexpr int g2 = sv + 3 * N * 4;      // [3][2][N][4] g2 values (forward) / adjoints (backward)
+  static constexpr int yv = g2 + 3 * 2 * N * 4;  // [N][N]  Yt
+  // region R, lifetimes disjoint: {Phi [N][N][2], B [N][N][2]} (F5..B1) -> fbar (B2) -> dbar (B3..B4)
+  static constexpr int R = yv + N * N;
+  static constexpr int ph = R;
+  static constexpr int mx = R + N * N * 2;
+  static constexpr int fbar = R;                 // [N][DFM]
+  static constexpr int dbar = R;                 // [N][N][3]
+  static constexpr int R_n = cmax(cmax(4 * N * N, N * DFM), 3 * N * N);
+  static constexpr int ybar = R + R_n;           // [N][N]
+  static constexpr int hbar = ybar + N * N;      // adjoints of h^0..h^3 (layout of hl)
   static constexpr int zsb = hbar + hl_n;        // [N][4]
-  static constexpr int fbar = zsb + N * 4;       // [N][DFM]
-  static constexpr int gsum = fbar + N * DFM;    // [2][D0]
-  static constexpr int g2b = gsum + 2 * D0;      // [3][2][N][4]
-  static constexpr int dbar = g2b + 3 * 2 * N * 4;  // [N][N][3]
-  static constexpr int red = dbar + N * N * 3;   // 64 scratch
-  static constexpr int end = red + 64;
+  static constexpr int gsum = zsb + N * 4;       // [2][D0]
+  static constexpr int loc = gsum + 2 * D0;      // [N + D0][48] electron-local Jacobians (direction lanes)
+  static constexpr int end = loc + (N + D0) * 48;
   static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
-  // offset of h^l inside the hl / hbar blocks
   static constexpr int hoff(int l) { return l == 0 ? 0 : N * D0 + (l - 1) * N * 4; }
 };
 
@@ -205,82 +205,95 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
     }
     env = s1 + s2;
   }
+  // d(Yt row)/dx and d(ae features)/dx of this lane's electron: kept lane-private in LDS until B4
   T* Yv = sm + SM::yv;
-  T Yd1[N];
+  T* loc = sm + SM::loc;
 #pragma unroll
   for (int col = 0; col < N; ++col) {
     PJ<T> s = P[Ly::wy + col] * yst[0];
 #pragma unroll
     for (int m = 1; m < NYW; ++m) s = s + P[Ly::wy + m * N + col] * yst[m];
     const PJ<T> yt = env * s;
-    Yd1[col] = yt.d1;
+    if (lane < 48) loc[col * 48 + lane] = yt.d1;
     if (val && live) Yv[er * N + col] = yt.v;
   }
-  T hfd1[D0];
 #pragma unroll
   for (int m = 0; m < D0; ++m) {
-    hfd1[m] = hf[m].d1;
+    if (lane < 48) loc[(N + m) * 48 + lane] = hf[m].d1;
     if (val && live) sm[SM::hl + er * D0 + m] = hf[m].v;
   }
   T jv = (val && live) ? jae.v : T(0);
   T jd1 = dir ? jae.d1 : T(0);
   __syncthreads();
 
-  // ------------------------------------------------------------------ F2 pair stream values (all N^2 pairs)
-  T* p2 = sm + SM::p2;
-  for (int it = lane; it < N * N; it += 64) {
-    const int k = it / N, i = it - k * N;
-    T p[4];
-    if (k == i) {
-#pragma unroll
-      for (int f = 0; f < 4; ++f) p[f] = T(0);
-    } else {
-      T d[3];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) d[c] = xs[i * 3 + c] - xs[k * 3 + c];
-      const T r = f_sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
-      p[0] = r;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) p[1 + c] = d[c];
-      if (k < i) {
-        const T cusp = P[Ly::jee_c + k * N + i], al = P[Ly::jee_a + k * N + i];
-        jv += f_div(cusp * r, al * r + T(1));
-      }
-    }
-#pragma unroll
-    for (int f = 0; f < 4; ++f) p2[((0 * N + k) * N + i) * 4 + f] = p[f];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const T* dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
-      const T* db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
-      T q[4];
-#pragma unroll
-      for (int o = 0; o < 4; ++o) {
-        T s = db[o];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) s += p[m] * dw[m * 4 + o];
-        q[o] = f_tanh(s);
-      }
-#pragma unroll
-      for (int o = 0; o < 4; ++o) {
-        p[o] = (p[o] + q[o]) * RSQ2;
-        p2[(((j + 1) * N + k) * N + i) * 4 + o] = p[o];
-      }
-    }
-  }
-  __syncthreads();
-
-  // ------------------------------------------------------------------ F3 g2[l][G][i][f] = mean_{k in G} h2^l[k,i,f]
+  // ------------------------------------------------------------------ F2+F3 pair stream + spin-group column means
+  // lane = (column i, quarter kq): pairs (k, i) with k = kq, kq+4, ...; the three layers'
+  // h2[k,i] values are summed per spin group in registers and quad-reduced with DPP.
   T* g2 = sm + SM::g2;
-  for (int it = lane; it < 3 * 2 * N * 4; it += 64) {
-    const int f = it & 3;
-    const int i = (it >> 2) % N;
-    const int G = ((it >> 2) / N) & 1;
-    const int l = (it >> 2) / (2 * N);
-    const int k0 = G ? nup : 0, k1 = G ? N : nup;
-    T s = T(0);
-    for (int k = k0; k < k1; ++k) s += p2[((l * N + k) * N + i) * 4 + f];
-    g2[it] = s * (G ? ginv1 : ginv0);
+  {
+    const int i = lane >> 2, kq = lane & 3;
+    const bool icol = i < N;
+    const int ii = icol ? i : N - 1;
+    T acc[3][2][4];
+#pragma unroll
+    for (int l = 0; l < 3; ++l)
+#pragma unroll
+      for (int G = 0; G < 2; ++G)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) acc[l][G][f] = T(0);
+#pragma unroll
+    for (int t = 0; t < (N + 3) / 4; ++t) {
+      const int k = kq + 4 * t;
+      if (k < N) {
+        const bool diag = (k == ii);
+        T d[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) d[c] = xs[ii * 3 + c] - xs[k * 3 + c];
+        const T r2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+        const T r = f_sqrt(diag ? T(1) : r2);
+        T p[4] = {diag ? T(0) : r, diag ? T(0) : d[0], diag ? T(0) : d[1], diag ? T(0) : d[2]};
+        if (icol && k < ii) {
+          const T cusp = P[Ly::jee_c + k * N + ii], al = P[Ly::jee_a + k * N + ii];
+          jv += f_div(cusp * r, al * r + T(1));
+        }
+        const bool G1 = k >= nup;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          acc[0][0][f] += G1 ? T(0) : p[f];
+          acc[0][1][f] += G1 ? p[f] : T(0);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const T* dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
+          const T* db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
+          T q[4];
+#pragma unroll
+          for (int o = 0; o < 4; ++o) {
+            T s = db[o];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) s += p[m] * dw[m * 4 + o];
+            q[o] = f_tanh(s);
+          }
+#pragma unroll
+          for (int o = 0; o < 4; ++o) {
+            p[o] = (p[o] + q[o]) * RSQ2;
+            acc[j + 1][0][o] += G1 ? T(0) : p[o];
+            acc[j + 1][1][o] += G1 ? p[o] : T(0);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < 3; ++l)
+#pragma unroll
+      for (int G = 0; G < 2; ++G)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          T v = acc[l][G][f];
+          v += dpp<0xB1>(v);
+          v += dpp<0x4E>(v);
+          if (icol && kq == 0) g2[((l * 2 + G) * N + i) * 4 + f] = v * (G ? ginv1 : ginv0);
+        }
   }
   __syncthreads();
 
@@ -389,7 +402,7 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
   T* zsb = sm + SM::zsb;
   T* fbar = sm + SM::fbar;
   T* gsum = sm + SM::gsum;
-  T* g2b = sm + SM::g2b;
+  T* g2b = sm + SM::g2;    // forward g2 values are dead after F4: reuse for their adjoints
 #pragma unroll
   for (int l = 2; l >= 0; --l) {
     const int d1 = l == 0 ? D0 : NH;
@@ -518,9 +531,9 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
       g += dbar[(k * N + le) * 3 + c] - dbar[(le * N + k) * 3 + c];
     }
 #pragma unroll
-    for (int col = 0; col < N; ++col) g += ybar[le * N + col] * Yd1[col];
+    for (int col = 0; col < N; ++col) g += ybar[le * N + col] * loc[col * 48 + (lane < 48 ? lane : 47)];
 #pragma unroll
-    for (int m = 0; m < D0; ++m) g += hbar[le * D0 + m] * hfd1[m];
+    for (int m = 0; m < D0; ++m) g += hbar[le * D0 + m] * loc[(N + m) * 48 + (lane < 48 ? lane : 47)];
   }
 
   // ------------------------------------------------------------------ outputs
