@@ -22,14 +22,24 @@ using namespace aq;
 // ============================================================================ small kernels
 
 // v2 = sum(x[0..n)) ; taueff = (sqrt(1 + 2 tau a v2) - 1)/(a v2), a = 0.25  (VMCmcstep.py:11-14)
+// One 1024-thread block; each thread keeps all its loads in flight (fixed summation
+// order, so the result is deterministic).
 template <typename T>
-__global__ __launch_bounds__(256) void k_taueff(const T* __restrict__ x, int n, double tstep, double* out) {
-  __shared__ double red[256];
-  double s = 0.0;
-  for (int i = threadIdx.x; i < n; i += 256) s += (double)x[i];
-  red[threadIdx.x] = s;
+__global__ __launch_bounds__(1024) void k_taueff(const T* __restrict__ x, int n, double tstep, double* out) {
+  __shared__ double red[1024];
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int i = threadIdx.x;
+  for (; i + 3 * 1024 < n; i += 4 * 1024) {
+    const T a = x[i], b = x[i + 1024], c = x[i + 2048], d = x[i + 3072];
+    s0 += (double)a;
+    s1 += (double)b;
+    s2 += (double)c;
+    s3 += (double)d;
+  }
+  for (; i < n; i += 1024) s0 += (double)x[i];
+  red[threadIdx.x] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
+  for (int w = 512; w > 0; w >>= 1) {
     if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
@@ -350,9 +360,9 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
     timed(c, 1, s, [&] { ops.walker(c->dtype, MODE_GRAD, ka, B, s); });
     // (2) limdrift factor over the device batch (:60)
     if (c->dtype == AIQMC_F32)
-      k_taueff<float><<<dim3(1), dim3(256), 0, s>>>((const float*)c->d_sq, B, tstep, c->d_taueff);
+      k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)c->d_sq, B, tstep, c->d_taueff);
     else
-      k_taueff<double><<<dim3(1), dim3(256), 0, s>>>((const double*)c->d_sq, B, tstep, c->d_taueff);
+      k_taueff<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)c->d_sq, B, tstep, c->d_taueff);
     // (3) single-electron proposals x^(i): value + gradient (:55-79, :95-97)
     KArgs kp = base_args(c);
     kp.nconf = B * N;
@@ -370,10 +380,10 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
     timed(c, 0, s, [&] { ops.walker(c->dtype, MODE_GRAD, kp, B * N, s); });
     // (4) limdrift factor of the proposal gradients over all B*N*3N entries (:80)
     if (c->dtype == AIQMC_F32)
-      k_taueff<float><<<dim3(1), dim3(256), 0, s>>>((const float*)c->d_sqn, B * N, tstep,
+      k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)c->d_sqn, B * N, tstep,
                          c->d_taueff + 1);
     else
-      k_taueff<double><<<dim3(1), dim3(256), 0, s>>>((const double*)c->d_sqn, B * N, tstep,
+      k_taueff<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)c->d_sqn, B * N, tstep,
                          c->d_taueff + 1);
     // (5) acceptance and move (:83-106)
     ops.accept(c->dtype, pos, c->d_grad, c->d_gown, c->d_lp, c->d_lpn, g1, g2, uu, c->d_taueff, B, tstep, seed, step,

@@ -1,0 +1,69 @@
+"""The reference-shaped Python API (make_ai_net / local_energy / main_monte_carlo)
+driven exactly like main_all_electrons_adam_muti_GPU.py:104-197, vs the oracle."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(name="Be", B=16, dtype=torch.float64):
+    from oracle import system
+    from aiqmc import spin_indices
+    from aiqmc.wavefunction_Ynlm import nn
+    from aiqmc.initial_electrons_positions.init import init_electrons
+    s = system.make_system(name)
+    par, anti, npar, nanti = spin_indices.jastrow_indices_ee(spins=s.spins, nelectrons=s.nelectrons)
+    up, dn = spin_indices.spin_indices_h(s.spins)
+    network = nn.make_ai_net(ndim=3, nelectrons=s.nelectrons, natoms=s.natoms, nspins=s.nspins, determinants=1,
+                             charges=s.charges, parallel_indices=par, antiparallel_indices=anti,
+                             n_parallel=npar, n_antiparallel=nanti, spin_up_indices=up, spin_down_indices=dn)
+    params = system.init_params(np.random.default_rng(3), s, randomize_aux=True)
+    pos, spins = init_electrons(7, None, s.atoms, s.charges, s.spins, B, 1.0)
+    atoms = np.tile(s.atoms[None], (B, 1, 1))          # batch-tiled, as the driver does
+    charges = np.tile(s.charges[None], (B, 1))
+    data = nn.AINetData(positions=pos.to("cuda", dtype).contiguous(), spins=spins, atoms=atoms,
+                        charges=charges)
+    return s, network, params, data
+
+
+def test_apply_and_local_energy_match_oracle():
+    from oracle import hamiltonian, network as onet
+    from aiqmc.Energy import hamiltonian as H
+    s, network, params, data = _setup()
+    phase, logabs = network.apply(params, data.positions, data.spins, data.atoms, data.charges)
+    el_fn = H.local_energy(f=network.apply, charges=s.charges, nspins=s.spins)
+    e_l, mat = el_fn(params, None, data)
+    assert mat is None
+    net = onet.Network(s)
+    e_ref, l_ref, _ = hamiltonian.batch_local_energy(net, onet.to_torch(params), data.positions.cpu())
+    np.testing.assert_allclose(logabs.cpu().numpy(), l_ref.numpy(), rtol=1e-10, atol=1e-10)
+    assert np.max(np.abs(e_l.cpu().numpy() - e_ref.numpy())) < 1e-6
+    ke = H.local_kinetic_energy(network.apply, complex_output=False)(params, data)
+    assert torch.isfinite(ke).all()
+
+
+def test_main_monte_carlo_host_draws_match_oracle():
+    from oracle import mcstep, network as onet
+    from aiqmc.VMC import VMCmcstep
+    s, network, params, data = _setup(B=8)
+    N, B, nsteps = s.nelectrons, 8, 2
+    rng = np.random.default_rng(9)
+    g1 = torch.tensor(rng.standard_normal((nsteps, B, 3 * N)))
+    g2 = torch.tensor(rng.standard_normal((nsteps, B, N, 3 * N)))
+    u = torch.tensor(rng.uniform(size=(nsteps, B, N)))
+    x0 = data.positions.cpu().clone()
+    mc_step = VMCmcstep.main_monte_carlo(f=network.apply, tstep=0.05, ndim=3, nelectrons=N, nsteps=nsteps,
+                                         batch_size=B)
+    out = mc_step(params, data, VMCmcstep.HostDraws(g1, g2, u))
+    ref = mcstep.mc_step(onet.Network(s), onet.to_torch(params), x0, g1, g2, u, 0.05, nsteps)
+    np.testing.assert_allclose(out.positions.cpu().numpy(), ref.numpy(), rtol=1e-9, atol=1e-9)
+    assert out.positions.data_ptr() == data.positions.data_ptr()     # in place (donate_argnums analogue)
+
+
+def test_param_update_is_picked_up():
+    s, network, params, data = _setup(B=4)
+    _, l1 = network.apply(params, data.positions, None, data.atoms, None)
+    params["orbitals"][0]["b"] = params["orbitals"][0]["b"] + 0.5
+    _, l2 = network.apply(params, data.positions, None, data.atoms, None)
+    assert not torch.allclose(l1, l2)
