@@ -52,6 +52,26 @@ __global__ __launch_bounds__(1024) void k_taueff(const T* __restrict__ x, int n,
   }
 }
 
+// Per-sweep random draws (production mode), one thread per (walker b, electron i):
+// gauss1[b][3i..3i+2], gauss2[b][i][0..2] standard normals, u[b][i] in [0,1) --
+// the same buffers the caller supplies in AIQMC_RNG_HOST mode.
+template <typename T>
+__global__ __launch_bounds__(256) void k_draws(uint64_t seed, uint64_t step, int B, int N, T* __restrict__ g1,
+                                               T* __restrict__ g2, T* __restrict__ u) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * N) return;
+  float a[3], b[3], c[4];
+  philox_normal3f(seed, step, (uint32_t)t, 0u, a);
+  philox_normal3f(seed, step, (uint32_t)t, 1u, b);
+  philox_u4(seed, step, (uint32_t)t, 2u, c);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    g1[(size_t)t * 3 + k] = (T)a[k];
+    g2[(size_t)t * 3 + k] = (T)b[k];
+  }
+  u[t] = (T)(c[0] - 5.9604644775390625e-08f);   // [0,1)
+}
+
 // ============================================================================ host side
 
 static thread_local std::string g_err;
@@ -104,10 +124,11 @@ static void timed(aiqmc_ctx* c, int slot, hipStream_t s, F&& fn) {
 }
 
 static void free_ws(aiqmc_ctx* c) {
-  void* ps[] = {c->d_grad, c->d_lp, c->d_sq, c->d_lpn, c->d_gown, c->d_sqn, c->d_taueff};
+  void* ps[] = {c->d_grad, c->d_lp, c->d_sq, c->d_lpn, c->d_gown, c->d_sqn, c->d_taueff, c->d_g1, c->d_g2, c->d_u};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   c->d_grad = c->d_lp = c->d_sq = c->d_lpn = c->d_gown = c->d_sqn = nullptr;
+  c->d_g1 = c->d_g2 = c->d_u = nullptr;
   c->d_taueff = nullptr;
   c->ws_B = 0;
   c->ws_bytes = 0;
@@ -118,10 +139,11 @@ static int ensure_ws(aiqmc_ctx* c, int B) {
   free_ws(c);
   const size_t s = c->dtype == AIQMC_F32 ? 4 : 8;
   const size_t N = (size_t)c->N;
-  size_t bytes[6] = {B * 3 * N * s, B * s, B * s, B * N * s, B * N * 3 * s, B * N * s};
-  void** ptrs[6] = {&c->d_grad, &c->d_lp, &c->d_sq, &c->d_lpn, &c->d_gown, &c->d_sqn};
+  size_t bytes[9] = {B * 3 * N * s, B * s, B * s, B * N * s, B * N * 3 * s, B * N * s,
+                     B * N * 3 * s, B * N * 3 * s, B * N * s};
+  void** ptrs[9] = {&c->d_grad, &c->d_lp, &c->d_sq, &c->d_lpn, &c->d_gown, &c->d_sqn, &c->d_g1, &c->d_g2, &c->d_u};
   int64_t tot = 0;
-  for (int k = 0; k < 6; ++k) {
+  for (int k = 0; k < 9; ++k) {
     HIPCHK(hipMalloc(ptrs[k], bytes[k]));
     tot += (int64_t)bytes[k];
   }
@@ -347,9 +369,25 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
   const size_t es = c->dtype == AIQMC_F32 ? 4 : 8;
   for (int st = 0; st < nsteps; ++st) {
     const uint64_t step = offset + (uint64_t)st;
-    const char* g1 = rng_mode == AIQMC_RNG_HOST ? (const char*)gauss1 + (size_t)st * B * 3 * N * es : nullptr;
-    const char* g2 = rng_mode == AIQMC_RNG_HOST ? (const char*)gauss2 + (size_t)st * B * N * 3 * es : nullptr;
-    const char* uu = rng_mode == AIQMC_RNG_HOST ? (const char*)u + (size_t)st * B * N * es : nullptr;
+    const char* g1;
+    const char* g2;
+    const char* uu;
+    if (rng_mode == AIQMC_RNG_HOST) {
+      g1 = (const char*)gauss1 + (size_t)st * B * 3 * N * es;
+      g2 = (const char*)gauss2 + (size_t)st * B * N * 3 * es;
+      uu = (const char*)u + (size_t)st * B * N * es;
+    } else {
+      const int nb = (B * N + 255) / 256;
+      if (c->dtype == AIQMC_F32)
+        k_draws<float><<<dim3(nb), dim3(256), 0, s>>>(seed, step, B, N, (float*)c->d_g1, (float*)c->d_g2,
+                                                       (float*)c->d_u);
+      else
+        k_draws<double><<<dim3(nb), dim3(256), 0, s>>>(seed, step, B, N, (double*)c->d_g1, (double*)c->d_g2,
+                                                        (double*)c->d_u);
+      g1 = (const char*)c->d_g1;
+      g2 = (const char*)c->d_g2;
+      uu = (const char*)c->d_u;
+    }
     // (1) grad log|psi| at the walkers (VMCmcstep.py:41-53)
     KArgs ka = base_args(c);
     ka.nconf = B;
@@ -386,7 +424,7 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
       k_taueff<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)c->d_sqn, B * N, tstep,
                          c->d_taueff + 1);
     // (5) acceptance and move (:83-106)
-    ops.accept(c->dtype, pos, c->d_grad, c->d_gown, c->d_lp, c->d_lpn, g1, g2, uu, c->d_taueff, B, tstep, seed, step,
+    ops.accept(c->dtype, pos, c->d_grad, c->d_gown, c->d_lp, c->d_lpn, g1, g2, uu, c->d_taueff, B, tstep,
                accept_out, s);
   }
   HIPCHK(hipGetLastError());

@@ -30,6 +30,7 @@ struct aiqmc_ctx {
   int ws_B = 0;
   void *d_grad = nullptr, *d_lp = nullptr, *d_sq = nullptr, *d_lpn = nullptr, *d_gown = nullptr,
        *d_sqn = nullptr;
+  void *d_g1 = nullptr, *d_g2 = nullptr, *d_u = nullptr;   // per-sweep Philox draws
   double* d_taueff = nullptr;
   int64_t ws_bytes = 0;
   // optional per-kernel HIP-event timing (aiqmc_profile_*): slot -> recorded (start, stop) pairs
@@ -43,7 +44,7 @@ struct ShapeOps {
   void (*walker)(int dtype, int mode, const KArgs& ka, int nconf, hipStream_t s);
   void (*accept)(int dtype, void* pos, const void* grad, const void* gown, const void* lp, const void* lpn,
                  const void* g1, const void* g2, const void* u, const double* te, int B, double tstep,
-                 uint64_t seed, uint64_t step, int32_t* acc, hipStream_t s);
+                 int32_t* acc, hipStream_t s);
   int64_t nkern;
   long (*ncanon)(int npar, int nanti);
   void (*pack)(const aiqmc_ctx* c, const double* flat, std::vector<double>& out);

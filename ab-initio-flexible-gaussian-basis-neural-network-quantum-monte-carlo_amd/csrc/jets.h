@@ -214,24 +214,25 @@ __host__ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k
   }
 }
 
-// 4 uniforms in (0,1] from (seed, step, stream id, kind)
-__device__ __forceinline__ void philox_uniform4(uint64_t seed, uint64_t step, uint32_t sid, uint32_t kind,
-                                                double u[4]) {
+// 4 uniforms from (seed, step, stream id, kind): u in (0,1] (24-bit grid)
+__device__ __forceinline__ void philox_u4(uint64_t seed, uint64_t step, uint32_t sid, uint32_t kind, float u[4]) {
   uint32_t c[4] = {sid, (uint32_t)step, (uint32_t)(step >> 32), kind};
   philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
 #pragma unroll
-  for (int j = 0; j < 4; ++j) u[j] = ((double)c[j] + 1.0) * 2.3283064365386963e-10;   // (0,1]
+  for (int j = 0; j < 4; ++j) u[j] = (float)((c[j] >> 8) + 1u) * 5.9604644775390625e-08f;
 }
-// 3 standard normals (Box-Muller on 4 uniforms)
-template <typename T>
-__device__ __forceinline__ void philox_normal3(uint64_t seed, uint64_t step, uint32_t sid, uint32_t kind, T out[3]) {
-  double u[4];
-  philox_uniform4(seed, step, sid, kind, u);
-  const double r0 = sqrt(-2.0 * log(u[0])), r1 = sqrt(-2.0 * log(u[2]));
-  const double tp = 6.283185307179586;
-  out[0] = (T)(r0 * cos(tp * u[1]));
-  out[1] = (T)(r0 * sin(tp * u[1]));
-  out[2] = (T)(r1 * cos(tp * u[3]));
+// 3 standard normals (Box-Muller on 4 uniforms, float math)
+__device__ __forceinline__ void philox_normal3f(uint64_t seed, uint64_t step, uint32_t sid, uint32_t kind,
+                                                float out[3]) {
+  float u[4];
+  philox_u4(seed, step, sid, kind, u);
+  const float r0 = sqrtf(-2.0f * __logf(u[0])), r1 = sqrtf(-2.0f * __logf(u[2]));
+  float s0, c0, s1, c1;
+  __sincosf(6.283185307179586f * u[1], &s0, &c0);
+  __sincosf(6.283185307179586f * u[3], &s1, &c1);
+  out[0] = r0 * c0;
+  out[1] = r0 * s0;
+  out[2] = r1 * c1;
 }
 
 }  // namespace aq

@@ -24,7 +24,7 @@ __global__ __launch_bounds__(256) void k_accept(T* __restrict__ pos, const T* __
                                                 const T* __restrict__ lpn, const T* __restrict__ gauss1,
                                                 const T* __restrict__ gauss2, const T* __restrict__ u,
                                                 const double* __restrict__ taueff, int B, double tstep_d,
-                                                uint64_t seed, uint64_t step, int32_t* accept_count) {
+                                                int32_t* accept_count) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= B * N) return;
   const int b = t / N, i = t - b * N;
@@ -32,21 +32,12 @@ __global__ __launch_bounds__(256) void k_accept(T* __restrict__ pos, const T* __
   const T sq = sqrt(tstep);
   const T te1 = (T)taueff[0], te2 = (T)taueff[1];
   T z1[3], z2[3];
-  T uu;
-  if (gauss1) {
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      z1[c] = gauss1[(size_t)b * 3 * N + 3 * i + c];
-      z2[c] = gauss2[((size_t)b * N + i) * 3 + c];
-    }
-    uu = u[(size_t)b * N + i];
-  } else {
-    philox_normal3<T>(seed, step, (uint32_t)(b * N + i), 0u, z1);
-    philox_normal3<T>(seed, step, (uint32_t)(b * N + i), 1u, z2);
-    double uv[4];
-    philox_uniform4(seed, step, (uint32_t)(b * N + i), 2u, uv);
-    uu = (T)(uv[0] - 2.3283064365386963e-10);   // [0,1)
+  for (int c = 0; c < 3; ++c) {
+    z1[c] = gauss1[(size_t)b * 3 * N + 3 * i + c];
+    z2[c] = gauss2[((size_t)b * N + i) * 3 + c];
   }
+  const T uu = u[(size_t)b * N + i];
   T gmove[3];
   T tp = T(0);
 #pragma unroll
@@ -228,13 +219,13 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
 template <int N, int A>
 static void accept_impl(int dtype, void* pos, const void* grad, const void* gown, const void* lp, const void* lpn,
                         const void* g1, const void* g2, const void* u, const double* te, int B, double tstep,
-                        uint64_t seed, uint64_t step, int32_t* acc, hipStream_t s) {
+                        int32_t* acc, hipStream_t s) {
   const int nt = B * N;
   const int nb = (nt + 255) / 256;
   if (dtype == AIQMC_F32)
-    k_accept<float, N><<<dim3(nb), dim3(256), 0, s>>>((float*)pos, (const float*)grad, (const float*)gown, (const float*)lp, (const float*)lpn, (const float*)g1, (const float*)g2, (const float*)u, te, B, tstep, seed, step, acc);
+    k_accept<float, N><<<dim3(nb), dim3(256), 0, s>>>((float*)pos, (const float*)grad, (const float*)gown, (const float*)lp, (const float*)lpn, (const float*)g1, (const float*)g2, (const float*)u, te, B, tstep, acc);
   else
-    k_accept<double, N><<<dim3(nb), dim3(256), 0, s>>>((double*)pos, (const double*)grad, (const double*)gown, (const double*)lp, (const double*)lpn, (const double*)g1, (const double*)g2, (const double*)u, te, B, tstep, seed, step, acc);
+    k_accept<double, N><<<dim3(nb), dim3(256), 0, s>>>((double*)pos, (const double*)grad, (const double*)gown, (const double*)lp, (const double*)lpn, (const double*)g1, (const double*)g2, (const double*)u, te, B, tstep, acc);
 }
 
 

@@ -25,6 +25,7 @@
 #include "jets.h"
 #include "layout.h"
 #include "gj.h"
+#include "electron.h"
 
 namespace aq {
 
@@ -42,7 +43,7 @@ struct KArgs {
   // by  grad_eff*tstep + sqrt(tstep)*gauss1  (VMCmcstep.py:58-78)
   int proposal;
   const void* pgrad;      // [B][3N] grad log|psi| at the walkers
-  const void* gauss1;     // [B][3N] standard normals (host rng) or nullptr (philox)
+  const void* gauss1;     // [B][3N] standard normals (host draws or k_draws output)
   const double* taueff;   // device scalar: limdrift factor of pgrad (VMCmcstep.py:11-14)
   double tstep;
   uint64_t seed, step;
@@ -289,15 +290,7 @@ __global__ __launch_bounds__(64) void k_walker(KArgs ka) {
   if (lane < 3 * N) {
     T x = ((const T*)ka.pos)[(size_t)pb * 3 * N + lane];
     if (ka.proposal && lane / 3 == pi) {
-      T z;
-      if (ka.gauss1) {
-        z = ((const T*)ka.gauss1)[(size_t)pb * 3 * N + lane];
-      } else {
-        T g3[3];
-        philox_normal3<T>(ka.seed, ka.step, (uint32_t)(pb * N + pi), 0u, g3);
-        const int c = lane - 3 * pi;
-        z = c == 0 ? g3[0] : (c == 1 ? g3[1] : g3[2]);
-      }
+      const T z = ((const T*)ka.gauss1)[(size_t)pb * 3 * N + lane];   // drawn by the host or k_draws
       const T ge = ((const T*)ka.pgrad)[(size_t)pb * 3 * N + lane] * (T)(*ka.taueff);
       x = x + (ge * tstep + f_sqrt(tstep) * z);
     }
@@ -305,112 +298,13 @@ __global__ __launch_bounds__(64) void k_walker(KArgs ka) {
   }
   __syncthreads();
 
-  // ------------------------------------------------------------------ per-electron stage (lanes of electron le)
-  PJ<T> xe[3];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) xe[c] = PJ<T>{xs[le * 3 + c], (lc == c) ? T(1) : T(0), T(0)};
-  PJ<T> hf[4 * A];
-  PJ<T> yin[4 * A + 2];
-  PJ<T> ra[A];
-  PJ<T> aev[A][3];
-  PJ<T> hisum = pjc(T(0)), spsum = pjc(T(0));
-  T vv = T(0);
-  {
-    const T PI = T(3.141592653589793);
-    const T c0 = T(0.5) * f_sqrt(T(1) / PI), c1 = f_sqrt(T(3) / (T(4) * PI));
-    const T k15h = T(0.5) * f_sqrt(T(15) / PI), k5q = T(0.25) * f_sqrt(T(5) / PI);
-    const T k15q = T(0.25) * f_sqrt(T(15) / PI), k35 = T(0.25) * f_sqrt(T(35) / (T(2) * PI));
-    const T k105h = T(0.5) * f_sqrt(T(105) / PI), k21 = T(0.25) * f_sqrt(T(21) / (T(2) * PI));
-    const T k7 = T(0.25) * f_sqrt(T(7) / PI), k105q = T(0.25) * f_sqrt(T(105) / PI);
-#pragma unroll
-    for (int a = 0; a < A; ++a) {
-      PJ<T> ae[3];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) ae[c] = xe[c] - P[Ly::atoms + a * 3 + c];   // nn.py:111
-      const PJ<T> r = pj_sqrt(ae[0] * ae[0] + ae[1] * ae[1] + ae[2] * ae[2]);   // nn.py:113
-      ra[a] = r;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) aev[a][c] = ae[c];
-      hf[4 * a] = r;                                                       // nn.py:134-136
-#pragma unroll
-      for (int c = 0; c < 3; ++c) hf[4 * a + 1 + c] = ae[c];
-      const PJ<T> x0 = ae[0] / r, x1 = ae[1] / r, x2 = ae[2] / r;          // nn.py:327
-      yin[4 * a + 0] = pjc(c0);                                            // nn.py:164-167
-      yin[4 * a + 1] = c1 * x0;
-      yin[4 * a + 2] = c1 * x1;
-      yin[4 * a + 3] = c1 * x2;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) spsum = spsum + yin[4 * a + m];
-      // nn.py:182-193 with y = r and x[3] -> x[2] (Q3)
-      const PJ<T> y2 = r * r, y3 = y2 * r;
-      const PJ<T> x00 = x0 * x0, x11 = x1 * x1, x22 = x2 * x2;
-      hisum = hisum + k15h * (x0 * x1 / y2);
-      hisum = hisum + k15h * (x1 * x2 / y2);
-      hisum = hisum + k5q * ((T(3) * x22 - y2) / y2);
-      hisum = hisum + k15h * (x0 * x2 / y2);
-      hisum = hisum + k15q * ((x00 - x11) / y2);
-      hisum = hisum + k35 * ((x1 * (T(3) * x00 - x11)) / y3);
-      hisum = hisum + k105h * (x0 * x1 * x2 / y3);
-      hisum = hisum + k21 * ((x1 * (T(5) * x22 - y2)) / y3);
-      hisum = hisum + k7 * ((T(5) * (x22 * x2) - T(3) * x2 * y2) / y3);
-      hisum = hisum + k21 * ((x0 * (T(5) * x22 - y2)) / y3);
-      hisum = hisum + k105q * (((x00 - x11) * x2) / y3);
-      hisum = hisum + k35 * ((x0 * (x00 - T(3) * x11)) / y3);
-      vv += (val && live) ? -P[Ly::charges + a] / r.v : T(0);             // hamiltonian.py:190-198
-    }
-  }
-  yin[4 * A] = hisum / T(12 * A);                                          // nn.py:336-339
-  yin[4 * A + 1] = spsum / T(4 * A);
-  // Ynlm stream (nn.py:313-319, 340-341)
-  PJ<T> yst[NYW];
-  {
-    constexpr int DY0 = Ly::DY0;
-#pragma unroll
-    for (int o = 0; o < NYW; ++o) {
-      PJ<T> s = P[Ly::y_w0 + o] * yin[0];
-#pragma unroll
-      for (int m = 1; m < DY0; ++m) s = s + P[Ly::y_w0 + m * NYW + o] * yin[m];
-      yst[o] = pj_tanh(s + P[Ly::y_b0 + o]);
-      if constexpr (DY0 == NYW) yst[o] = T(0.70710678118654752) * (yin[o] + yst[o]);
-    }
-#pragma unroll
-    for (int l = 1; l < 3; ++l) {
-      const int wo = l == 1 ? Ly::y_w1 : Ly::y_w2;
-      const int bo = l == 1 ? Ly::y_b1 : Ly::y_b2;
-      PJ<T> nx[NYW];
-#pragma unroll
-      for (int o = 0; o < NYW; ++o) {
-        PJ<T> s = P[wo + o] * yst[0];
-#pragma unroll
-        for (int m = 1; m < NYW; ++m) s = s + P[wo + m * NYW + o] * yst[m];
-        nx[o] = pj_tanh(s + P[bo + o]);
-      }
-#pragma unroll
-      for (int o = 0; o < NYW; ++o) yst[o] = T(0.70710678118654752) * (yst[o] + nx[o]);
-    }
-  }
-  // envelope of electron le (envelope.py:26-30, Q1) and e-n Jastrow (Jastrow.py:84-93)
-  PJ<T> env = pjc(T(0)), jae = pjc(T(0));
-  {
-    const T alpha = P[Ly::env_alpha + le], xi = P[Ly::env_xi + le];
-    PJ<T> s1 = pjc(T(0)), s2 = pjc(T(0));
-#pragma unroll
-    for (int a = 0; a < A; ++a) {
-      const T beta = P[Ly::env_beta + le * A + a];
-      s1 = s1 + alpha * pj_exp(-beta * (ra[a] * ra[a]));
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const T pi_ = P[Ly::env_pi + (le * A + a) * 3 + c];
-        const T sg = P[Ly::env_sigma + (le * A + a) * 3 + c];
-        s2 = s2 + (sg * xi) * pj_exp(-pi_ * aev[a][c]);
-      }
-      const T bj = P[Ly::jae_b + le * A + a];
-      const T c34 = P[Ly::c34 + a], c14 = P[Ly::c14 + a];
-      const PJ<T> ex = pj_exp(-(c14 * bj) * ra[a]);
-      jae = jae + (-c34 * (pjc(T(1)) - ex)) / (T(2) * bj);
-    }
-    env = s1 + s2;
-  }
+  // ------------------------------------------------------------------ per-electron stage (electron.h)
+  ElecOut<T, A> eo;
+  electron_stage<T, N, A>(P, xs, le, lc, eo);
+  const PJ<T>* hf = eo.hf;
+  const PJ<T>* yst = eo.yst;
+  const PJ<T> env = eo.env, jae = eo.jae;
+  T vv = (val && live) ? eo.ven : T(0);
   // Yt row of electron le: env * (y . What)   (nn.py:449-452, 479-485)
   T Yd1[N], Yd2[N];
 #pragma unroll
