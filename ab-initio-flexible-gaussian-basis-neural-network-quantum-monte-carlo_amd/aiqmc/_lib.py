@@ -19,13 +19,17 @@ AIQMC_F64 = 1
 AIQMC_RNG_HOST = 0
 AIQMC_RNG_PHILOX = 1
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaiqmc_hip.so")
+# AIQMC_LIB_VARIANT=phaseprof selects the diagnostics build (make -C csrc phaseprof)
+_VARIANT = os.environ.get("AIQMC_LIB_VARIANT", "")
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                        "libaiqmc_hip.so" if not _VARIANT else f"libaiqmc_hip_{_VARIANT}.so")
 
 EXPORTED_SYMBOLS = (
     "aiqmc_create", "aiqmc_destroy", "aiqmc_param_count", "aiqmc_set_params",
     "aiqmc_logpsi", "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_mc_step",
     "aiqmc_workspace_bytes", "aiqmc_last_error", "aiqmc_supported_shapes",
     "aiqmc_profile_enable", "aiqmc_profile_read", "aiqmc_debug_logpsi_grad_forward",
+    "aiqmc_debug_set_proposal_reuse", "aiqmc_debug_phase_cycles",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -81,6 +85,10 @@ def load() -> ctypes.CDLL:
                                   ctypes.c_uint64, ctypes.c_uint64, vp, vp]
     lib.aiqmc_debug_logpsi_grad_forward.argtypes = [vp, vp, i32, vp, vp, vp]
     lib.aiqmc_debug_logpsi_grad_forward.restype = ctypes.c_int
+    lib.aiqmc_debug_set_proposal_reuse.argtypes = [vp, i32]
+    lib.aiqmc_debug_set_proposal_reuse.restype = ctypes.c_int
+    lib.aiqmc_debug_phase_cycles.argtypes = [vp, vp]
+    lib.aiqmc_debug_phase_cycles.restype = ctypes.c_int
     lib.aiqmc_profile_enable.argtypes = [vp, i32]
     lib.aiqmc_profile_read.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64)]
     lib.aiqmc_last_error.restype = ctypes.c_char_p
@@ -235,6 +243,17 @@ class Context:
         check(self._lib.aiqmc_debug_logpsi_grad_forward(self._h, _ptr(p), B, _ptr(logabs), _ptr(grad),
                                                         _stream(self.device)), "aiqmc_debug_logpsi_grad_forward")
         return logabs, grad
+
+    def set_proposal_reuse(self, on: bool):
+        """Diagnostics: proposals from the walker cache (default) or recomputed from scratch."""
+        check(self._lib.aiqmc_debug_set_proposal_reuse(self._h, 1 if on else 0), "aiqmc_debug_set_proposal_reuse")
+
+    def phase_cycles(self):
+        """Diagnostics (AQ_PHASE_PROF builds): per-phase cycle sums [32], then cleared."""
+        import numpy as np
+        out = np.zeros(32, dtype=np.uint64)
+        check(self._lib.aiqmc_debug_phase_cycles(self._h, out.ctypes.data), "aiqmc_debug_phase_cycles")
+        return out
 
     def local_energy(self, pos: torch.Tensor, want_logabs: bool = False, want_grad: bool = False,
                      out: Optional[torch.Tensor] = None):

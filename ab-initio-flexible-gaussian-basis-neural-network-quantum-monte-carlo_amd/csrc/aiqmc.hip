@@ -124,11 +124,13 @@ static void timed(aiqmc_ctx* c, int slot, hipStream_t s, F&& fn) {
 }
 
 static void free_ws(aiqmc_ctx* c) {
-  void* ps[] = {c->d_grad, c->d_lp, c->d_sq, c->d_lpn, c->d_gown, c->d_sqn, c->d_taueff, c->d_g1, c->d_g2, c->d_u};
+  void* ps[] = {c->d_grad, c->d_lp, c->d_sq, c->d_lpn, c->d_gown, c->d_sqn, c->d_taueff, c->d_g1, c->d_g2, c->d_u,
+                c->d_wc, c->d_ec};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   c->d_grad = c->d_lp = c->d_sq = c->d_lpn = c->d_gown = c->d_sqn = nullptr;
   c->d_g1 = c->d_g2 = c->d_u = nullptr;
+  c->d_wc = c->d_ec = nullptr;
   c->d_taueff = nullptr;
   c->ws_B = 0;
   c->ws_bytes = 0;
@@ -139,11 +141,15 @@ static int ensure_ws(aiqmc_ctx* c, int B) {
   free_ws(c);
   const size_t s = c->dtype == AIQMC_F32 ? 4 : 8;
   const size_t N = (size_t)c->N;
-  size_t bytes[9] = {B * 3 * N * s, B * s, B * s, B * N * s, B * N * 3 * s, B * N * s,
-                     B * N * 3 * s, B * N * 3 * s, B * N * s};
-  void** ptrs[9] = {&c->d_grad, &c->d_lp, &c->d_sq, &c->d_lpn, &c->d_gown, &c->d_sqn, &c->d_g1, &c->d_g2, &c->d_u};
+  ShapeOps ops;
+  shape_ops(c->N, c->A, &ops);
+  size_t bytes[11] = {B * 3 * N * s, B * s, B * s, B * N * s, B * N * 3 * s, B * N * s,
+                      B * N * 3 * s, B * N * 3 * s, B * N * s, B * (size_t)ops.wcache_n * s,
+                      B * N * (size_t)ops.ecache_n * s};
+  void** ptrs[11] = {&c->d_grad, &c->d_lp, &c->d_sq, &c->d_lpn, &c->d_gown, &c->d_sqn, &c->d_g1, &c->d_g2, &c->d_u,
+                     &c->d_wc, &c->d_ec};
   int64_t tot = 0;
-  for (int k = 0; k < 9; ++k) {
+  for (int k = 0; k < 11; ++k) {
     HIPCHK(hipMalloc(ptrs[k], bytes[k]));
     tot += (int64_t)bytes[k];
   }
@@ -395,6 +401,7 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
     ka.logabs = c->d_lp;
     ka.grad = c->d_grad;
     ka.sumsq = c->d_sq;
+    ka.wcache = c->reuse ? c->d_wc : nullptr;
     timed(c, 1, s, [&] { ops.walker(c->dtype, MODE_GRAD, ka, B, s); });
     // (2) limdrift factor over the device batch (:60)
     if (c->dtype == AIQMC_F32)
@@ -415,6 +422,12 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
     kp.logabs = c->d_lpn;
     kp.gown = c->d_gown;
     kp.sumsq = c->d_sqn;
+    if (c->reuse) {
+      // moved electron's local stage for all B*N proposals, then proposals from the walker caches
+      kp.wcache = c->d_wc;
+      kp.ecache = c->d_ec;
+      ops.moved(c->dtype, kp, s);
+    }
     timed(c, 0, s, [&] { ops.walker(c->dtype, MODE_GRAD, kp, B * N, s); });
     // (4) limdrift factor of the proposal gradients over all B*N*3N entries (:80)
     if (c->dtype == AIQMC_F32)
@@ -471,6 +484,22 @@ int aiqmc_debug_logpsi_grad_forward(aiqmc_ctx* c, const void* pos, int32_t B, vo
   ka.grad = grad;
   ops.walker(c->dtype, MODE_GRAD_FWD, ka, B, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_debug_set_proposal_reuse(aiqmc_ctx* c, int32_t on) {
+  if (!c) return fail(AIQMC_EINVAL, "null context");
+  c->reuse = on != 0;
+  return AIQMC_OK;
+}
+
+int aiqmc_debug_phase_cycles(aiqmc_ctx* c, uint64_t* out32) {
+  if (!c || !out32) return fail(AIQMC_EINVAL, "null argument");
+  ShapeOps ops;
+  shape_ops(c->N, c->A, &ops);
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipDeviceSynchronize());
+  ops.phase_read((unsigned long long*)out32);
   return AIQMC_OK;
 }
 

@@ -31,6 +31,8 @@ struct aiqmc_ctx {
   void *d_grad = nullptr, *d_lp = nullptr, *d_sq = nullptr, *d_lpn = nullptr, *d_gown = nullptr,
        *d_sqn = nullptr;
   void *d_g1 = nullptr, *d_g2 = nullptr, *d_u = nullptr;   // per-sweep Philox draws
+  void *d_wc = nullptr, *d_ec = nullptr;                    // Metropolis caches (walker_rev.h WCache/ECache)
+  bool reuse = true;                                        // proposals reuse the walker's cached stage
   double* d_taueff = nullptr;
   int64_t ws_bytes = 0;
   // optional per-kernel HIP-event timing (aiqmc_profile_*): slot -> recorded (start, stop) pairs
@@ -45,6 +47,9 @@ struct ShapeOps {
   void (*accept)(int dtype, void* pos, const void* grad, const void* gown, const void* lp, const void* lpn,
                  const void* g1, const void* g2, const void* u, const double* te, int B, double tstep,
                  int32_t* acc, hipStream_t s);
+  void (*moved)(int dtype, const KArgs& ka, hipStream_t s);   // k_moved_electron over ka.nconf proposals
+  void (*phase_read)(unsigned long long* out32);               // AQ_PHASE_PROF builds only
+  int wcache_n, ecache_n;                                      // cache entries per walker / per proposal
   int64_t nkern;
   long (*ncanon)(int npar, int nanti);
   void (*pack)(const aiqmc_ctx* c, const double* flat, std::vector<double>& out);

@@ -30,13 +30,14 @@ struct ElecOut {
   T ven;
 };
 
+// xpos: the 3 coordinates of electron le; le selects the per-electron parameters.
 template <typename T, int N, int A>
-__device__ __forceinline__ void electron_stage(const T* __restrict__ P, const T* xs, int le, int lc,
+__device__ __forceinline__ void electron_stage(const T* __restrict__ P, const T* xpos, int le, int lc,
                                                ElecOut<T, A>& o) {
   using Ly = Lay<N, A>;
   PJ<T> xe[3];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) xe[c] = PJ<T>{xs[le * 3 + c], (lc == c) ? T(1) : T(0), T(0)};
+  for (int c = 0; c < 3; ++c) xe[c] = PJ<T>{xpos[c], (lc == c) ? T(1) : T(0), T(0)};
   PJ<T> yin[4 * A + 2];
   PJ<T> ra[A];
   PJ<T> aev[A][3];

@@ -217,6 +217,15 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
 }
 
 template <int N, int A>
+static void moved_impl(int dtype, const KArgs& ka, hipStream_t s) {
+  const int nb = (ka.nconf + 15) / 16;
+  if (dtype == AIQMC_F32)
+    k_moved_electron<float, N, A><<<dim3(nb), dim3(64), 0, s>>>(ka);
+  else
+    k_moved_electron<double, N, A><<<dim3(nb), dim3(64), 0, s>>>(ka);
+}
+
+template <int N, int A>
 static void accept_impl(int dtype, void* pos, const void* grad, const void* gown, const void* lp, const void* lpn,
                         const void* g1, const void* g2, const void* u, const double* te, int B, double tstep,
                         int32_t* acc, hipStream_t s) {
@@ -229,12 +238,26 @@ static void accept_impl(int dtype, void* pos, const void* grad, const void* gown
 }
 
 
+static void phase_read_impl(unsigned long long* out) {
+#ifdef AQ_PHASE_PROF
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(aq_phase_cycles), 32 * sizeof(unsigned long long));
+  unsigned long long z[32] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(aq_phase_cycles), z, sizeof(z));
+#else
+  for (int k = 0; k < 32; ++k) out[k] = 0;
+#endif
+}
+
 #define AQ_CAT2(a, b, c) aiqmc_shape_ops_##a##_##b##c
 #define AQ_CAT(a, b) AQ_CAT2(a, b, )
 bool AQ_CAT(AQ_N, AQ_A)(ShapeOps* ops) {
   ops->set_lds = &set_lds_impl<AQ_N, AQ_A>;
   ops->walker = &walker_impl<AQ_N, AQ_A>;
   ops->accept = &accept_impl<AQ_N, AQ_A>;
+  ops->moved = &moved_impl<AQ_N, AQ_A>;
+  ops->phase_read = &phase_read_impl;
+  ops->wcache_n = WCache<AQ_N, AQ_A>::size;
+  ops->ecache_n = ECache<AQ_N, AQ_A>::size;
   ops->nkern = Lay<AQ_N, AQ_A>::total;
   ops->ncanon = &Lay<AQ_N, AQ_A>::canon;
   ops->pack = &pack_params<AQ_N, AQ_A>;

@@ -47,6 +47,9 @@ struct KArgs {
   const double* taueff;   // device scalar: limdrift factor of pgrad (VMCmcstep.py:11-14)
   double tstep;
   uint64_t seed, step;
+  // Metropolis caches (walker_rev.h WCache / ECache); nullptr outside aiqmc_mc_step
+  void* wcache;
+  void* ecache;
   // outputs (nullable)
   void* logabs;           // [nconf]
   void* phase;            // [nconf]
@@ -300,7 +303,7 @@ __global__ __launch_bounds__(64) void k_walker(KArgs ka) {
 
   // ------------------------------------------------------------------ per-electron stage (electron.h)
   ElecOut<T, A> eo;
-  electron_stage<T, N, A>(P, xs, le, lc, eo);
+  electron_stage<T, N, A>(P, xs + le * 3, le, lc, eo);
   const PJ<T>* hf = eo.hf;
   const PJ<T>* yst = eo.yst;
   const PJ<T> env = eo.env, jae = eo.jae;

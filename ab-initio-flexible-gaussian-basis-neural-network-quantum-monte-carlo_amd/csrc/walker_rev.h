@@ -25,6 +25,22 @@
 
 namespace aq {
 
+// Diagnostics build (-DAQ_PHASE_PROF): per-phase shader-clock cycles summed over
+// waves, [0..15] walker launches, [16..31] proposal launches (aiqmc_debug_phase_cycles).
+#ifdef AQ_PHASE_PROF
+static __device__ unsigned long long aq_phase_cycles[32];
+#define AQ_PH(k)                                                                         \
+  do {                                                                                   \
+    const unsigned long long t_ = __builtin_readcyclecounter();                          \
+    if (lane == 0) atomicAdd(&aq_phase_cycles[(ka.proposal ? 16 : 0) + (k)], t_ - t_ph); \
+    t_ph = t_;                                                                           \
+  } while (0)
+#else
+#define AQ_PH(k) \
+  do {           \
+  } while (0)
+#endif
+
 template <typename T, int N, int A>
 struct SmemRev {
   static constexpr int D0 = 4 * A;               // layer-0 h width
@@ -45,7 +61,7 @@ struct SmemRev {
   static constexpr int mx = R + N * N * 2;
   static constexpr int fbar = R;                 // [N][DFM]
   static constexpr int dbar = R;                 // [N][N][3]
-  static constexpr int R_n = cmax(cmax(4 * N * N, N * DFM), 3 * N * N);
+  static constexpr int R_n = cmax(cmax(cmax(4 * N * N, N * DFM), 3 * N * N), 4 + 16 * 12);  // + reuse scratch
   static constexpr int ybar = R + R_n;           // [N][N]
   static constexpr int hbar = ybar + N * N;      // adjoints of h^0..h^3 (layout of hl)
   static constexpr int zsb = hbar + hl_n;        // [N][4]
@@ -55,6 +71,107 @@ struct SmemRev {
   static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
   static constexpr int hoff(int l) { return l == 0 ? 0 : N * D0 + (l - 1) * N * 4; }
 };
+
+// Per-walker cache written by the walker launch of a Metropolis sweep and read by
+// the N single-electron proposals of that walker (they differ from it in one
+// electron): electron-local stage of every electron and the spin-group column
+// sums of the pair stream.
+template <int N, int A>
+struct WCache {
+  static constexpr int D0 = 4 * A;
+  static constexpr int yv = 0;                      // [N][N]     Yt values
+  static constexpr int h0 = yv + N * N;             // [N][D0]    ae features
+  static constexpr int loc = h0 + N * D0;           // [N+D0][48] electron-local Jacobians
+  static constexpr int jaev = loc + (N + D0) * 48;  // [N]        J_ae per electron
+  static constexpr int jaed = jaev + N;             // [48]       dJ_ae/dx per direction lane
+  static constexpr int g2 = jaed + 48;              // [3][2][N][4]
+  static constexpr int jee = g2 + 3 * 2 * N * 4;    // [1]        J_ee
+  static constexpr int size = ((jee + 1 + 63) / 64) * 64;
+};
+// Per-proposal electron-local stage of the moved electron (k_moved_electron).
+template <int N, int A>
+struct ECache {
+  static constexpr int D0 = 4 * A;
+  static constexpr int yv = 0;          // [N]     Yt row values
+  static constexpr int h0 = N;          // [D0]    ae features
+  static constexpr int yd = N + D0;     // [3][N]  dYt/dx_c
+  static constexpr int hd = yd + 3 * N; // [3][D0] dfeat/dx_c
+  static constexpr int jv = hd + 3 * D0;
+  static constexpr int jd = jv + 1;     // [3]
+  static constexpr int size = ((jd + 3 + 15) / 16) * 16;
+};
+
+template <typename T, int N, int A>
+__device__ __forceinline__ void pair_values(const T d[3], const T* __restrict__ P, T out[3][4]) {
+  using Ly = Lay<N, A>;
+  const T RSQ2 = T(0.70710678118654752);
+  T p[4];
+  p[0] = f_sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) p[1 + c] = d[c];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) out[0][f] = p[f];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const T* dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
+    const T* db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
+    T q[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      T s = db[o];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) s += p[m] * dw[m * 4 + o];
+      q[o] = f_tanh(s);
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      p[o] = (p[o] + q[o]) * RSQ2;
+      out[j + 1][o] = p[o];
+    }
+  }
+}
+
+// Electron-local stage of the moved electron of proposals q = 16*block + s (lane = 16c + s).
+template <typename T, int N, int A>
+__global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
+  using Ly = Lay<N, A>;
+  using EC = ECache<N, A>;
+  constexpr int D0 = 4 * A;
+  const T* __restrict__ P = (const T*)ka.prm;
+  const int lane = threadIdx.x;
+  const int lc = lane >> 4, s = lane & 15;
+  const int q = blockIdx.x * 16 + s;
+  if (q >= ka.nconf) return;
+  const int b = q / N, i = q - b * N;
+  const T tstep = (T)ka.tstep;
+  const T te = (T)(*ka.taueff);
+  T xp[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const size_t o = (size_t)b * 3 * N + 3 * i + c;
+    const T ge = ((const T*)ka.pgrad)[o] * te;
+    xp[c] = ((const T*)ka.pos)[o] + (ge * tstep + f_sqrt(tstep) * ((const T*)ka.gauss1)[o]);
+  }
+  ElecOut<T, A> eo;
+  electron_stage<T, N, A>(P, xp, i, lc, eo);
+  T* E = (T*)ka.ecache + (size_t)q * EC::size;
+#pragma unroll
+  for (int col = 0; col < N; ++col) {
+    PJ<T> sy = P[Ly::wy + col] * eo.yst[0];
+#pragma unroll
+    for (int m = 1; m < NYW; ++m) sy = sy + P[Ly::wy + m * N + col] * eo.yst[m];
+    const PJ<T> yt = eo.env * sy;
+    if (lc == 3) E[EC::yv + col] = yt.v;
+    else E[EC::yd + lc * N + col] = yt.d1;
+  }
+#pragma unroll
+  for (int m = 0; m < D0; ++m) {
+    if (lc == 3) E[EC::h0 + m] = eo.hf[m].v;
+    else E[EC::hd + lc * D0 + m] = eo.hf[m].d1;
+  }
+  if (lc == 3) E[EC::jv] = eo.jae.v;
+  else E[EC::jd + lc] = eo.jae.d1;
+}
 
 template <typename T, int N, int A>
 __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
@@ -79,6 +196,9 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
   const T RSQ2 = T(0.70710678118654752);
   const T ginv0 = T(1) / T(nup), ginv1 = T(1) / T(N - nup);
   const int* rowsrc = ka.rowsrc;
+#ifdef AQ_PHASE_PROF
+  unsigned long long t_ph = __builtin_readcyclecounter();
+#endif
 
   // ------------------------------------------------------------------ F0 positions (as k_walker)
   int pb = conf, pi = -1;
@@ -91,110 +211,211 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
     if (ka.proposal && lane / 3 == pi) {
       const T z = ((const T*)ka.gauss1)[(size_t)pb * 3 * N + lane];   // drawn by the host or k_draws
       const T ge = ((const T*)ka.pgrad)[(size_t)pb * 3 * N + lane] * (T)(*ka.taueff);
+      sm[SM::R + (lane - 3 * pi)] = x;                       // old position of the moved electron
       x = x + (ge * tstep + f_sqrt(tstep) * z);
     }
     xs[lane] = x;
   }
   __syncthreads();
 
+  AQ_PH(0);
   // ------------------------------------------------------------------ F1 per-electron stage (electron.h)
-  ElecOut<T, A> eo;
-  electron_stage<T, N, A>(P, xs, le, lc, eo);
-  const PJ<T>* hf = eo.hf;
-  const PJ<T>* yst = eo.yst;
-  const PJ<T> env = eo.env, jae = eo.jae;
-  // d(Yt row)/dx and d(ae features)/dx of this lane's electron: kept lane-private in LDS until B4
+  using WC = WCache<N, A>;
+  using EC = ECache<N, A>;
+  const bool reuse = ka.proposal && ka.ecache != nullptr;
   T* Yv = sm + SM::yv;
   T* loc = sm + SM::loc;
+  T jv = T(0), jd1 = T(0), jve = T(0);
+  if (reuse) {
+    // walker b's cached stage, electron pi's entries from the moved-electron kernel
+    const T* Wb = (const T*)ka.wcache + (size_t)pb * WC::size;
+    const T* Eq = (const T*)ka.ecache + (size_t)conf * EC::size;
+    for (int idx = lane; idx < N * N; idx += 64) {
+      const int r = idx / N;
+      Yv[idx] = (r == pi) ? Eq[EC::yv + (idx - r * N)] : Wb[WC::yv + idx];
+    }
+    for (int idx = lane; idx < N * D0; idx += 64) {
+      const int e = idx / D0;
+      sm[SM::hl + idx] = (e == pi) ? Eq[EC::h0 + (idx - e * D0)] : Wb[WC::h0 + idx];
+    }
+    if (lane < 48) {
+      const bool mine = (er == pi);
+      const int c = lc;
 #pragma unroll
-  for (int col = 0; col < N; ++col) {
-    PJ<T> s = P[Ly::wy + col] * yst[0];
-#pragma unroll
-    for (int m = 1; m < NYW; ++m) s = s + P[Ly::wy + m * N + col] * yst[m];
-    const PJ<T> yt = env * s;
-    if (lane < 48) loc[col * 48 + lane] = yt.d1;
-    if (val && live) Yv[er * N + col] = yt.v;
+      for (int m = 0; m < N + D0; ++m) {
+        const T wv = Wb[WC::loc + m * 48 + lane];
+        const T ev = Eq[m < N ? EC::yd + c * N + m : EC::hd + c * D0 + (m - N)];
+        loc[m * 48 + lane] = mine ? ev : wv;
+      }
+    }
+    jv = (val && live) ? ((er == pi) ? Eq[EC::jv] : Wb[WC::jaev + er]) : T(0);
+    jd1 = dir ? ((le == pi) ? Eq[EC::jd + lc] : Wb[WC::jaed + lane]) : T(0);
+  } else {
+    ElecOut<T, A> eo;
+    electron_stage<T, N, A>(P, xs + le * 3, le, lc, eo);
+    const PJ<T>* hf = eo.hf;
+    const PJ<T>* yst = eo.yst;
+    const PJ<T> env = eo.env, jae = eo.jae;
+    // d(Yt row)/dx and d(ae features)/dx of this lane's electron: kept lane-private in LDS until B4
+      #pragma unroll
+    for (int col = 0; col < N; ++col) {
+      PJ<T> s = P[Ly::wy + col] * yst[0];
+  #pragma unroll
+      for (int m = 1; m < NYW; ++m) s = s + P[Ly::wy + m * N + col] * yst[m];
+      const PJ<T> yt = env * s;
+      if (lane < 48) loc[col * 48 + lane] = yt.d1;
+      if (val && live) Yv[er * N + col] = yt.v;
+    }
+  #pragma unroll
+    for (int m = 0; m < D0; ++m) {
+      if (lane < 48) loc[(N + m) * 48 + lane] = hf[m].d1;
+      if (val && live) sm[SM::hl + er * D0 + m] = hf[m].v;
+    }
+    jv = (val && live) ? jae.v : T(0);
+    jd1 = dir ? jae.d1 : T(0);
+    if (ka.wcache) {
+      T* Wb = (T*)ka.wcache + (size_t)conf * WC::size;
+      if (val && live) Wb[WC::jaev + er] = jae.v;
+      if (lane < 48) Wb[WC::jaed + lane] = dir ? jae.d1 : T(0);
+    }
   }
-#pragma unroll
-  for (int m = 0; m < D0; ++m) {
-    if (lane < 48) loc[(N + m) * 48 + lane] = hf[m].d1;
-    if (val && live) sm[SM::hl + er * D0 + m] = hf[m].v;
-  }
-  T jv = (val && live) ? jae.v : T(0);
-  T jd1 = dir ? jae.d1 : T(0);
   __syncthreads();
+  if (ka.wcache && !ka.proposal) {
+    T* Wb = (T*)ka.wcache + (size_t)conf * WC::size;
+    for (int idx = lane; idx < N * N; idx += 64) Wb[WC::yv + idx] = Yv[idx];
+    for (int idx = lane; idx < N * D0; idx += 64) Wb[WC::h0 + idx] = sm[SM::hl + idx];
+    if (lane < 48)
+      for (int m = 0; m < N + D0; ++m) Wb[WC::loc + m * 48 + lane] = loc[m * 48 + lane];
+  }
 
+  AQ_PH(1);
   // ------------------------------------------------------------------ F2+F3 pair stream + spin-group column means
   // lane = (column i, quarter kq): pairs (k, i) with k = kq, kq+4, ...; the three layers'
   // h2[k,i] values are summed per spin group in registers and quad-reduced with DPP.
   T* g2 = sm + SM::g2;
-  {
-    const int i = lane >> 2, kq = lane & 3;
-    const bool icol = i < N;
-    const int ii = icol ? i : N - 1;
-    T acc[3][2][4];
+  if (reuse) {
+    // walker b's sums, patched with the 2(N-1) pairs that involve the moved electron pi
+    const T* Wb = (const T*)ka.wcache + (size_t)pb * WC::size;
+    for (int idx = lane; idx < 3 * 2 * N * 4; idx += 64) g2[idx] = Wb[WC::g2 + idx];
+    T* S = sm + SM::R + 4;                          // [16][12] column-pi deltas
+    const T* xo = sm + SM::R;                       // old position of pi
+    __syncthreads();
+    if (lane < 32) {
+      const bool rowp = lane < 16;                  // rowp: pair (pi, j); else pair (k, pi)
+      const int o = lane & 15;
+      if (o < N && o != pi) {
+        T dn[3], dd[3];
 #pragma unroll
-    for (int l = 0; l < 3; ++l)
-#pragma unroll
-      for (int G = 0; G < 2; ++G)
-#pragma unroll
-        for (int f = 0; f < 4; ++f) acc[l][G][f] = T(0);
-#pragma unroll
-    for (int t = 0; t < (N + 3) / 4; ++t) {
-      const int k = kq + 4 * t;
-      if (k < N) {
-        const bool diag = (k == ii);
-        T d[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) d[c] = xs[ii * 3 + c] - xs[k * 3 + c];
-        const T r2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
-        const T r = f_sqrt(diag ? T(1) : r2);
-        T p[4] = {diag ? T(0) : r, diag ? T(0) : d[0], diag ? T(0) : d[1], diag ? T(0) : d[2]};
-        if (icol && k < ii) {
-          const T cusp = P[Ly::jee_c + k * N + ii], al = P[Ly::jee_a + k * N + ii];
-          jv += f_div(cusp * r, al * r + T(1));
+        for (int c = 0; c < 3; ++c) {
+          dn[c] = rowp ? xs[o * 3 + c] - xs[pi * 3 + c] : xs[pi * 3 + c] - xs[o * 3 + c];
+          dd[c] = rowp ? xs[o * 3 + c] - xo[c] : xo[c] - xs[o * 3 + c];
         }
-        const bool G1 = k >= nup;
+        T vn[3][4], vo[3][4];
+        pair_values<T, N, A>(dn, P, vn);
+        pair_values<T, N, A>(dd, P, vo);
+        if (rowp) {
+          const int Gp = pi >= nup ? 1 : 0;
+          const T gw = Gp ? ginv1 : ginv0;
 #pragma unroll
-        for (int f = 0; f < 4; ++f) {
-          acc[0][0][f] += G1 ? T(0) : p[f];
-          acc[0][1][f] += G1 ? p[f] : T(0);
-        }
+          for (int l = 0; l < 3; ++l)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const T* dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
-          const T* db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
-          T q[4];
+            for (int f = 0; f < 4; ++f) g2[((l * 2 + Gp) * N + o) * 4 + f] += (vn[l][f] - vo[l][f]) * gw;
+          const T cusp = P[Ly::jee_c + pi * N + o], al = P[Ly::jee_a + pi * N + o];
+          jve += f_div(cusp * vn[0][0], al * vn[0][0] + T(1)) - f_div(cusp * vo[0][0], al * vo[0][0] + T(1));
+        } else {
 #pragma unroll
-          for (int o = 0; o < 4; ++o) {
-            T s = db[o];
+          for (int l = 0; l < 3; ++l)
 #pragma unroll
-            for (int m = 0; m < 4; ++m) s += p[m] * dw[m * 4 + o];
-            q[o] = f_tanh(s);
-          }
-#pragma unroll
-          for (int o = 0; o < 4; ++o) {
-            p[o] = (p[o] + q[o]) * RSQ2;
-            acc[j + 1][0][o] += G1 ? T(0) : p[o];
-            acc[j + 1][1][o] += G1 ? p[o] : T(0);
-          }
+            for (int f = 0; f < 4; ++f) S[o * 12 + l * 4 + f] = vn[l][f] - vo[l][f];
         }
       }
     }
-#pragma unroll
-    for (int l = 0; l < 3; ++l)
-#pragma unroll
-      for (int G = 0; G < 2; ++G)
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-          T v = acc[l][G][f];
-          v += dpp<0xB1>(v);
-          v += dpp<0x4E>(v);
-          if (icol && kq == 0) g2[((l * 2 + G) * N + i) * 4 + f] = v * (G ? ginv1 : ginv0);
+    __syncthreads();
+    if (lane < 24) {
+      const int l = lane >> 3, G = (lane >> 2) & 1, f = lane & 3;
+      const int k0 = G ? nup : 0, k1 = G ? N : nup;
+      T acc = T(0);
+      for (int k = k0; k < k1; ++k)
+        if (k != pi) acc += S[k * 12 + l * 4 + f];
+      g2[((l * 2 + G) * N + pi) * 4 + f] += acc * (G ? ginv1 : ginv0);
+    }
+    if (lane == 0) jve += Wb[WC::jee];
+  } else {
+    {
+      const int i = lane >> 2, kq = lane & 3;
+      const bool icol = i < N;
+      const int ii = icol ? i : N - 1;
+      T acc[3][2][4];
+  #pragma unroll
+      for (int l = 0; l < 3; ++l)
+  #pragma unroll
+        for (int G = 0; G < 2; ++G)
+  #pragma unroll
+          for (int f = 0; f < 4; ++f) acc[l][G][f] = T(0);
+  #pragma unroll
+      for (int t = 0; t < (N + 3) / 4; ++t) {
+        const int k = kq + 4 * t;
+        if (k < N) {
+          const bool diag = (k == ii);
+          T d[3];
+  #pragma unroll
+          for (int c = 0; c < 3; ++c) d[c] = xs[ii * 3 + c] - xs[k * 3 + c];
+          const T r2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+          const T r = f_sqrt(diag ? T(1) : r2);
+          T p[4] = {diag ? T(0) : r, diag ? T(0) : d[0], diag ? T(0) : d[1], diag ? T(0) : d[2]};
+          if (icol && k < ii) {
+            const T cusp = P[Ly::jee_c + k * N + ii], al = P[Ly::jee_a + k * N + ii];
+            jve += f_div(cusp * r, al * r + T(1));
+          }
+          const bool G1 = k >= nup;
+  #pragma unroll
+          for (int f = 0; f < 4; ++f) {
+            acc[0][0][f] += G1 ? T(0) : p[f];
+            acc[0][1][f] += G1 ? p[f] : T(0);
+          }
+  #pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const T* dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
+            const T* db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
+            T q[4];
+  #pragma unroll
+            for (int o = 0; o < 4; ++o) {
+              T s = db[o];
+  #pragma unroll
+              for (int m = 0; m < 4; ++m) s += p[m] * dw[m * 4 + o];
+              q[o] = f_tanh(s);
+            }
+  #pragma unroll
+            for (int o = 0; o < 4; ++o) {
+              p[o] = (p[o] + q[o]) * RSQ2;
+              acc[j + 1][0][o] += G1 ? T(0) : p[o];
+              acc[j + 1][1][o] += G1 ? p[o] : T(0);
+            }
+          }
         }
+      }
+  #pragma unroll
+      for (int l = 0; l < 3; ++l)
+  #pragma unroll
+        for (int G = 0; G < 2; ++G)
+  #pragma unroll
+          for (int f = 0; f < 4; ++f) {
+            T v = acc[l][G][f];
+            v += dpp<0xB1>(v);
+            v += dpp<0x4E>(v);
+            if (icol && kq == 0) g2[((l * 2 + G) * N + i) * 4 + f] = v * (G ? ginv1 : ginv0);
+          }
+    }
   }
   __syncthreads();
+  if (ka.wcache && !ka.proposal) {
+    T* Wb = (T*)ka.wcache + (size_t)conf * WC::size;
+    for (int idx = lane; idx < 3 * 2 * N * 4; idx += 64) Wb[WC::g2 + idx] = g2[idx];
+    const T je = wave_sum(jve);
+    if (lane == 0) Wb[WC::jee] = je;
+  }
 
+  AQ_PH(2);
   // ------------------------------------------------------------------ F4 h-stream layers (values)
   T* hl = sm + SM::hl;
   T* g1 = sm + SM::g1;
@@ -246,6 +467,7 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
     __syncthreads();
   }
 
+  AQ_PH(3);
   // ------------------------------------------------------------------ F5 Phi, A = Phi * Yt, Gauss-Jordan -> B = A^{-1}
   T* Ph = sm + SM::ph;
   T* Mx = sm + SM::mx;
@@ -273,6 +495,7 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
 #define BRE(c, s) Mx[((c) * N + (s)) * 2]
 #define BIM(c, s) Mx[((c) * N + (s)) * 2 + 1]
 
+  AQ_PH(4);
   // ------------------------------------------------------------------ B1 adjoints of H (= h^3) and Yt
   T* hbar = sm + SM::hbar;
   T* ybar = sm + SM::ybar;
@@ -296,6 +519,7 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
 #undef BIM
   __syncthreads();
 
+  AQ_PH(5);
   // ------------------------------------------------------------------ B2 back through the h-stream layers
   T* zsb = sm + SM::zsb;
   T* fbar = sm + SM::fbar;
@@ -352,6 +576,7 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
     __syncthreads();
   }
 
+  AQ_PH(6);
   // ------------------------------------------------------------------ B3 pair adjoints d(logpsi)/d(x_i - x_k)
   T* dbar = sm + SM::dbar;
   for (int it = lane; it < N * (N - 1); it += 64) {
@@ -420,6 +645,7 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
   }
   __syncthreads();
 
+  AQ_PH(7);
   // ------------------------------------------------------------------ B4 gradient per direction lane (c, e)
   T g = jd1;
   {
@@ -434,10 +660,11 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
     for (int m = 0; m < D0; ++m) g += hbar[le * D0 + m] * loc[(N + m) * 48 + (lane < 48 ? lane : 47)];
   }
 
+  AQ_PH(8);
   // ------------------------------------------------------------------ outputs
   const T gd = dir ? g : T(0);
   const T sumsq = wave_sum(gd * gd);
-  const T lpsi = logdet + wave_sum(jv);
+  const T lpsi = logdet + wave_sum(jv + jve);
   if (ka.grad && dir) ((T*)ka.grad)[(size_t)conf * 3 * N + 3 * le + lc] = g;
   if (ka.gown && dir && le == pi) ((T*)ka.gown)[(size_t)conf * 3 + lc] = g;
   if (lane == 0) {
@@ -445,6 +672,7 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
     if (ka.phase) ((T*)ka.phase)[conf] = f_atan2(phi, phr);
     if (ka.sumsq) ((T*)ka.sumsq)[conf] = sumsq;
   }
+  AQ_PH(9);
 }
 
 }  // namespace aq

@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--system", default="N2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-walkers", type=int, default=8)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     return ap.parse_args()
 
 
@@ -124,14 +125,16 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+        dist.init_process_group(args.dist_backend if torch.cuda.is_available() else "gloo")
+    # one process per GPU; if fewer GPUs than ranks are visible (a rehearsal), ranks share devices
+    local_dev = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     dtype = torch.float32 if args.dtype == "f32" else torch.float64
     from aiqmc import constants, _lib
     from aiqmc.initial_electrons_positions.init import init_electrons
 
-    atoms, charges, spins, network, params, ctx = build(args.system, dtype, local_rank)
+    atoms, charges, spins, network, params, ctx = build(args.system, dtype, local_dev)
     N = int(charges.sum())
     B = args.walkers
     pos0, _ = init_electrons(1000 + rank, None, atoms, charges, spins, B, 1.0)

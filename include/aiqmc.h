@@ -119,6 +119,17 @@ int aiqmc_profile_read(aiqmc_ctx* ctx, int32_t slot, double* total_ms, int64_t* 
 int aiqmc_debug_logpsi_grad_forward(aiqmc_ctx* ctx, const void* pos, int32_t B, void* logabs, void* grad,
                                     void* stream);
 
+/* Diagnostics: aiqmc_mc_step evaluates each single-electron proposal from the
+ * walker's cached electron stage and pair sums, recomputing only the moved
+ * electron and its 2(N-1) pairs (default, on = 1).  on = 0 recomputes every
+ * proposal from scratch; both must agree to rounding. */
+int aiqmc_debug_set_proposal_reuse(aiqmc_ctx* ctx, int32_t on);
+
+/* Diagnostics: shader-clock cycles per phase of the reverse-mode kernel, summed
+ * over waves since the last call ([0..15] walker, [16..31] proposal launches);
+ * all zero unless the library was built with -DAQ_PHASE_PROF. */
+int aiqmc_debug_phase_cycles(aiqmc_ctx* ctx, uint64_t* out32);
+
 /* Bytes of device workspace the context holds (for memory planning). */
 int64_t aiqmc_workspace_bytes(const aiqmc_ctx* ctx);
 

@@ -111,3 +111,36 @@ def test_other_shapes_reverse_vs_forward(name):
     torch.cuda.synchronize()
     assert torch.allclose(g_r, g_f, rtol=1e-8, atol=1e-8)
     assert torch.allclose(la_r, la_f, rtol=1e-10, atol=1e-10)
+
+
+@pytest.mark.parametrize("name", ["H2", "Be", "C", "Ne", "C2", "N2"])
+def test_proposal_reuse_matches_recompute(name):
+    """Proposals from the walker cache (moved electron + its 2(N-1) pairs recomputed)
+    == proposals evaluated from scratch, on the same Philox draws."""
+    s, ctx = _ctx(name, torch.float64)
+    x0 = torch.tensor(_walkers(s, 512, seed=9), device="cuda")
+    a = x0.clone().contiguous()
+    b = x0.clone().contiguous()
+    ctx.set_proposal_reuse(True)
+    acc_a = ctx.mc_step(a, 4, 0.05, seed=3, offset=5, count_accepts=True)
+    ctx.set_proposal_reuse(False)
+    acc_b = ctx.mc_step(b, 4, 0.05, seed=3, offset=5, count_accepts=True)
+    ctx.set_proposal_reuse(True)
+    torch.cuda.synchronize()
+    assert torch.equal(acc_a, acc_b)
+    assert torch.allclose(a, b, rtol=0, atol=1e-11), float((a - b).abs().max())
+
+
+def test_proposal_reuse_matches_recompute_f32_4096():
+    s, ctx = _ctx("N2", torch.float32)
+    x0 = torch.tensor(_walkers(s, 4096, seed=10), dtype=torch.float32, device="cuda")
+    a = x0.clone().contiguous()
+    b = x0.clone().contiguous()
+    ctx.mc_step(a, 2, 0.05, seed=1, offset=0)
+    ctx.set_proposal_reuse(False)
+    ctx.mc_step(b, 2, 0.05, seed=1, offset=0)
+    ctx.set_proposal_reuse(True)
+    torch.cuda.synchronize()
+    # fp32 rounding may flip an acceptance whose ratio sits within ~1e-6 of its uniform
+    differ = ((a - b).abs().reshape(4096, -1).amax(1) > 1e-4).float().mean()
+    assert float(differ) < 2e-3, float(differ)
