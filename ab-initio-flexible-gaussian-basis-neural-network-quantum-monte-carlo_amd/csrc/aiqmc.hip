@@ -248,6 +248,7 @@ int aiqmc_destroy(aiqmc_ctx* c) {
   if (!c) return AIQMC_OK;
   (void)hipSetDevice(c->device);
   free_ws(c);
+  if (c->d_wcp) (void)hipFree(c->d_wcp);
   for (auto& v : c->ev_used)
     for (auto& p : v) {
       (void)hipEventDestroy(p.first);
@@ -313,6 +314,9 @@ int aiqmc_logpsi(aiqmc_ctx* c, const void* pos, int32_t B, void* logabs, void* p
   ka.pos = pos;
   ka.logabs = logabs;
   ka.phase = phase;
+  rc = ensure_ws(c, B);
+  if (rc) return rc;
+  ka.wcache = c->d_wc;   // the kernel keeps its electron-local Jacobians there
   ops.walker(c->dtype, MODE_GRAD, ka, B, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
@@ -330,6 +334,9 @@ int aiqmc_logpsi_grad(aiqmc_ctx* c, const void* pos, int32_t B, void* logabs, vo
   ka.pos = pos;
   ka.logabs = logabs;
   ka.grad = grad;
+  rc = ensure_ws(c, B);
+  if (rc) return rc;
+  ka.wcache = c->d_wc;
   ops.walker(c->dtype, MODE_GRAD, ka, B, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
@@ -370,6 +377,13 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
   if (rc) return rc;
   ShapeOps ops;
   shape_ops(c->N, c->A, &ops);
+  if (!c->reuse && c->wcp_B < B) {
+    if (c->d_wcp) (void)hipFree(c->d_wcp);
+    c->d_wcp = nullptr;
+    c->wcp_B = 0;
+    HIPCHK(hipMalloc(&c->d_wcp, (size_t)B * c->N * ops.wcache_n * (c->dtype == AIQMC_F32 ? 4 : 8)));
+    c->wcp_B = B;
+  }
   hipStream_t s = (hipStream_t)stream;
   const int N = c->N;
   const size_t es = c->dtype == AIQMC_F32 ? 4 : 8;
@@ -401,7 +415,7 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
     ka.logabs = c->d_lp;
     ka.grad = c->d_grad;
     ka.sumsq = c->d_sq;
-    ka.wcache = c->reuse ? c->d_wc : nullptr;
+    ka.wcache = c->d_wc;
     timed(c, 1, s, [&] { ops.walker(c->dtype, MODE_GRAD, ka, B, s); });
     // (2) limdrift factor over the device batch (:60)
     if (c->dtype == AIQMC_F32)
@@ -427,6 +441,8 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
       kp.wcache = c->d_wc;
       kp.ecache = c->d_ec;
       ops.moved(c->dtype, kp, s);
+    } else {
+      kp.wcache = c->d_wcp;   // per-proposal scratch of the same layout
     }
     timed(c, 0, s, [&] { ops.walker(c->dtype, MODE_GRAD, kp, B * N, s); });
     // (4) limdrift factor of the proposal gradients over all B*N*3N entries (:80)

@@ -32,6 +32,8 @@ struct aiqmc_ctx {
        *d_sqn = nullptr;
   void *d_g1 = nullptr, *d_g2 = nullptr, *d_u = nullptr;   // per-sweep Philox draws
   void *d_wc = nullptr, *d_ec = nullptr;                    // Metropolis caches (walker_rev.h WCache/ECache)
+  void* d_wcp = nullptr;                                    // per-proposal cache scratch (reuse off)
+  int wcp_B = 0;
   bool reuse = true;                                        // proposals reuse the walker's cached stage
   double* d_taueff = nullptr;
   int64_t ws_bytes = 0;

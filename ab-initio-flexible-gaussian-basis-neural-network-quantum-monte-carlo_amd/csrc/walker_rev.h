@@ -49,25 +49,25 @@ struct SmemRev {
   static constexpr int hl_n = N * D0 + 3 * N * 4;
   static constexpr int cmax(int a, int b) { return a > b ? a : b; }
   static constexpr int xs = 0;                   // 48
-  static constexpr int hl = 48;                  // h^0 [N][D0], h^1..h^3 [N][4]
+  static constexpr int hl = 48;                  // h^0 [N][D0], h^1..h^3 [N][4] (F1..F5)
+  static constexpr int hbar = hl;                // their adjoints, same layout (B1..B4)
   static constexpr int g1 = hl + hl_n;           // [3][2][D0]
   static constexpr int cq = g1 + 3 * 2 * D0;     // [3][N][QM]  conv outputs (kept for backward)
   static constexpr int sv = cq + 3 * N * QM;     // [3][N][4]   single outputs
   static constexpr int g2 = sv + 3 * N * 4;      // [3][2][N][4] g2 values (forward) / adjoints (backward)
-  static constexpr int yv = g2 + 3 * 2 * N * 4;  // [N][N]  Yt
-  // region R, lifetimes disjoint: {Phi [N][N][2], B [N][N][2]} (F5..B1) -> fbar (B2) -> dbar (B3..B4)
+  static constexpr int yv = g2 + 3 * 2 * N * 4;  // [N][N]  Yt (F1..B1)
+  static constexpr int ybar = yv;                // [N][N]  its adjoint (B1..B4)
+  // region R, lifetimes disjoint: reuse scratch (F0..F2) -> {Phi [N][N][2], B [N][N][2]} (F5..B1)
+  // -> {fbar [N][DFM], zsb [N][4], gsum [2][D0]} (B2) -> dbar [N][N][3] (B3..B4)
   static constexpr int R = yv + N * N;
   static constexpr int ph = R;
   static constexpr int mx = R + N * N * 2;
-  static constexpr int fbar = R;                 // [N][DFM]
-  static constexpr int dbar = R;                 // [N][N][3]
-  static constexpr int R_n = cmax(cmax(cmax(4 * N * N, N * DFM), 3 * N * N), 4 + 16 * 12);  // + reuse scratch
-  static constexpr int ybar = R + R_n;           // [N][N]
-  static constexpr int hbar = ybar + N * N;      // adjoints of h^0..h^3 (layout of hl)
-  static constexpr int zsb = hbar + hl_n;        // [N][4]
-  static constexpr int gsum = zsb + N * 4;       // [2][D0]
-  static constexpr int loc = gsum + 2 * D0;      // [N + D0][48] electron-local Jacobians (direction lanes)
-  static constexpr int end = loc + (N + D0) * 48;
+  static constexpr int fbar = R;
+  static constexpr int zsb = R + N * DFM;
+  static constexpr int gsum = zsb + N * 4;
+  static constexpr int dbar = R;
+  static constexpr int R_n = cmax(cmax(cmax(4 * N * N, N * DFM + 4 * N + 2 * D0), 3 * N * N), 4 + 64 * 12);
+  static constexpr int end = R + R_n;
   static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
   static constexpr int hoff(int l) { return l == 0 ? 0 : N * D0 + (l - 1) * N * 4; }
 };
@@ -131,6 +131,14 @@ __device__ __forceinline__ void pair_values(const T d[3], const T* __restrict__ 
   }
 }
 
+// Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2):
+// give every XCD a contiguous range of configurations, so the N proposals of a
+// walker (and that walker's cache) land on one L2.
+__device__ __forceinline__ int xcd_major(int blk, int n) {
+  if ((n & 7) != 0) return blk;
+  return (blk & 7) * (n >> 3) + (blk >> 3);
+}
+
 // Electron-local stage of the moved electron of proposals q = 16*block + s (lane = 16c + s).
 template <typename T, int N, int A>
 __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
@@ -140,7 +148,7 @@ __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
   const T* __restrict__ P = (const T*)ka.prm;
   const int lane = threadIdx.x;
   const int lc = lane >> 4, s = lane & 15;
-  const int q = blockIdx.x * 16 + s;
+  const int q = xcd_major(blockIdx.x, gridDim.x) * 16 + s;
   if (q >= ka.nconf) return;
   const int b = q / N, i = q - b * N;
   const T tstep = (T)ka.tstep;
@@ -183,7 +191,7 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
   T* sm = (T*)smem_raw;
   T* xs = sm + SM::xs;
 
-  const int conf = blockIdx.x;
+  const int conf = xcd_major(blockIdx.x, gridDim.x);
   const int lane = threadIdx.x;
   const int lc = lane >> 4;
   const int er = lane & 15;
@@ -220,126 +228,129 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
 
   AQ_PH(0);
   // ------------------------------------------------------------------ F1 per-electron stage (electron.h)
+  // Walker cache: read (proposal with reuse: this proposal's walker pb) or written (by conf).
   using WC = WCache<N, A>;
   using EC = ECache<N, A>;
   const bool reuse = ka.proposal && ka.ecache != nullptr;
+  T* Wc = (T*)ka.wcache + (size_t)(reuse ? pb : conf) * WC::size;
+  const T* Eq = reuse ? (const T*)ka.ecache + (size_t)conf * EC::size : nullptr;
   T* Yv = sm + SM::yv;
-  T* loc = sm + SM::loc;
+  T* g2 = sm + SM::g2;
   T jv = T(0), jd1 = T(0), jve = T(0);
   if (reuse) {
-    // walker b's cached stage, electron pi's entries from the moved-electron kernel
-    const T* Wb = (const T*)ka.wcache + (size_t)pb * WC::size;
-    const T* Eq = (const T*)ka.ecache + (size_t)conf * EC::size;
-    for (int idx = lane; idx < N * N; idx += 64) {
-      const int r = idx / N;
-      Yv[idx] = (r == pi) ? Eq[EC::yv + (idx - r * N)] : Wb[WC::yv + idx];
-    }
-    for (int idx = lane; idx < N * D0; idx += 64) {
-      const int e = idx / D0;
-      sm[SM::hl + idx] = (e == pi) ? Eq[EC::h0 + (idx - e * D0)] : Wb[WC::h0 + idx];
-    }
-    if (lane < 48) {
-      const bool mine = (er == pi);
-      const int c = lc;
+    // walker pb's cached stage and pair sums, electron pi's entries from k_moved_electron;
+    // all loads issued before the first LDS store
+    constexpr int NY = (N * N + 63) / 64, NHh = (N * D0 + 63) / 64, NG = (3 * 2 * N * 4 + 63) / 64;
+    T ry[NY], rh[NHh], rg[NG];
 #pragma unroll
-      for (int m = 0; m < N + D0; ++m) {
-        const T wv = Wb[WC::loc + m * 48 + lane];
-        const T ev = Eq[m < N ? EC::yd + c * N + m : EC::hd + c * D0 + (m - N)];
-        loc[m * 48 + lane] = mine ? ev : wv;
-      }
+    for (int t = 0; t < NY; ++t) {
+      const int idx = lane + 64 * t;
+      const int r = idx / N;
+      ry[t] = idx < N * N ? ((r == pi) ? Eq[EC::yv + (idx - r * N)] : Wc[WC::yv + idx]) : T(0);
     }
-    jv = (val && live) ? ((er == pi) ? Eq[EC::jv] : Wb[WC::jaev + er]) : T(0);
-    jd1 = dir ? ((le == pi) ? Eq[EC::jd + lc] : Wb[WC::jaed + lane]) : T(0);
+#pragma unroll
+    for (int t = 0; t < NHh; ++t) {
+      const int idx = lane + 64 * t;
+      const int e = idx / D0;
+      rh[t] = idx < N * D0 ? ((e == pi) ? Eq[EC::h0 + (idx - e * D0)] : Wc[WC::h0 + idx]) : T(0);
+    }
+#pragma unroll
+    for (int t = 0; t < NG; ++t) {
+      const int idx = lane + 64 * t;
+      rg[t] = idx < 3 * 2 * N * 4 ? Wc[WC::g2 + idx] : T(0);
+    }
+    jv = (val && live) ? ((er == pi) ? Eq[EC::jv] : Wc[WC::jaev + er]) : T(0);
+    jd1 = dir ? ((le == pi) ? Eq[EC::jd + lc] : Wc[WC::jaed + lane]) : T(0);
+    jve = lane == 0 ? Wc[WC::jee] : T(0);
+#pragma unroll
+    for (int t = 0; t < NY; ++t)
+      if (lane + 64 * t < N * N) Yv[lane + 64 * t] = ry[t];
+#pragma unroll
+    for (int t = 0; t < NHh; ++t)
+      if (lane + 64 * t < N * D0) sm[SM::hl + lane + 64 * t] = rh[t];
+#pragma unroll
+    for (int t = 0; t < NG; ++t)
+      if (lane + 64 * t < 3 * 2 * N * 4) g2[lane + 64 * t] = rg[t];
   } else {
     ElecOut<T, A> eo;
     electron_stage<T, N, A>(P, xs + le * 3, le, lc, eo);
-    const PJ<T>* hf = eo.hf;
-    const PJ<T>* yst = eo.yst;
-    const PJ<T> env = eo.env, jae = eo.jae;
-    // d(Yt row)/dx and d(ae features)/dx of this lane's electron: kept lane-private in LDS until B4
-      #pragma unroll
+    // d(Yt row)/dx and d(ae features)/dx of this lane's electron -> walker cache (read in B4)
+    T* Wl = Wc + WC::loc + lane;
+#pragma unroll
     for (int col = 0; col < N; ++col) {
-      PJ<T> s = P[Ly::wy + col] * yst[0];
-  #pragma unroll
-      for (int m = 1; m < NYW; ++m) s = s + P[Ly::wy + m * N + col] * yst[m];
-      const PJ<T> yt = env * s;
-      if (lane < 48) loc[col * 48 + lane] = yt.d1;
+      PJ<T> sy = P[Ly::wy + col] * eo.yst[0];
+#pragma unroll
+      for (int m = 1; m < NYW; ++m) sy = sy + P[Ly::wy + m * N + col] * eo.yst[m];
+      const PJ<T> yt = eo.env * sy;
+      if (lane < 48) Wl[col * 48] = yt.d1;
       if (val && live) Yv[er * N + col] = yt.v;
     }
-  #pragma unroll
+#pragma unroll
     for (int m = 0; m < D0; ++m) {
-      if (lane < 48) loc[(N + m) * 48 + lane] = hf[m].d1;
-      if (val && live) sm[SM::hl + er * D0 + m] = hf[m].v;
+      if (lane < 48) Wl[(N + m) * 48] = eo.hf[m].d1;
+      if (val && live) sm[SM::hl + er * D0 + m] = eo.hf[m].v;
     }
-    jv = (val && live) ? jae.v : T(0);
-    jd1 = dir ? jae.d1 : T(0);
-    if (ka.wcache) {
-      T* Wb = (T*)ka.wcache + (size_t)conf * WC::size;
-      if (val && live) Wb[WC::jaev + er] = jae.v;
-      if (lane < 48) Wb[WC::jaed + lane] = dir ? jae.d1 : T(0);
+    jv = (val && live) ? eo.jae.v : T(0);
+    jd1 = dir ? eo.jae.d1 : T(0);
+    if (!ka.proposal) {
+      if (val && live) Wc[WC::jaev + er] = eo.jae.v;
+      if (lane < 48) Wc[WC::jaed + lane] = jd1;
     }
   }
   __syncthreads();
-  if (ka.wcache && !ka.proposal) {
-    T* Wb = (T*)ka.wcache + (size_t)conf * WC::size;
-    for (int idx = lane; idx < N * N; idx += 64) Wb[WC::yv + idx] = Yv[idx];
-    for (int idx = lane; idx < N * D0; idx += 64) Wb[WC::h0 + idx] = sm[SM::hl + idx];
-    if (lane < 48)
-      for (int m = 0; m < N + D0; ++m) Wb[WC::loc + m * 48 + lane] = loc[m * 48 + lane];
+  if (!ka.proposal) {
+    for (int idx = lane; idx < N * N; idx += 64) Wc[WC::yv + idx] = Yv[idx];
+    for (int idx = lane; idx < N * D0; idx += 64) Wc[WC::h0 + idx] = sm[SM::hl + idx];
   }
 
   AQ_PH(1);
   // ------------------------------------------------------------------ F2+F3 pair stream + spin-group column means
   // lane = (column i, quarter kq): pairs (k, i) with k = kq, kq+4, ...; the three layers'
   // h2[k,i] values are summed per spin group in registers and quad-reduced with DPP.
-  T* g2 = sm + SM::g2;
   if (reuse) {
-    // walker b's sums, patched with the 2(N-1) pairs that involve the moved electron pi
-    const T* Wb = (const T*)ka.wcache + (size_t)pb * WC::size;
-    for (int idx = lane; idx < 3 * 2 * N * 4; idx += 64) g2[idx] = Wb[WC::g2 + idx];
-    T* S = sm + SM::R + 4;                          // [16][12] column-pi deltas
+    // patch walker pb's sums with the 2(N-1) pairs of the moved electron pi. lane = 16*part + o:
+    // part 0/1: pair (pi, o) at the new/old x_pi (column o); part 2/3: pair (o, pi) (column pi)
+    T* S = sm + SM::R + 4;                          // [64][12] pair-stream values
     const T* xo = sm + SM::R;                       // old position of pi
-    __syncthreads();
-    if (lane < 32) {
-      const bool rowp = lane < 16;                  // rowp: pair (pi, j); else pair (k, pi)
-      const int o = lane & 15;
-      if (o < N && o != pi) {
-        T dn[3], dd[3];
+    {
+      const int o = lane & 15, part = lane >> 4;
+      const int os = o < N ? o : N - 1;
+      const T* xp = (part & 1) ? xo : xs + pi * 3;
+      T d[3];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          dn[c] = rowp ? xs[o * 3 + c] - xs[pi * 3 + c] : xs[pi * 3 + c] - xs[o * 3 + c];
-          dd[c] = rowp ? xs[o * 3 + c] - xo[c] : xo[c] - xs[o * 3 + c];
-        }
-        T vn[3][4], vo[3][4];
-        pair_values<T, N, A>(dn, P, vn);
-        pair_values<T, N, A>(dd, P, vo);
-        if (rowp) {
-          const int Gp = pi >= nup ? 1 : 0;
-          const T gw = Gp ? ginv1 : ginv0;
+      for (int c = 0; c < 3; ++c) d[c] = (part < 2) ? xs[os * 3 + c] - xp[c] : xp[c] - xs[os * 3 + c];
+      T v[3][4];
+      pair_values<T, N, A>(d, P, v);
 #pragma unroll
-          for (int l = 0; l < 3; ++l)
+      for (int l = 0; l < 3; ++l)
 #pragma unroll
-            for (int f = 0; f < 4; ++f) g2[((l * 2 + Gp) * N + o) * 4 + f] += (vn[l][f] - vo[l][f]) * gw;
-          const T cusp = P[Ly::jee_c + pi * N + o], al = P[Ly::jee_a + pi * N + o];
-          jve += f_div(cusp * vn[0][0], al * vn[0][0] + T(1)) - f_div(cusp * vo[0][0], al * vo[0][0] + T(1));
-        } else {
-#pragma unroll
-          for (int l = 0; l < 3; ++l)
-#pragma unroll
-            for (int f = 0; f < 4; ++f) S[o * 12 + l * 4 + f] = vn[l][f] - vo[l][f];
-        }
+        for (int f = 0; f < 4; ++f) S[lane * 12 + l * 4 + f] = v[l][f];
+      if (part < 2 && o < N && o != pi) {
+        const T cusp = P[Ly::jee_c + pi * N + o], al = P[Ly::jee_a + pi * N + o];
+        const T je = f_div(cusp * v[0][0], al * v[0][0] + T(1));
+        jve += part == 0 ? je : -je;
       }
     }
     __syncthreads();
-    if (lane < 24) {
-      const int l = lane >> 3, G = (lane >> 2) & 1, f = lane & 3;
+    if (lane < 16) {
+      if (lane < N && lane != pi) {
+        const int Gp = pi >= nup ? 1 : 0;
+        const T gw = Gp ? ginv1 : ginv0;
+#pragma unroll
+        for (int l = 0; l < 3; ++l)
+#pragma unroll
+          for (int f = 0; f < 4; ++f)
+            g2[((l * 2 + Gp) * N + lane) * 4 + f] += (S[lane * 12 + l * 4 + f] - S[(16 + lane) * 12 + l * 4 + f]) * gw;
+      }
+    } else if (lane < 40) {
+      const int t = lane - 16;
+      const int l = t >> 3, G = (t >> 2) & 1, f = t & 3;
       const int k0 = G ? nup : 0, k1 = G ? N : nup;
       T acc = T(0);
       for (int k = k0; k < k1; ++k)
-        if (k != pi) acc += S[k * 12 + l * 4 + f];
+        if (k != pi) acc += S[(32 + k) * 12 + l * 4 + f] - S[(48 + k) * 12 + l * 4 + f];
       g2[((l * 2 + G) * N + pi) * 4 + f] += acc * (G ? ginv1 : ginv0);
     }
-    if (lane == 0) jve += Wb[WC::jee];
   } else {
     {
       const int i = lane >> 2, kq = lane & 3;
@@ -408,11 +419,10 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
     }
   }
   __syncthreads();
-  if (ka.wcache && !ka.proposal) {
-    T* Wb = (T*)ka.wcache + (size_t)conf * WC::size;
-    for (int idx = lane; idx < 3 * 2 * N * 4; idx += 64) Wb[WC::g2 + idx] = g2[idx];
+  if (!ka.proposal) {
+    for (int idx = lane; idx < 3 * 2 * N * 4; idx += 64) Wc[WC::g2 + idx] = g2[idx];
     const T je = wave_sum(jve);
-    if (lane == 0) Wb[WC::jee] = je;
+    if (lane == 0) Wc[WC::jee] = je;
   }
 
   AQ_PH(2);
@@ -511,6 +521,7 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
     }
     hbar[SM::hoff(3) + rowsrc[r] * 4 + f] = q;
   }
+  __syncthreads();   // ybar overwrites Yt
   for (int idx = lane; idx < N * N; idx += 64) {
     const int r = idx / N, c = idx - r * N;
     ybar[idx] = BRE(c, r) * Ph[idx * 2] - BIM(c, r) * Ph[idx * 2 + 1];
@@ -646,18 +657,31 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
   __syncthreads();
 
   AQ_PH(7);
+  // electron-local Jacobians of this lane's (electron, direction) for B4, fetched ahead of B3:
+  // from the walker cache, or the moved electron's entry of this proposal
+  const int c4 = lc < 3 ? lc : 0;
+  T lv[N + D0];
+  {
+    const bool mov = reuse && le == pi;
+    const T* la = mov ? Eq + EC::yd + c4 * N : Wc + WC::loc + (lane < 48 ? lane : 47);
+    const T* lb = mov ? Eq + EC::hd + c4 * D0 : Wc + WC::loc + N * 48 + (lane < 48 ? lane : 47);
+    const int st = mov ? 1 : 48;
+#pragma unroll
+    for (int m = 0; m < N; ++m) lv[m] = la[m * st];
+#pragma unroll
+    for (int m = 0; m < D0; ++m) lv[N + m] = lb[m * st];
+  }
   // ------------------------------------------------------------------ B4 gradient per direction lane (c, e)
   T g = jd1;
   {
-    const int c = lc < 3 ? lc : 0;
     for (int k = 0; k < N; ++k) {
       if (k == le) continue;
-      g += dbar[(k * N + le) * 3 + c] - dbar[(le * N + k) * 3 + c];
+      g += dbar[(k * N + le) * 3 + c4] - dbar[(le * N + k) * 3 + c4];
     }
 #pragma unroll
-    for (int col = 0; col < N; ++col) g += ybar[le * N + col] * loc[col * 48 + (lane < 48 ? lane : 47)];
+    for (int col = 0; col < N; ++col) g += ybar[le * N + col] * lv[col];
 #pragma unroll
-    for (int m = 0; m < D0; ++m) g += hbar[le * D0 + m] * loc[(N + m) * 48 + (lane < 48 ? lane : 47)];
+    for (int m = 0; m < D0; ++m) g += hbar[le * D0 + m] * lv[N + m];
   }
 
   AQ_PH(8);
