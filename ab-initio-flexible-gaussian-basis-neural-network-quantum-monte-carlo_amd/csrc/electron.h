@@ -32,7 +32,7 @@ struct ElecOut {
 
 // xpos: the 3 coordinates of electron le; le selects the per-electron parameters.
 template <typename T, int N, int A>
-__device__ __forceinline__ void electron_stage(const T* __restrict__ P, const T* xpos, int le, int lc,
+__device__ __forceinline__ void electron_stage(cptr<T> P, const T* xpos, int le, int lc,
                                                ElecOut<T, A>& o) {
   using Ly = Lay<N, A>;
   PJ<T> xe[3];

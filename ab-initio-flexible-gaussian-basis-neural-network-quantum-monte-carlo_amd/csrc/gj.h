@@ -2,14 +2,9 @@
 // matrix per wavefront (replaces jnp.linalg.slogdet, network_blocks.py:156, and
 // provides B = A^{-1} for the derivative contractions).
 //
-// Layout: lane l = 16*cg + j holds row j (< N) of [A | I], columns
-// cg*CW .. cg*CW+CW-1 (CW = ceil(2N/4)) in VGPRs for the whole elimination.
-// Partial pivoting is virtual: at step k the pivot row p_k is the unused row
-// with the first maximal |re|+|im| in column k (LAPACK izamax rule); no rows
-// move.  With E the accumulated row operations, E A = L with L[p_k,k] = 1,
-// so A^{-1}[k,:] = (right block)[p_k,:] and det A = sgn(p) prod_k pivot_k.
-// Per step: one 16-lane DPP max + ballot for the pivot, 2 readlanes for the
-// pivot value, 2 + 2*CW ds_bpermute broadcasts, CW complex row updates.
+// Partial pivoting is virtual (no rows move): the pivot of step k is the unused
+// row with the first maximal |re|+|im| in column k (LAPACK izamax rule), the
+// same rows LU partial pivoting selects.  Layout and step: see gj_inverse.
 #pragma once
 #include "jets.h"
 
@@ -17,59 +12,104 @@ namespace aq {
 
 template <typename T> __device__ __forceinline__ T f_max(T a, T b) { return a > b ? a : b; }
 
-template <typename T> __device__ __forceinline__ T rowmax16(T x) {
-  x = f_max(x, dpp<0xB1>(x));
-  x = f_max(x, dpp<0x4E>(x));
-  x = f_max(x, dpp<0x141>(x));
-  x = f_max(x, dpp<0x140>(x));
-  return x;
+
+// DPP row_newbcast:k (lane k of each 16-lane row to the whole row); k must fold to a
+// constant (fully unrolled loops).
+template <typename T> __device__ __forceinline__ T row_bcast(T x, int k) {
+  switch (k) {
+    case 0: return dpp<0x150>(x);
+    case 1: return dpp<0x151>(x);
+    case 2: return dpp<0x152>(x);
+    case 3: return dpp<0x153>(x);
+    case 4: return dpp<0x154>(x);
+    case 5: return dpp<0x155>(x);
+    case 6: return dpp<0x156>(x);
+    case 7: return dpp<0x157>(x);
+    case 8: return dpp<0x158>(x);
+    case 9: return dpp<0x159>(x);
+    case 10: return dpp<0x15A>(x);
+    case 11: return dpp<0x15B>(x);
+    case 12: return dpp<0x15C>(x);
+    case 13: return dpp<0x15D>(x);
+    case 14: return dpp<0x15E>(x);
+    default: return dpp<0x15F>(x);
+  }
 }
 
 // A[r][c] = Ph[r][c] * Yv[r][c]  (Ph complex interleaved [N][N][2], Yv real [N][N]).
 // Writes B = A^{-1} to Bout[N][N][2]; returns log|det A| and the unit phase (phr, phi).
+//
+// In-place Gauss-Jordan, column layout: lane l = 16*rg + c holds column c (< N) of
+// rows rg*RW .. rg*RW+RW-1 (RW = ceil(N/4)) in VGPRs.  Step k (unrolled):
+//   pivot p_k = first unused row with maximal |re|+|im| in column k (izamax rule;
+//     per-lane best over its rows, readlanes of the four row groups, ballot);
+//   q[c]  = a[p][c] / piv (c != k),  q[k] = 1 / piv   (one ds_bpermute per component);
+//   a[r][c] <- (c == k ? 0 : a[r][c]) - a[r][k] q[c] for r != p, a[p][c] <- q[c],
+//     a[r][k] broadcast inside the 16-lane row by DPP row_newbcast:k.
+// Only N columns are carried (the inverse builds up in the pivot columns), so no
+// identity block.  With virtual pivoting X[p_k][c] = A^{-1}[k][p_c]; det A =
+// sgn(p) prod_k pivot_k.
+// Pivot key of a candidate: bits of |re|+|im| (monotone for non-negative floats; the
+// high word for double) with the low 3 bits replaced by 4 - t, so a max over
+// (row slot t, row group) picks the largest magnitude and, among equal truncated
+// magnitudes, the lowest row.  0 marks used / dead rows.
+__device__ __forceinline__ unsigned key_bits(float x) { return __float_as_uint(x); }
+__device__ __forceinline__ unsigned key_bits(double x) {
+  return (unsigned)(__builtin_bit_cast(unsigned long long, x) >> 32);
+}
+
 template <typename T, int N>
 __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, int lane, T& logdet, T& phr,
                                            T& phi) {
-  constexpr int CW = (2 * N + 3) / 4;
-  const int j = lane & 15;
-  const int cg = lane >> 4;
-  const bool rowlive = j < N;
-  T mr[CW], mi[CW];
+  constexpr int RW = (N + 3) / 4;
+  const int c = lane & 15;
+  const int rg = lane >> 4;
+  const bool clive = c < N;
+  T ar[RW], ai[RW];
+  unsigned kmask[RW], kcode[RW];
+  int myk[RW];
 #pragma unroll
-  for (int t = 0; t < CW; ++t) {
-    const int c = cg * CW + t;
+  for (int t = 0; t < RW; ++t) {
+    const int r = rg * RW + t;
+    const bool live = r < N;
     T a = T(0), b = T(0);
-    if (rowlive && c < N) {
-      const T y = Yv[j * N + c];
-      a = Ph[(j * N + c) * 2] * y;
-      b = Ph[(j * N + c) * 2 + 1] * y;
-    } else if (rowlive && c < 2 * N && c - N == j) {
-      a = T(1);
+    if (live && clive) {
+      const T y = Yv[r * N + c];
+      a = Ph[(r * N + c) * 2] * y;
+      b = Ph[(r * N + c) * 2 + 1] * y;
     }
-    mr[t] = a;
-    mi[t] = b;
+    ar[t] = a;
+    ai[t] = b;
+    kmask[t] = live ? ~7u : 0u;
+    kcode[t] = live ? (unsigned)(4 - t) : 0u;
+    myk[t] = 0;
   }
-  bool used = !rowlive;
-  int myk = 0;
-  int pk[N];
+  int myp = 0;
+  unsigned used = 0;   // rows chosen so far (uniform bitmask)
+  int inv = 0;         // inversions of the pivot sequence, for sgn(p)
   T ld = T(0), pr_ = T(1), pi_ = T(0);
 #pragma unroll
   for (int k = 0; k < N; ++k) {
-    constexpr int dummy = 0;
-    (void)dummy;
-    const int kc = k / CW, kt = k % CW;
-    const bool cand = (cg == kc) && !used;
-    const T key = cand ? f_abs(mr[kt]) + f_abs(mi[kt]) : T(-1);
-    const T m = rowmax16(key);
-    const unsigned long long mask = __ballot(cand && key == m);
-    const int p = (int)__builtin_ctzll(mask) - 16 * kc;
-    pk[k] = p;
-    if (j == p) {
-      used = true;
-      myk = k;
+    // ---- pivot: first maximal |re|+|im| among the unused rows of column k
+    unsigned best = 0;
+#pragma unroll
+    for (int t = 0; t < RW; ++t) {
+      const unsigned key = (key_bits(f_abs(ar[t]) + f_abs(ai[t])) & kmask[t]) | kcode[t];
+      best = best > key ? best : key;
     }
-    const T pr = rdlane(mr[kt], 16 * kc + p);
-    const T pim = rdlane(mi[kt], 16 * kc + p);
+    const unsigned b0 = (unsigned)rdlane((int)best, k), b1 = (unsigned)rdlane((int)best, 16 + k);
+    const unsigned b2 = (unsigned)rdlane((int)best, 32 + k), b3 = (unsigned)rdlane((int)best, 48 + k);
+    const unsigned m01 = b0 > b1 ? b0 : b1, m23 = b2 > b3 ? b2 : b3;
+    const unsigned m = m01 > m23 ? m01 : m23;
+    const int g = b0 == m ? 0 : (b1 == m ? 1 : (b2 == m ? 2 : 3));
+    const int ps = m ? 4 - (int)(m & 7u) : 0;
+    const int p = g * RW + ps;
+    inv += __builtin_popcount(used >> p);      // earlier pivots above p
+    used |= 1u << p;
+    // ---- row p of this lane's column (register ps of lane 16 g + c)
+    const T sr = ar[ps], si = ai[ps];
+    const T pr = rdlane(sr, 16 * g + k);
+    const T pim = rdlane(si, 16 * g + k);
     const T den = pr * pr + pim * pim;
     const T rden = f_rcp(den);
     ld += T(0.5) * f_log(den);                 // log|pivot|
@@ -80,34 +120,45 @@ __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, in
       pr_ = nr;
       pi_ = ni;
     }
-    const T ir = pr * rden, ii = -pim * rden;
-    const T fr = __shfl(mr[kt], 16 * kc + j);
-    const T fi = __shfl(mi[kt], 16 * kc + j);
-    const bool isp = (j == p);
+    const T ir = pr * rden, ii = -pim * rden;   // 1 / pivot
+    const T q0r = __shfl(sr, 16 * g + c), q0i = __shfl(si, 16 * g + c);
+    const bool ck = (c == k);
+    const T qr = ck ? ir : q0r * ir - q0i * ii;
+    const T qi = ck ? ii : q0r * ii + q0i * ir;
+    T mqr = -qr, mqi = -qi;
+    // opaque to the optimiser: keeps the updates in v_fmac form (VOP2), which can
+    // take the DPP row broadcast of a[r][k] as an operand (VOP3 with neg cannot on gfx9)
+    asm volatile("" : "+v"(mqr), "+v"(mqi));
+    // ---- eliminate column k from every row (the pivot row is overwritten below)
 #pragma unroll
-    for (int t = 0; t < CW; ++t) {
-      const T qr = __shfl(mr[t], 16 * cg + p);
-      const T qi = __shfl(mi[t], 16 * cg + p);
-      const T sr = qr * ir - qi * ii, si = qr * ii + qi * ir;
-      const T ur = mr[t] - (fr * sr - fi * si);
-      const T ui = mi[t] - (fr * si + fi * sr);
-      mr[t] = isp ? sr : ur;
-      mi[t] = isp ? si : ui;
+    for (int t = 0; t < RW; ++t) {
+      const T fr = row_bcast(ar[t], k);        // a[r][k]
+      const T fi = row_bcast(ai[t], k);
+      T nr = ck ? T(0) : ar[t], ni = ck ? T(0) : ai[t];
+      nr = f_fma(fr, mqr, nr);                 // v_fmac with the DPP broadcast folded in
+      nr = f_fma(fi, qi, nr);
+      ni = f_fma(fr, mqi, ni);
+      ni = f_fma(fi, mqr, ni);
+      ar[t] = nr;
+      ai[t] = ni;
     }
+    if (rg == g) {
+      ar[ps] = qr;
+      ai[ps] = qi;
+      myk[ps] = k;
+      kmask[ps] = 0u;
+      kcode[ps] = 0u;
+    }
+    myp = ck ? p : myp;
   }
 #pragma unroll
-  for (int t = 0; t < CW; ++t) {
-    const int c = cg * CW + t;
-    if (rowlive && c >= N && c < 2 * N) {
-      Bout[(myk * N + (c - N)) * 2] = mr[t];
-      Bout[(myk * N + (c - N)) * 2 + 1] = mi[t];
+  for (int t = 0; t < RW; ++t) {
+    const int r = rg * RW + t;
+    if (r < N && clive) {
+      Bout[(myk[t] * N + myp) * 2] = ar[t];
+      Bout[(myk[t] * N + myp) * 2 + 1] = ai[t];
     }
   }
-  int inv = 0;
-#pragma unroll
-  for (int a = 0; a < N; ++a)
-#pragma unroll
-    for (int b = a + 1; b < N; ++b) inv += pk[a] > pk[b] ? 1 : 0;
   if (inv & 1) {
     pr_ = -pr_;
     pi_ = -pi_;

@@ -25,6 +25,13 @@
 
 namespace aq {
 
+// Pointer to the packed kernel parameters.  Deliberately the generic address space:
+// with address space 4 (constant) the compiler moves wave-uniform weights into
+// SGPRs, and gfx9's one-SGPR/no-literal VOP3 operand rule then costs extra v_mov
+// instructions in these VALU-bound kernels (measured: +6% VALU).
+template <typename T> using cptr = const T* __restrict__;
+template <typename T> __device__ __forceinline__ cptr<T> param_ptr(const void* p) { return (cptr<T>)p; }
+
 // Scalar math.  float uses the hardware approximations (v_sqrt_f32, v_rcp_f32,
 // v_exp_f32: ~1 ulp), which is well inside the fp32 parity tolerance of the
 // reference's own float32 arithmetic; double keeps the correctly rounded
@@ -54,6 +61,8 @@ template <> __device__ __forceinline__ double f_tanh(double x) { return tanh(x);
 template <typename T> __device__ __forceinline__ T f_abs(T x);
 template <> __device__ __forceinline__ float f_abs(float x) { return fabsf(x); }
 template <> __device__ __forceinline__ double f_abs(double x) { return fabs(x); }
+__device__ __forceinline__ float f_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double f_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 template <typename T> __device__ __forceinline__ T f_hypot(T x, T y);
 template <> __device__ __forceinline__ float f_hypot(float x, float y) { return hypotf(x, y); }
 template <> __device__ __forceinline__ double f_hypot(double x, double y) { return hypot(x, y); }
@@ -136,13 +145,16 @@ __device__ __forceinline__ double rdlane(double x, int l) {
 }
 __device__ __forceinline__ int rdlane(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
 
+// Every DPP pattern used here (quad_perm, row_ror, row_mirror, row_newbcast) has a
+// valid source lane for every lane, so bound_ctrl is set and no "old" value is needed;
+// this lets the compiler fold the move into the consuming VOP2 instruction.
 template <int CTRL> __device__ __forceinline__ float dpp(float x) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
 }
 template <int CTRL> __device__ __forceinline__ double dpp(double x) {
   const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
-  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xF, 0xF, false);
-  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, false);
+  const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)b, CTRL, 0xF, 0xF, true);
+  const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, true);
   return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 

@@ -74,7 +74,7 @@ struct Smem {
 };
 
 template <typename T, int N, int A, bool LAP, int L>
-__device__ __forceinline__ void h_layer(const T* __restrict__ P, const T* xs, T* hb, const PJ<T>* hf,
+__device__ __forceinline__ void h_layer(cptr<T> P, const T* xs, T* hb, const PJ<T>* hf,
                                         int lane, int lc, int er, int le, bool val, bool dir, bool live,
                                         int nup, T& jd1, T& jd2, T& jv, T& vv) {
   using Ly = Lay<N, A>;
@@ -82,10 +82,10 @@ __device__ __forceinline__ void h_layer(const T* __restrict__ P, const T* xs, T*
   constexpr int DIN = (L == 0) ? 4 * A : NH;
   constexpr int DF = 3 * DIN + 2 * NH2;
   constexpr int Q = DF / 4;
-  const T* convw = P + (L == 0 ? Ly::conv_w0 : (L == 1 ? Ly::conv_w1 : Ly::conv_w2));
-  const T* convb = P + (L == 0 ? Ly::conv_b0 : (L == 1 ? Ly::conv_b1 : Ly::conv_b2));
-  const T* sngw = P + (L == 0 ? Ly::sng_w0 : (L == 1 ? Ly::sng_w1 : Ly::sng_w2));
-  const T* sngb = P + (L == 0 ? Ly::sng_b0 : (L == 1 ? Ly::sng_b1 : Ly::sng_b2));
+  const cptr<T> convw = P + (L == 0 ? Ly::conv_w0 : (L == 1 ? Ly::conv_w1 : Ly::conv_w2));
+  const cptr<T> convb = P + (L == 0 ? Ly::conv_b0 : (L == 1 ? Ly::conv_b1 : Ly::conv_b2));
+  const cptr<T> sngw = P + (L == 0 ? Ly::sng_w0 : (L == 1 ? Ly::sng_w1 : Ly::sng_w2));
+  const cptr<T> sngb = P + (L == 0 ? Ly::sng_b0 : (L == 1 ? Ly::sng_b1 : Ly::sng_b2));
   const int glo[2] = {0, nup};
   const int ghi[2] = {nup, N};
   const T ginv[2] = {T(1) / T(nup), T(1) / T(N - nup)};
@@ -154,8 +154,8 @@ __device__ __forceinline__ void h_layer(const T* __restrict__ P, const T* xs, T*
     // pair stream: L double layers, tanh + residual (nn.py:305-309)
 #pragma unroll
     for (int j = 0; j < L; ++j) {
-      const T* dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
-      const T* db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
+      const cptr<T> dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
+      const cptr<T> db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
       PJ<T> q[4];
 #pragma unroll
       for (int o = 0; o < 4; ++o) {
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(64) void k_walker(KArgs ka) {
   using Ly = Lay<N, A>;
   using SM = Smem<T, N, LAP>;
   constexpr int NC = SM::NC;
-  const T* __restrict__ P = (const T*)ka.prm;
+  const cptr<T> P = param_ptr<T>(ka.prm);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   T* sm = (T*)smem_raw;
   T* xs = sm + SM::xs;

@@ -51,22 +51,18 @@ struct SmemRev {
   static constexpr int xs = 0;                   // 48
   static constexpr int hl = 48;                  // h^0 [N][D0], h^1..h^3 [N][4] (F1..F5)
   static constexpr int hbar = hl;                // their adjoints, same layout (B1..B4)
-  static constexpr int g1 = hl + hl_n;           // [3][2][D0]
-  static constexpr int cq = g1 + 3 * 2 * D0;     // [3][N][QM]  conv outputs (kept for backward)
+  static constexpr int cq = hl + hl_n;           // [3][N][QM]  conv outputs (kept for backward)
   static constexpr int sv = cq + 3 * N * QM;     // [3][N][4]   single outputs
   static constexpr int g2 = sv + 3 * N * 4;      // [3][2][N][4] g2 values (forward) / adjoints (backward)
   static constexpr int yv = g2 + 3 * 2 * N * 4;  // [N][N]  Yt (F1..B1)
   static constexpr int ybar = yv;                // [N][N]  its adjoint (B1..B4)
   // region R, lifetimes disjoint: reuse scratch (F0..F2) -> {Phi [N][N][2], B [N][N][2]} (F5..B1)
-  // -> {fbar [N][DFM], zsb [N][4], gsum [2][D0]} (B2) -> dbar [N][N][3] (B3..B4)
+  // -> dbar [N][N][3] (B3..B4)
   static constexpr int R = yv + N * N;
   static constexpr int ph = R;
   static constexpr int mx = R + N * N * 2;
-  static constexpr int fbar = R;
-  static constexpr int zsb = R + N * DFM;
-  static constexpr int gsum = zsb + N * 4;
   static constexpr int dbar = R;
-  static constexpr int R_n = cmax(cmax(cmax(4 * N * N, N * DFM + 4 * N + 2 * D0), 3 * N * N), 4 + 64 * 12);
+  static constexpr int R_n = cmax(cmax(4 * N * N, 3 * N * N), 4 + 64 * 12);
   static constexpr int end = R + R_n;
   static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
   static constexpr int hoff(int l) { return l == 0 ? 0 : N * D0 + (l - 1) * N * 4; }
@@ -102,7 +98,7 @@ struct ECache {
 };
 
 template <typename T, int N, int A>
-__device__ __forceinline__ void pair_values(const T d[3], const T* __restrict__ P, T out[3][4]) {
+__device__ __forceinline__ void pair_values(const T d[3], cptr<T> P, T out[3][4]) {
   using Ly = Lay<N, A>;
   const T RSQ2 = T(0.70710678118654752);
   T p[4];
@@ -113,8 +109,8 @@ __device__ __forceinline__ void pair_values(const T d[3], const T* __restrict__ 
   for (int f = 0; f < 4; ++f) out[0][f] = p[f];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const T* dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
-    const T* db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
+    const cptr<T> dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
+    const cptr<T> db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
     T q[4];
 #pragma unroll
     for (int o = 0; o < 4; ++o) {
@@ -131,6 +127,20 @@ __device__ __forceinline__ void pair_values(const T d[3], const T* __restrict__ 
   }
 }
 
+// Sum of x over the lanes 4i+f with equal f (i.e. over electrons, per unit f); every
+// lane receives its class total.  row_ror:4, row_ror:8, then across the four rows.
+template <typename T> __device__ __forceinline__ T class4_sum(T x) {
+  x += dpp<0x124>(x);
+  x += dpp<0x128>(x);
+  x += __shfl_xor(x, 16);
+  x += __shfl_xor(x, 32);
+  return x;
+}
+// Value of x held by lane M of this lane's quad.
+template <int M, typename T> __device__ __forceinline__ T quad_bcast(T x) {
+  return dpp<M | (M << 2) | (M << 4) | (M << 6)>(x);
+}
+
 // Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2):
 // give every XCD a contiguous range of configurations, so the N proposals of a
 // walker (and that walker's cache) land on one L2.
@@ -145,7 +155,7 @@ __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
   using Ly = Lay<N, A>;
   using EC = ECache<N, A>;
   constexpr int D0 = 4 * A;
-  const T* __restrict__ P = (const T*)ka.prm;
+  const cptr<T> P = param_ptr<T>(ka.prm);
   const int lane = threadIdx.x;
   const int lc = lane >> 4, s = lane & 15;
   const int q = xcd_major(blockIdx.x, gridDim.x) * 16 + s;
@@ -181,12 +191,19 @@ __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
   else E[EC::jd + lc] = eo.jae.d1;
 }
 
+// Occupancy hint per instantiation: fp32 N2 (14, 2) lands one VGPR above the
+// 4-waves/SIMD budget (128) without it and fits it without spilling with it.
+template <typename T, int N, int A> struct RevWaves {
+  static constexpr int value = (sizeof(T) == 4 && N == 14 && A == 2) ? 4 : 1;
+};
+
 template <typename T, int N, int A>
-__global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, N, A>::value))) void k_walker_rev(
+    KArgs ka) {
   using Ly = Lay<N, A>;
   using SM = SmemRev<T, N, A>;
   constexpr int D0 = SM::D0;
-  const T* __restrict__ P = (const T*)ka.prm;
+  const cptr<T> P = param_ptr<T>(ka.prm);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   T* sm = (T*)smem_raw;
   T* xs = sm + SM::xs;
@@ -386,8 +403,8 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
           }
   #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            const T* dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
-            const T* db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
+            const cptr<T> dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
+            const cptr<T> db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
             T q[4];
   #pragma unroll
             for (int o = 0; o < 4; ++o) {
@@ -427,55 +444,89 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
 
   AQ_PH(2);
   // ------------------------------------------------------------------ F4 h-stream layers (values)
+  // lane = 4i + f (electron i, unit f): h^l[i][f] stays in a register across layers; the
+  // spin-group means are class sums over lanes of equal f; the four lanes of electron i
+  // each evaluate all of its conv outputs (no LDS round trip, no barrier).
   T* hl = sm + SM::hl;
-  T* g1 = sm + SM::g1;
   T* cqv = sm + SM::cq;
   T* sv = sm + SM::sv;
+  const int fi = lane >> 2, ff = lane & 3;
+  const bool ilive = fi < N;
+  const int ic = ilive ? fi : N - 1;
+  const bool inG1 = ic >= nup;
+  T hreg = T(0);
 #pragma unroll
   for (int l = 0; l < 3; ++l) {
     const int d1 = l == 0 ? D0 : NH;
     const int DF = 3 * d1 + 8;
     const int Q = DF / 4;
-    const T* hin = hl + SM::hoff(l);
-    T* hout = hl + SM::hoff(l + 1);
-    const T* convw = P + (l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2));
-    const T* convb = P + (l == 0 ? Ly::conv_b0 : (l == 1 ? Ly::conv_b1 : Ly::conv_b2));
-    const T* sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
-    const T* sngb = P + (l == 0 ? Ly::sng_b0 : (l == 1 ? Ly::sng_b1 : Ly::sng_b2));
-    T* g1l = g1 + l * 2 * D0;
-    if (lane < 2 * d1) {
-      const int G = lane / d1, m = lane - G * d1;
-      const int k0 = G ? nup : 0, k1 = G ? N : nup;
-      T s = T(0);
-      for (int k = k0; k < k1; ++k) s += hin[k * d1 + m];
-      g1l[G * d1 + m] = s * (G ? ginv1 : ginv0);
-    }
-    __syncthreads();
-    for (int it = lane; it < N * Q; it += 64) {
-      const int i = it / Q, q = it - i * Q;
-      T z = T(0);
+    const int T4 = d1 / 4;
+    const cptr<T> convw = P + (l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2)) + ic * DF;
+    const cptr<T> convb = P + (l == 0 ? Ly::conv_b0 : (l == 1 ? Ly::conv_b1 : Ly::conv_b2)) + ic * Q;
+    const cptr<T> sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
+    const cptr<T> sngb = P + (l == 0 ? Ly::sng_b0 : (l == 1 ? Ly::sng_b1 : Ly::sng_b2));
+    T hrow[D0];
+    T gs[2][D0 / 4];
+    if (l == 0) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int j = 4 * q + s;
-        T F;
-        if (j < d1) F = hin[i * d1 + j];
-        else if (j < 3 * d1) F = g1l[j - d1];
-        else F = g2[((l * 2 + (j - 3 * d1) / 4) * N + i) * 4 + ((j - 3 * d1) & 3)];
-        z += F * convw[i * DF + j];
+      for (int m = 0; m < D0; ++m) hrow[m] = hl[ic * D0 + m];
+#pragma unroll
+      for (int t = 0; t < D0 / 4; ++t) {
+        const T x = ilive ? hl[ic * D0 + ff + 4 * t] : T(0);
+        gs[0][t] = class4_sum(inG1 ? T(0) : x);
+        gs[1][t] = class4_sum(inG1 ? x : T(0));
       }
-      cqv[(l * N + i) * SM::QM + q] = f_tanh(z * T(0.25) + convb[i * Q + q]);
+    } else {
+      hrow[0] = quad_bcast<0>(hreg);
+      hrow[1] = quad_bcast<1>(hreg);
+      hrow[2] = quad_bcast<2>(hreg);
+      hrow[3] = quad_bcast<3>(hreg);
+      const T x = ilive ? hreg : T(0);
+      gs[0][0] = class4_sum(inG1 ? T(0) : x);
+      gs[1][0] = class4_sum(inG1 ? x : T(0));
     }
-    __syncthreads();
-    if (lane < N * 4) {
-      const int i = lane >> 2, f = lane & 3;
-      T z = sngb[f];
-      for (int q = 0; q < Q; ++q) z += cqv[(l * N + i) * SM::QM + q] * sngw[q * 4 + f];
-      const T s = f_tanh(z);
-      sv[(l * N + i) * 4 + f] = s;
-      hout[i * 4 + f] = (d1 == NH) ? (hin[i * d1 + f] + s) * RSQ2 : s;
+    T g1v[2][D0];
+#pragma unroll
+    for (int G = 0; G < 2; ++G)
+#pragma unroll
+      for (int t = 0; t < D0 / 4; ++t) {
+        if (t < T4) {
+          const T gw = G ? ginv1 : ginv0;
+          g1v[G][4 * t + 0] = quad_bcast<0>(gs[G][t]) * gw;
+          g1v[G][4 * t + 1] = quad_bcast<1>(gs[G][t]) * gw;
+          g1v[G][4 * t + 2] = quad_bcast<2>(gs[G][t]) * gw;
+          g1v[G][4 * t + 3] = quad_bcast<3>(gs[G][t]) * gw;
+        }
+      }
+    T cq[SM::QM];
+#pragma unroll
+    for (int q = 0; q < SM::QM; ++q) {
+      if (q < Q) {
+        T z = T(0);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int j = 4 * q + s4;
+          T F;
+          if (j < d1) F = hrow[j];
+          else if (j < 3 * d1) F = g1v[(j - d1) / d1][(j - d1) % d1];
+          else F = g2[((l * 2 + (j - 3 * d1) / 4) * N + ic) * 4 + ((j - 3 * d1) & 3)];
+          z += F * convw[j];
+        }
+        cq[q] = f_tanh(z * T(0.25) + convb[q]);
+        if (ilive && (q & 3) == ff) cqv[(l * N + ic) * SM::QM + q] = cq[q];
+      }
     }
-    __syncthreads();
+    T z = sngb[ff];
+#pragma unroll
+    for (int q = 0; q < SM::QM; ++q)
+      if (q < Q) z += cq[q] * sngw[q * 4 + ff];
+    const T sval = f_tanh(z);
+    if (ilive) sv[(l * N + ic) * 4 + ff] = sval;
+    const T hin = l == 0 ? hl[ic * D0 + ff] : hreg;
+    hreg = (d1 == NH) ? (hin + sval) * RSQ2 : sval;
   }
+  if (ilive) hl[SM::hoff(3) + ic * 4 + ff] = hreg;
+  __syncthreads();
 
   AQ_PH(3);
   // ------------------------------------------------------------------ F5 Phi, A = Phi * Yt, Gauss-Jordan -> B = A^{-1}
@@ -532,60 +583,60 @@ __global__ __launch_bounds__(64) void k_walker_rev(KArgs ka) {
 
   AQ_PH(5);
   // ------------------------------------------------------------------ B2 back through the h-stream layers
-  T* zsb = sm + SM::zsb;
-  T* fbar = sm + SM::fbar;
-  T* gsum = sm + SM::gsum;
+  // lane map of F4: the adjoint of h^{l+1}[i][f] stays in a register.
   T* g2b = sm + SM::g2;    // forward g2 values are dead after F4: reuse for their adjoints
+  {
+    T hb = hbar[SM::hoff(3) + ic * 4 + ff];
 #pragma unroll
-  for (int l = 2; l >= 0; --l) {
-    const int d1 = l == 0 ? D0 : NH;
-    const int DF = 3 * d1 + 8;
-    const int Q = DF / 4;
-    const T* convw = P + (l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2));
-    const T* sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
-    const T* hbo = hbar + SM::hoff(l + 1);
-    T* hbi = hbar + SM::hoff(l);
-    // single: s = tanh(c Ws + b), h_out = res(h_in, s)
-    if (lane < N * 4) {
-      const int i = lane >> 2, f = lane & 3;
-      const T s = sv[(l * N + i) * 4 + f];
-      const T ho = hbo[i * 4 + f];
-      const T sb = (d1 == NH) ? ho * RSQ2 : ho;
-      zsb[i * 4 + f] = sb * (T(1) - s * s);
-    }
-    __syncthreads();
-    // conv: c = tanh(0.25 sum F w + b)
-    for (int it = lane; it < N * Q; it += 64) {
-      const int i = it / Q, q = it - i * Q;
-      T cb = T(0);
+    for (int l = 2; l >= 0; --l) {
+      const int d1 = l == 0 ? D0 : NH;
+      const int DF = 3 * d1 + 8;
+      const int Q = DF / 4;
+      const int T4 = d1 / 4;
+      const cptr<T> convw = P + (l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2)) + ic * DF;
+      const cptr<T> sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
+      // single: s = tanh(c Ws + b), h_out = res(h_in, s)
+      const T sval = sv[(l * N + ic) * 4 + ff];
+      const T sb = (d1 == NH) ? hb * RSQ2 : hb;
+      const T zs = sb * (T(1) - sval * sval);
+      const T zq[4] = {quad_bcast<0>(zs), quad_bcast<1>(zs), quad_bcast<2>(zs), quad_bcast<3>(zs)};
+      // conv: c = tanh(0.25 sum F w + b); fb[q] = adjoint of input 4q + f
+      T fb[SM::QM];
 #pragma unroll
-      for (int f = 0; f < 4; ++f) cb += zsb[i * 4 + f] * sngw[q * 4 + f];
-      const T c = cqv[(l * N + i) * SM::QM + q];
-      const T zc = cb * (T(1) - c * c) * T(0.25);
+      for (int q = 0; q < SM::QM; ++q) {
+        if (q < Q) {
+          T cb = T(0);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) fbar[i * SM::DFM + 4 * q + s] = zc * convw[i * DF + 4 * q + s];
+          for (int m = 0; m < 4; ++m) cb += zq[m] * sngw[q * 4 + m];
+          const T c = cqv[(l * N + ic) * SM::QM + q];
+          fb[q] = cb * (T(1) - c * c) * T(0.25) * convw[4 * q + ff];
+        }
+      }
+      // g2 adjoints (inputs 3 d1 + 4G + f), consumed by B3
+      if (ilive) {
+        g2b[((l * 2 + 0) * N + ic) * 4 + ff] = fb[3 * T4 + 0];
+        g2b[((l * 2 + 1) * N + ic) * 4 + ff] = fb[3 * T4 + 1];
+      }
+      // group-mean adjoints and h^l adjoints of units m = f + 4t
+      T hn = T(0);
+#pragma unroll
+      for (int t = 0; t < D0 / 4; ++t) {
+        if (t < T4) {
+          const T s0 = class4_sum(ilive ? fb[T4 + t] : T(0)) * ginv0;
+          const T s1 = class4_sum(ilive ? fb[2 * T4 + t] : T(0)) * ginv1;
+          T v = fb[t] + (inG1 ? s1 : s0);
+          if (d1 == NH) v += hb * RSQ2;
+          if (l == 0) {
+            if (ilive) hbar[ic * D0 + ff + 4 * t] = v;
+          } else {
+            hn = v;
+          }
+        }
+      }
+      hb = hn;
     }
-    __syncthreads();
-    // group-mean adjoints: gsum[G][m] = sum_i fbar[i][d1*(1+G)+m]; g2 adjoints
-    if (lane < 2 * d1) {
-      const int G = lane / d1, m = lane - G * d1;
-      T s = T(0);
-      for (int i = 0; i < N; ++i) s += fbar[i * SM::DFM + d1 * (1 + G) + m];
-      gsum[G * d1 + m] = s * (G ? ginv1 : ginv0);
-    }
-    for (int it = lane; it < 2 * N * 4; it += 64) {
-      const int f = it & 3, i = (it >> 2) % N, G = (it >> 2) / N;
-      g2b[((l * 2 + G) * N + i) * 4 + f] = fbar[i * SM::DFM + 3 * d1 + 4 * G + f];
-    }
-    __syncthreads();
-    for (int it = lane; it < N * d1; it += 64) {
-      const int k = it / d1, m = it - k * d1;
-      T v = fbar[k * SM::DFM + m] + gsum[(k >= nup ? 1 : 0) * d1 + m];
-      if (d1 == NH) v += hbo[k * 4 + m] * RSQ2;
-      hbi[k * d1 + m] = v;
-    }
-    __syncthreads();
   }
+  __syncthreads();
 
   AQ_PH(6);
   // ------------------------------------------------------------------ B3 pair adjoints d(logpsi)/d(x_i - x_k)
