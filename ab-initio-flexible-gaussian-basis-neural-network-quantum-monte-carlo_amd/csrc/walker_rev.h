@@ -82,7 +82,8 @@ struct WCache {
   static constexpr int jaed = jaev + N;             // [48]       dJ_ae/dx per direction lane
   static constexpr int g2 = jaed + 48;              // [3][2][N][4]
   static constexpr int jee = g2 + 3 * 2 * N * 4;    // [1]        J_ee
-  static constexpr int size = ((jee + 1 + 63) / 64) * 64;
+  static constexpr int pt = ((jee + 1 + 3) / 4) * 4; // [N][N][8]  tanh outputs t1, t2 of pair (k, i)
+  static constexpr int size = ((pt + 8 * N * N + 63) / 64) * 64;
 };
 // Per-proposal electron-local stage of the moved electron (k_moved_electron).
 template <int N, int A>
@@ -413,6 +414,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, 
               for (int m = 0; m < 4; ++m) s += p[m] * dw[m * 4 + o];
               q[o] = f_tanh(s);
             }
+            if (!ka.proposal && icol && !diag) {       // walker cache: t_{j+1} of pair (k, i)
+              T* tp = Wc + WC::pt + (k * N + ii) * 8 + j * 4;
+#pragma unroll
+              for (int o = 0; o < 4; ++o) tp[o] = q[o];
+            }
   #pragma unroll
             for (int o = 0; o < 4; ++o) {
               p[o] = (p[o] + q[o]) * RSQ2;
@@ -613,9 +619,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, 
         }
       }
       // g2 adjoints (inputs 3 d1 + 4G + f), consumed by B3
-      if (ilive) {
-        g2b[((l * 2 + 0) * N + ic) * 4 + ff] = fb[3 * T4 + 0];
-        g2b[((l * 2 + 1) * N + ic) * 4 + ff] = fb[3 * T4 + 1];
+      if (ilive) {   // pre-scaled by the group-mean weights 1/|G| of the pair sums
+        g2b[((l * 2 + 0) * N + ic) * 4 + ff] = fb[3 * T4 + 0] * ginv0;
+        g2b[((l * 2 + 1) * N + ic) * 4 + ff] = fb[3 * T4 + 1] * ginv1;
       }
       // group-mean adjoints and h^l adjoints of units m = f + 4t
       T hn = T(0);
@@ -641,45 +647,82 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, 
   AQ_PH(6);
   // ------------------------------------------------------------------ B3 pair adjoints d(logpsi)/d(x_i - x_k)
   T* dbar = sm + SM::dbar;
+  // Proposals from the walker cache: the 2(N-1) pairs of the moved electron pi come first
+  // (iteration 0) and recompute their forward values; every other pair takes t1, t2
+  // from walker pb's cache, so iterations >= 1 skip the forward recompute.
   for (int it = lane; it < N * (N - 1); it += 64) {
-    const int k = it / (N - 1);
-    const int jj = it - k * (N - 1);
-    const int i = jj + (jj >= k ? 1 : 0);
+    int k, i;
+    bool fresh = true;
+    if (reuse) {
+      constexpr int M = 2 * (N - 1);
+      if (it < M) {
+        const int j = it < N - 1 ? it : it - (N - 1);
+        const int o = j + (j >= pi ? 1 : 0);
+        k = it < N - 1 ? pi : o;
+        i = it < N - 1 ? o : pi;
+      } else {
+        if constexpr (N > 2) {
+          const int u = it - M;
+          const int kk = u / (N - 2);
+          const int jj = u - kk * (N - 2);
+          const int ii = jj + (jj >= kk ? 1 : 0);
+          k = kk + (kk >= pi ? 1 : 0);
+          i = ii + (ii >= pi ? 1 : 0);
+          fresh = false;
+        } else {
+          k = i = 0;
+        }
+      }
+    } else {
+      k = it / (N - 1);
+      const int jj = it - k * (N - 1);
+      i = jj + (jj >= k ? 1 : 0);
+    }
     const int G = k >= nup ? 1 : 0;
-    const T gw = G ? ginv1 : ginv0;
     T d[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) d[c] = xs[i * 3 + c] - xs[k * 3 + c];
     const T r = f_sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
     T p0[4] = {r, d[0], d[1], d[2]};
-    // recompute the two double layers (values)
     T t1[4], p1[4], t2[4];
+    if (fresh) {
+      // recompute the two double layers (values)
 #pragma unroll
-    for (int o = 0; o < 4; ++o) {
-      T s = P[Ly::dbl_b0 + o];
+      for (int o = 0; o < 4; ++o) {
+        T s = P[Ly::dbl_b0 + o];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) s += p0[m] * P[Ly::dbl_w0 + m * 4 + o];
-      t1[o] = f_tanh(s);
-    }
+        for (int m = 0; m < 4; ++m) s += p0[m] * P[Ly::dbl_w0 + m * 4 + o];
+        t1[o] = f_tanh(s);
+      }
 #pragma unroll
-    for (int o = 0; o < 4; ++o) p1[o] = (p0[o] + t1[o]) * RSQ2;
+      for (int o = 0; o < 4; ++o) p1[o] = (p0[o] + t1[o]) * RSQ2;
 #pragma unroll
-    for (int o = 0; o < 4; ++o) {
-      T s = P[Ly::dbl_b1 + o];
+      for (int o = 0; o < 4; ++o) {
+        T s = P[Ly::dbl_b1 + o];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) s += p1[m] * P[Ly::dbl_w1 + m * 4 + o];
-      t2[o] = f_tanh(s);
+        for (int m = 0; m < 4; ++m) s += p1[m] * P[Ly::dbl_w1 + m * 4 + o];
+        t2[o] = f_tanh(s);
+      }
+    } else {
+      const T* tp = Wc + WC::pt + (k * N + i) * 8;
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        t1[o] = tp[o];
+        t2[o] = tp[4 + o];
+      }
+#pragma unroll
+      for (int o = 0; o < 4; ++o) p1[o] = (p0[o] + t1[o]) * RSQ2;
     }
     // adjoints: output of layer l feeds g2[l][G][i] with weight 1/|G|
     T pb2[4], pb1[4], pb0[4];
 #pragma unroll
-    for (int f = 0; f < 4; ++f) pb2[f] = g2b[((2 * 2 + G) * N + i) * 4 + f] * gw;
+    for (int f = 0; f < 4; ++f) pb2[f] = g2b[((2 * 2 + G) * N + i) * 4 + f];
     T z2[4];
 #pragma unroll
     for (int o = 0; o < 4; ++o) z2[o] = pb2[o] * RSQ2 * (T(1) - t2[o] * t2[o]);
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      T s = g2b[((1 * 2 + G) * N + i) * 4 + m] * gw + pb2[m] * RSQ2;
+      T s = g2b[((1 * 2 + G) * N + i) * 4 + m] + pb2[m] * RSQ2;
 #pragma unroll
       for (int o = 0; o < 4; ++o) s += z2[o] * P[Ly::dbl_w1 + m * 4 + o];
       pb1[m] = s;
@@ -689,7 +732,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, 
     for (int o = 0; o < 4; ++o) z1[o] = pb1[o] * RSQ2 * (T(1) - t1[o] * t1[o]);
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      T s = g2b[((0 * 2 + G) * N + i) * 4 + m] * gw + pb1[m] * RSQ2;
+      T s = g2b[((0 * 2 + G) * N + i) * 4 + m] + pb1[m] * RSQ2;
 #pragma unroll
       for (int o = 0; o < 4; ++o) s += z1[o] * P[Ly::dbl_w0 + m * 4 + o];
       pb0[m] = s;
