@@ -222,7 +222,7 @@ def main():
             "local_energy_evals_per_s": total_walkers * args.steps / (el_ms_max * 1e-3),
             "mc_walker_steps_per_s": total_walkers * args.nsteps * args.steps / (mc_ms_max * 1e-3),
             "roofline": {
-                "kernel": "k_walker<float,14,2,GRAD> proposal launch (B*N value+gradient configs)",
+                "kernel": "k_walker_rev<float,14,2> proposal launch (B*N value+gradient configs)",
                 "bound": "mfma", "compute_unit": "VALU (fp32 dense peak = VALU peak)", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                 "frac": (achieved / peak) if achieved else None, "traffic": traffic,
                 "avg_launch_ms": prop_avg_ms, "launches": prop_n,
