@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_logpsi", "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_mc_step",
     "aiqmc_workspace_bytes", "aiqmc_last_error", "aiqmc_supported_shapes",
     "aiqmc_profile_enable", "aiqmc_profile_read", "aiqmc_debug_logpsi_grad_forward",
-    "aiqmc_debug_set_proposal_reuse", "aiqmc_debug_phase_cycles",
+    "aiqmc_debug_set_proposal_reuse", "aiqmc_debug_phase_cycles", "aiqmc_debug_local_energy_forward",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -85,6 +85,8 @@ def load() -> ctypes.CDLL:
                                   ctypes.c_uint64, ctypes.c_uint64, vp, vp]
     lib.aiqmc_debug_logpsi_grad_forward.argtypes = [vp, vp, i32, vp, vp, vp]
     lib.aiqmc_debug_logpsi_grad_forward.restype = ctypes.c_int
+    lib.aiqmc_debug_local_energy_forward.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+    lib.aiqmc_debug_local_energy_forward.restype = ctypes.c_int
     lib.aiqmc_debug_set_proposal_reuse.argtypes = [vp, i32]
     lib.aiqmc_debug_set_proposal_reuse.restype = ctypes.c_int
     lib.aiqmc_debug_phase_cycles.argtypes = [vp, vp]
@@ -264,6 +266,17 @@ class Context:
         grad = torch.empty_like(p) if want_grad else None
         check(self._lib.aiqmc_local_energy(self._h, _ptr(p), B, _ptr(el), _ptr(logabs), _ptr(grad),
                                            _stream(self.device)), "aiqmc_local_energy")
+        return el, logabs, grad
+
+    def local_energy_forward_mode(self, pos: torch.Tensor, want_logabs: bool = False, want_grad: bool = False):
+        """Diagnostics: the same quantity through the single-launch forward-Laplacian kernel."""
+        p = self._pos(pos)
+        B = p.shape[0]
+        el = torch.empty(B, dtype=self.dtype, device=self.device)
+        logabs = torch.empty(B, dtype=self.dtype, device=self.device) if want_logabs else None
+        grad = torch.empty_like(p) if want_grad else None
+        check(self._lib.aiqmc_debug_local_energy_forward(self._h, _ptr(p), B, _ptr(el), _ptr(logabs), _ptr(grad),
+                                                         _stream(self.device)), "aiqmc_debug_local_energy_forward")
         return el, logabs, grad
 
     def mc_step(self, pos: torch.Tensor, nsteps: int, tstep: float, gauss1=None, gauss2=None, u=None,

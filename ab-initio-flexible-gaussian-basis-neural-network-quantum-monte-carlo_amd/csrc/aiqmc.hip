@@ -249,6 +249,7 @@ int aiqmc_destroy(aiqmc_ctx* c) {
   (void)hipSetDevice(c->device);
   free_ws(c);
   if (c->d_wcp) (void)hipFree(c->d_wcp);
+  if (c->d_lc) (void)hipFree(c->d_lc);
   for (auto& v : c->ev_used)
     for (auto& p : v) {
       (void)hipEventDestroy(p.first);
@@ -262,7 +263,9 @@ int aiqmc_destroy(aiqmc_ctx* c) {
 }
 
 int64_t aiqmc_param_count(const aiqmc_ctx* c) { return c ? c->ncanon : -1; }
-int64_t aiqmc_workspace_bytes(const aiqmc_ctx* c) { return c ? c->ws_bytes : -1; }
+int64_t aiqmc_workspace_bytes(const aiqmc_ctx* c) {
+  return c ? c->ws_bytes + (int64_t)c->lc_B * c->lc_n * (c->dtype == AIQMC_F32 ? 4 : 8) : -1;
+}
 
 int aiqmc_set_params(aiqmc_ctx* c, const double* flat, int64_t n, void* stream) {
   if (!c || !flat) return fail(AIQMC_EINVAL, "null argument");
@@ -350,13 +353,47 @@ int aiqmc_local_energy(aiqmc_ctx* c, const void* pos, int32_t B, void* e_l, void
   if (!e_l) return fail(AIQMC_EINVAL, "null e_l");
   ShapeOps ops;
   shape_ops(c->N, c->A, &ops);
+  HIPCHK(hipSetDevice(c->device));
+  if (c->lc_B < B) {
+    if (c->d_lc) (void)hipFree(c->d_lc);
+    c->d_lc = nullptr;
+    c->lc_B = 0;
+    HIPCHK(hipMalloc(&c->d_lc, (size_t)B * ops.lcache_n * (c->dtype == AIQMC_F32 ? 4 : 8)));
+    c->lc_B = B;
+    c->lc_n = ops.lcache_n;
+  }
+  // adjoint pass (values, h-stream adjoints, pair sums, B, Phi, Q_f) -> LapCache -> first-derivative pass
+  KArgs k1 = base_args(c);
+  k1.nconf = B;
+  k1.pos = pos;
+  k1.logabs = logabs;
+  k1.lapcache = c->d_lc;
+  KArgs k2 = base_args(c);
+  k2.nconf = B;
+  k2.pos = pos;
+  k2.el = e_l;
+  k2.grad = grad;
+  k2.lapcache = c->d_lc;
+  timed(c, 2, (hipStream_t)stream, [&] { ops.lap(c->dtype, k1, k2, B, (hipStream_t)stream); });
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_debug_local_energy_forward(aiqmc_ctx* c, const void* pos, int32_t B, void* e_l, void* logabs, void* grad,
+                                     void* stream) {
+  int rc = check_call(c, pos, B);
+  if (rc) return rc;
+  if (B == 0) return AIQMC_OK;
+  if (!e_l) return fail(AIQMC_EINVAL, "null e_l");
+  ShapeOps ops;
+  shape_ops(c->N, c->A, &ops);
   KArgs ka = base_args(c);
   ka.nconf = B;
   ka.pos = pos;
   ka.el = e_l;
   ka.logabs = logabs;
   ka.grad = grad;
-  timed(c, 2, (hipStream_t)stream, [&] { ops.walker(c->dtype, MODE_LAP, ka, B, (hipStream_t)stream); });
+  ops.walker(c->dtype, MODE_LAP, ka, B, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
 }

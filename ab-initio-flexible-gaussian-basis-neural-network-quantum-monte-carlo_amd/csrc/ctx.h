@@ -34,6 +34,8 @@ struct aiqmc_ctx {
   void *d_wc = nullptr, *d_ec = nullptr;                    // Metropolis caches (walker_rev.h WCache/ECache)
   void* d_wcp = nullptr;                                    // per-proposal cache scratch (reuse off)
   int wcp_B = 0;
+  void* d_lc = nullptr;                                     // local-energy LapCache [B][lcache_n]
+  int lc_B = 0, lc_n = 0;
   bool reuse = true;                                        // proposals reuse the walker's cached stage
   double* d_taueff = nullptr;
   int64_t ws_bytes = 0;
@@ -50,8 +52,11 @@ struct ShapeOps {
                  const void* g1, const void* g2, const void* u, const double* te, int B, double tstep,
                  int32_t* acc, hipStream_t s);
   void (*moved)(int dtype, const KArgs& ka, hipStream_t s);   // k_moved_electron over ka.nconf proposals
+  // local energy: adjoint pass (k1) + first-derivative pass (k2), walker_lap.h
+  void (*lap)(int dtype, const KArgs& k1, const KArgs& k2, int nconf, hipStream_t s);
   void (*phase_read)(unsigned long long* out32);               // AQ_PHASE_PROF builds only
   int wcache_n, ecache_n;                                      // cache entries per walker / per proposal
+  int lcache_n;                                                // LapCache entries per walker
   int64_t nkern;
   long (*ncanon)(int npar, int nanti);
   void (*pack)(const aiqmc_ctx* c, const double* flat, std::vector<double>& out);

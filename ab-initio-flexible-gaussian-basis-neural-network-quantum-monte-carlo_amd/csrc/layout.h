@@ -85,4 +85,23 @@ struct Lay {
   }
 };
 
+// Per-walker cache of the local-energy launch pair (walker_lap.h): written by the
+// adjoint pass k_walker_rev<..., PREP>, read by k_walker_lap.
+template <int N, int A>
+struct LapCache {
+  static constexpr int D0 = 4 * A;
+  static constexpr int QM = (3 * D0 + 2 * NH2) / 4;   // conv outputs of layer 0 (the widest layer)
+  // one block per h-stream layer l at l * layer_n (staged in LDS a layer at a time)
+  static constexpr int cn = 0;                        // [N][QM][2]  conv nodes: 1 - c^2, abar phi''(z)
+  static constexpr int sn = cn + N * QM * 2;          // [N][4][2]   single nodes: 1 - s^2, abar phi''(z)
+  static constexpr int sd = sn + N * NH * 2;          // [2][N][3][4] sum_{k in G, k != i} dh2[k,i][f] / d(x_i - x_k)_c
+  static constexpr int layer_n = (sd + 2 * N * 3 * NH2 + 3) / 4 * 4;
+  static constexpr int h0b = 3 * layer_n;             // [N][D0]     adjoint of the layer-0 features
+  static constexpr int bm = (h0b + N * D0 + 3) / 4 * 4;   // [N][N][2] B = A^{-1}
+  static constexpr int ph = bm + 2 * N * N;           // [N][N][2]   Phi
+  static constexpr int qs = ph + 2 * N * N;           // [N][N][4][2] Q_f[r,s] = sum_c W_{s(r)}[f,c] Yt[r,c] B[c,s]
+  static constexpr int scal = qs + 8 * N * N;         // [0]         pair-local part of the Laplacian
+  static constexpr int size = (scal + 4 + 31) / 32 * 32;
+};
+
 }  // namespace aq

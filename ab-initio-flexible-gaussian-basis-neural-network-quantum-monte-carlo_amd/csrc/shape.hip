@@ -6,7 +6,7 @@
 #include <cstring>
 
 #include "ctx.h"
-#include "walker_rev.h"
+#include "walker_lap.h"
 
 using namespace aq;
 
@@ -216,6 +216,18 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
   }
 }
 
+// Local energy: adjoint pass (k_walker_rev<PREP>) then first-derivative pass (k_walker_lap).
+template <int N, int A>
+static void lap_impl(int dtype, const KArgs& k1, const KArgs& k2, int nconf, hipStream_t s) {
+  if (dtype == AIQMC_F32) {
+    k_walker_rev<float, N, A, true><<<dim3(nconf), dim3(64), SmemRev<float, N, A>::bytes, s>>>(k1);
+    k_walker_lap<float, N, A><<<dim3(nconf), dim3(64), SmemLap<float, N, A>::bytes, s>>>(k2);
+  } else {
+    k_walker_rev<double, N, A, true><<<dim3(nconf), dim3(64), SmemRev<double, N, A>::bytes, s>>>(k1);
+    k_walker_lap<double, N, A><<<dim3(nconf), dim3(64), SmemLap<double, N, A>::bytes, s>>>(k2);
+  }
+}
+
 template <int N, int A>
 static void moved_impl(int dtype, const KArgs& ka, hipStream_t s) {
   const int nb = (ka.nconf + 15) / 16;
@@ -255,6 +267,8 @@ bool AQ_CAT(AQ_N, AQ_A)(ShapeOps* ops) {
   ops->walker = &walker_impl<AQ_N, AQ_A>;
   ops->accept = &accept_impl<AQ_N, AQ_A>;
   ops->moved = &moved_impl<AQ_N, AQ_A>;
+  ops->lap = &lap_impl<AQ_N, AQ_A>;
+  ops->lcache_n = LapCache<AQ_N, AQ_A>::size;
   ops->phase_read = &phase_read_impl;
   ops->wcache_n = WCache<AQ_N, AQ_A>::size;
   ops->ecache_n = ECache<AQ_N, AQ_A>::size;

@@ -50,6 +50,8 @@ struct KArgs {
   // Metropolis caches (walker_rev.h WCache / ECache); nullptr outside aiqmc_mc_step
   void* wcache;
   void* ecache;
+  // local-energy launch pair (walker_lap.h LapCache); nullptr elsewhere
+  void* lapcache;
   // outputs (nullable)
   void* logabs;           // [nconf]
   void* phase;            // [nconf]

@@ -1,0 +1,363 @@
+// walker_lap.h -- local energy E_L = V - (lap log|psi| + |grad log|psi||^2) / 2 of the AIQMC
+// wavefunction (Energy/hamiltonian.py:236-260, complex_output=False; the reference's
+// jvp-of-grad loop :100-131) in two launches, one wavefront per walker each.
+//
+// 1. k_walker_rev<T,N,A,PREP=true> (walker_rev.h): the reverse-mode kernel's value pass
+//    and its adjoint pass through the mean-field (h) stream; writes the walker's
+//    LapCache (layout.h): for every tanh node m of the h stream its derivative 1 - t^2 and
+//    its curvature weight abar_m phi''(z_m) (abar = d log|det A| / d node, phi'' =
+//    -2 t (1 - t^2)); the adjoints of the layer-0 features; the pair-stream derivative
+//    sums sd; B = A^{-1}, Phi, Q_f = P_f B; and the pair-local part of the Laplacian.
+//
+// 2. k_walker_lap<T,N,A> (this file) carries FIRST derivatives only, lane (c, e) = the
+//    direction x_{e,c} (jets.h layout).  Every h-stream node is tanh of a linear map, so
+//    the determinant's term sum_{r,f} Hbar[r,f] lap H[r,f] (Hbar = Re Q_f[r,r]) equals
+//        sum_m abar_m phi''(z_m) |grad z_m|^2  +  sum_leaves abar_leaf lap(leaf)
+//    (leaves: the ae features, the pair terms of the column means g2).  Each direction
+//    lane adds abar_m phi''(z_m) (dz_m/dx_{e,c})^2 per node; no lane carries second
+//    derivatives through the dense stream (the forward-Laplacian kernel walker_kernel.h
+//    does, with twice the per-lane state and one wave per SIMD).  The determinant's own
+//    second-order terms use its low-rank structure (walker_kernel.h header):
+//        Re[(2 dPhi_e.Yt' + Phi_e.Yt'') b_e - sum_{r,s} S_rs S_sr - 2 sum_r z_r S_re - (w.b_e)^2]
+//    with S = sum_f diag(U_f) Q_f, U = dH/dx_{e,c}, w = Phi[e,:] dYt[e,:], z = B^T w.  The
+//    Jastrow factors and the per-electron stage (envelope, Ylm stream, ae features) are
+//    second-order jets along the lane direction.
+#pragma once
+#include "electron.h"
+#include "jets.h"
+#include "layout.h"
+#include "walker_kernel.h"
+#include "walker_rev.h"
+
+namespace aq {
+
+template <typename T, int N, int A>
+struct SmemLap {
+  static constexpr int xs = 0;                               // [48] positions
+  static constexpr int ly = 48;                              // one layer's LapCache block
+  // lane-private arrays [..][49]: direction lanes 0..47 own a column; the 16 value-row
+  // lanes share column 48 (they carry no derivatives; their stores there are don't-cares)
+  static constexpr int hb = ly + LapCache<N, A>::layer_n;    // [N][4][49] dh/dx
+  static constexpr int yd = hb + N * NH * 49;                // [2][N][49] dYt/dx, d2Yt/dx2 of row le
+  static constexpr int end = yd + 2 * N * 49;
+  static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
+};
+
+// One h-stream layer (nn.py:280-311) in first derivatives, column loop over electrons i.
+// ly: this layer's LapCache block (LDS); hb: dh/dx of every electron, updated in place
+// (column `lane` = min(lane, 48), see SmemLap).
+template <typename T, int N, int A, int L>
+__device__ __forceinline__ void lap_layer(cptr<T> P, const T* xs, T* hb, const T* ly, const PJ<T>* hf, int lane,
+                                          int lc, int er, int le, bool val, bool dir, bool live, int nup, T& jd1,
+                                          T& jd2, T& vv, T& acc) {
+  using Ly = Lay<N, A>;
+  using LC = LapCache<N, A>;
+  constexpr int DIN = (L == 0) ? 4 * A : NH;
+  constexpr int DF = 3 * DIN + 2 * NH2;
+  constexpr int Q = DF / 4;
+  const cptr<T> convw = P + (L == 0 ? Ly::conv_w0 : (L == 1 ? Ly::conv_w1 : Ly::conv_w2));
+  const cptr<T> sngw = P + (L == 0 ? Ly::sng_w0 : (L == 1 ? Ly::sng_w1 : Ly::sng_w2));
+  const T ginv[2] = {T(1) / T(nup), T(1) / T(N - nup)};
+  const T RSQ2 = T(0.70710678118654752);   // residual (x + y)/sqrt(2), nn.py:284
+  const bool inG[2] = {live && er < nup, live && er >= nup};
+  const int c3 = lc < 3 ? lc : 0;
+
+  // spin-group means of h (construct_symmetric_features, nn.py:142-150)
+  T g1[2][DIN];
+  if constexpr (L == 0) {
+#pragma unroll
+    for (int G = 0; G < 2; ++G)
+#pragma unroll
+      for (int m = 0; m < DIN; ++m) g1[G][m] = (dir && inG[G]) ? hf[m].d1 * ginv[G] : T(0);
+  } else {
+#pragma unroll
+    for (int m = 0; m < DIN; ++m) g1[0][m] = g1[1][m] = T(0);
+    for (int k = 0; k < nup; ++k)
+#pragma unroll
+      for (int m = 0; m < DIN; ++m) g1[0][m] += hb[(k * NH + m) * 49 + lane];
+    for (int k = nup; k < N; ++k)
+#pragma unroll
+      for (int m = 0; m < DIN; ++m) g1[1][m] += hb[(k * NH + m) * 49 + lane];
+#pragma unroll
+    for (int m = 0; m < DIN; ++m) {
+      g1[0][m] *= ginv[0];
+      g1[1][m] *= ginv[1];
+    }
+  }
+
+#pragma unroll 1
+  for (int i = 0; i < N; ++i) {
+    const bool diag = (le == i);
+    T d[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) d[c] = xs[i * 3 + c] - xs[le * 3 + c];
+    const T r = f_sqrt(diag ? T(1) : d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    const T ir = f_rcp(r);
+    const T dl = c3 == 0 ? d[0] : (c3 == 1 ? d[1] : d[2]);
+    const T r1 = -dl * ir;   // dr/dx_{le,lc}, with d = x_i - x_le
+    if constexpr (L == 0) {
+      // Pade e-e Jastrow term cusp r / (1 + alpha r) of pair (le, i) (Jastrow.py:51-52)
+      const T cusp = P[Ly::jee_c + le * N + i];
+      const T al = P[Ly::jee_a + le * N + i];
+      const T iden = f_rcp(al * r + T(1));
+      const T j1 = cusp * iden * iden;          // J'(r)
+      const T j2 = T(-2) * al * j1 * iden;      // J''(r)
+      if (dir && !diag) {
+        jd1 += j1 * r1;
+        jd2 += j2 * r1 * r1 + j1 * (T(1) - r1 * r1) * ir;
+      }
+      if (val && live && er < i) vv += ir;      // V_ee, each pair once (hamiltonian.py:177-187)
+    }
+    // pair stream h2[le,i] = [r, x_i - x_le] through L double layers (nn.py:305-309): value and
+    // derivative along x_{le,lc}
+    T pv[4], pd[4];
+    pv[0] = r;
+    pd[0] = r1;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      pv[1 + c] = d[c];
+      pd[1 + c] = (lc == c) ? T(-1) : T(0);
+    }
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const cptr<T> dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
+      const cptr<T> db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
+      T tv[4], td[4];
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        T zv = db[o], zd = T(0);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          zv += pv[m] * dw[m * 4 + o];
+          zd += pd[m] * dw[m * 4 + o];
+        }
+        tv[o] = f_tanh(zv);
+        td[o] = (T(1) - tv[o] * tv[o]) * zd;
+      }
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        pv[o] = (pv[o] + tv[o]) * RSQ2;
+        pd[o] = (pd[o] + td[o]) * RSQ2;
+      }
+    }
+    // column means of h2 over the spin groups (nn.py:151): lane (c, e != i) sees pair (e, i)
+    // only; lane (c, i) sees every pair (k, i) -- their derivative sums from the LapCache
+    const T* sdp = ly + LC::sd + (i * 3 + c3) * 4;
+    T g2[2][4];
+#pragma unroll
+    for (int G = 0; G < 2; ++G) {
+      const T cP = (dir && inG[G] && !diag) ? ginv[G] : T(0);
+      const T cS = (dir && diag) ? ginv[G] : T(0);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) g2[G][f] = cP * pd[f] + cS * sdp[G * N * 3 * 4 + f];
+    }
+    // h_i
+    T hi[DIN];
+#pragma unroll
+    for (int m = 0; m < DIN; ++m) {
+      if constexpr (L == 0) hi[m] = (diag && dir) ? hf[m].d1 : T(0);
+      else hi[m] = hb[(i * NH + m) * 49 + lane];
+    }
+    // convolutional layer c = tanh(mean_4(f w) + b) (network_blocks.py:106-116)
+    const T* cn = ly + LC::cn + i * LC::QM * 2;
+    T cq[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      T z = T(0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int idx = 4 * q + s;
+        T F;
+        if (idx < DIN) F = hi[idx];
+        else if (idx < 2 * DIN) F = g1[0][idx - DIN];
+        else if (idx < 3 * DIN) F = g1[1][idx - 2 * DIN];
+        else if (idx < 3 * DIN + 4) F = g2[0][idx - 3 * DIN];
+        else F = g2[1][idx - 3 * DIN - 4];
+        z += convw[i * DF + idx] * F;
+      }
+      z *= T(0.25);
+      cq[q] = cn[2 * q] * z;
+      acc += cn[2 * q + 1] * z * z;
+    }
+    // single linear + tanh + residual (nn.py:296-300)
+    const T* sn = ly + LC::sn + i * NH * 2;
+#pragma unroll
+    for (int f = 0; f < NH; ++f) {
+      T z = T(0);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) z += sngw[q * NH + f] * cq[q];
+      const T s1 = sn[2 * f] * z;
+      acc += sn[2 * f + 1] * z * z;
+      hb[(i * NH + f) * 49 + lane] = (DIN == NH) ? (hi[f] + s1) * RSQ2 : s1;
+    }
+  }
+}
+
+template <typename T, int N, int A>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_walker_lap(KArgs ka) {
+  using Ly = Lay<N, A>;
+  using LC = LapCache<N, A>;
+  using SM = SmemLap<T, N, A>;
+  constexpr int D0 = 4 * A;
+  const cptr<T> P = param_ptr<T>(ka.prm);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  T* sm = (T*)smem_raw;
+  T* xs = sm + SM::xs;
+  T* ly = sm + SM::ly;
+  T* hb = sm + SM::hb;
+
+  const int conf = xcd_major(blockIdx.x, gridDim.x);   // same walker -> XCD map as the adjoint pass
+  const int lane = threadIdx.x;
+  const int lc = lane >> 4;
+  const int er = lane & 15;
+  const int le = er < N ? er : N - 1;
+  const bool val = (lc == 3);
+  const bool live = er < N;
+  const bool dir = (lc < 3) && live;
+  const int nup = ka.nup;
+  const int l49 = lane < 48 ? lane : 48;
+  T* yd = sm + SM::yd;
+  const cptr<T> Lc = (const T*)ka.lapcache + (size_t)conf * LC::size;
+
+  if (lane < 3 * N) xs[lane] = ((const T*)ka.pos)[(size_t)conf * 3 * N + lane];
+  T h0b[D0];
+#pragma unroll
+  for (int m = 0; m < D0; ++m) h0b[m] = Lc[LC::h0b + le * D0 + m];
+  for (int idx = lane; idx < LC::layer_n; idx += 64) ly[idx] = Lc[idx];
+  __syncthreads();
+
+  // ------------------------------------------------------------------ per-electron stage (electron.h)
+  ElecOut<T, A> eo;
+  electron_stage<T, N, A>(P, xs + le * 3, le, lc, eo);
+  T vv = (val && live) ? eo.ven : T(0);
+  T acc = T(0);   // curvature sources, per direction lane
+#pragma unroll
+  for (int m = 0; m < D0; ++m) acc += h0b[m] * eo.hf[m].d2;   // ae features as leaves
+  // Yt row of electron le, first and second derivatives (nn.py:449-452, 479-485) -> LDS
+#pragma unroll
+  for (int col = 0; col < N; ++col) {
+    PJ<T> s = P[Ly::wy + col] * eo.yst[0];
+#pragma unroll
+    for (int m = 1; m < NYW; ++m) s = s + P[Ly::wy + m * N + col] * eo.yst[m];
+    const PJ<T> yt = eo.env * s;
+    yd[col * 49 + l49] = yt.d1;
+    yd[(N + col) * 49 + l49] = yt.d2;
+  }
+  T jd1 = dir ? eo.jae.d1 : T(0);
+  T jd2 = dir ? eo.jae.d2 : T(0);
+
+  // ------------------------------------------------------------------ h stream, first derivatives
+  lap_layer<T, N, A, 0>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc);
+  __syncthreads();
+  for (int idx = lane; idx < LC::layer_n; idx += 64) ly[idx] = Lc[LC::layer_n + idx];
+  __syncthreads();
+  lap_layer<T, N, A, 1>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc);
+  __syncthreads();
+  for (int idx = lane; idx < LC::layer_n; idx += 64) ly[idx] = Lc[2 * LC::layer_n + idx];
+  __syncthreads();
+  lap_layer<T, N, A, 2>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc);
+
+  // ------------------------------------------------------------------ determinant terms
+  // (phases fenced so that the scheduler does not stretch their live ranges across each other)
+  const int* rowsrc = ka.rowsrc;
+  using cT = const __attribute__((address_space(4))) T;   // wave-uniform reads -> scalar loads
+  cT* Qs = (cT*)(Lc + LC::qs);
+  cT* Bu = (cT*)(Lc + LC::bm);
+  const cptr<T> Bm = Lc + LC::bm;
+  const cptr<T> Ph = Lc + LC::ph;
+#define UH(r, f) hb[(rowsrc[r] * NH + (f)) * 49 + l49]
+  // E1: Yt row jets of electron le (stored after the per-electron stage)
+  T Yd1[N], Yd2[N];
+#pragma unroll
+  for (int col = 0; col < N; ++col) {
+    Yd1[col] = yd[col * 49 + l49];
+    Yd2[col] = yd[(N + col) * 49 + l49];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // E2: w = Phi[e,:] * dYt[e,:], w.b_e, and t2 = Re sum_col (2 dPhi[e,col] Yt'[col] +
+  //     Phi[e,col] Yt''[col]) B[col,e] with e = le (U of row e)
+  const int spe = le < nup ? 0 : 1;
+  T Ue[NH];
+#pragma unroll
+  for (int f = 0; f < NH; ++f) Ue[f] = UH(le, f);
+  T wr[N], wi[N];
+  T wbr = T(0), wbi = T(0), t2 = T(0);
+#pragma unroll
+  for (int col = 0; col < N; ++col) {
+    const T pr = Ph[(le * N + col) * 2], pm = Ph[(le * N + col) * 2 + 1];
+    const T br = Bm[(col * N + le) * 2], bi = Bm[(col * N + le) * 2 + 1];
+    wr[col] = pr * Yd1[col];
+    wi[col] = pm * Yd1[col];
+    wbr += wr[col] * br - wi[col] * bi;
+    wbi += wr[col] * bi + wi[col] * br;
+    T dpr = T(0), dpi = T(0);
+#pragma unroll
+    for (int f = 0; f < NH; ++f) {
+      dpr += Ue[f] * P[Ly::orb_w + ((spe * NH + f) * N + col) * 2];
+      dpi += Ue[f] * P[Ly::orb_w + ((spe * NH + f) * N + col) * 2 + 1];
+    }
+    const T xr = T(2) * dpr * Yd1[col] + pr * Yd2[col];
+    const T xi = T(2) * dpi * Yd1[col] + pm * Yd2[col];
+    t2 += xr * br - xi * bi;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // E3: gradient: sum_{r,f} U Re Q_f[r,r] + Re(w . b_e) + Jastrow
+  T g = jd1 + wbr;
+#pragma unroll 2
+  for (int r = 0; r < N; ++r)
+#pragma unroll
+    for (int f = 0; f < NH; ++f) g += UH(r, f) * Qs[((r * N + r) * NH + f) * 2];
+  // E4: cross = Re sum_r z_r S_re (z = B^T w);  ss = Re sum_{r,s} S_rs S_sr,  S_rs = sum_f U_rf Q_f[r,s]
+  T cross = T(0), ss = T(0);
+#pragma unroll 1
+  for (int r = 0; r < N; ++r) {
+    T ur[NH];
+#pragma unroll
+    for (int f = 0; f < NH; ++f) ur[f] = UH(r, f);
+    T zr = T(0), zi = T(0);
+#pragma unroll
+    for (int col = 0; col < N; ++col) {
+      const T br = Bu[(col * N + r) * 2], bi = Bu[(col * N + r) * 2 + 1];
+      zr += br * wr[col] - bi * wi[col];
+      zi += br * wi[col] + bi * wr[col];
+    }
+    T sr = T(0), si = T(0), dr = T(0), di = T(0);
+#pragma unroll
+    for (int f = 0; f < NH; ++f) {
+      sr += ur[f] * Qs[((r * N + le) * NH + f) * 2];
+      si += ur[f] * Qs[((r * N + le) * NH + f) * 2 + 1];
+      dr += ur[f] * Qs[((r * N + r) * NH + f) * 2];
+      di += ur[f] * Qs[((r * N + r) * NH + f) * 2 + 1];
+    }
+    cross += zr * sr - zi * si;
+    ss += dr * dr - di * di;
+#pragma unroll 1
+    for (int s = r + 1; s < N; ++s) {
+      T ar = T(0), ai = T(0), br = T(0), bi = T(0);
+#pragma unroll
+      for (int f = 0; f < NH; ++f) {
+        const T us = UH(s, f);
+        ar += ur[f] * Qs[((r * N + s) * NH + f) * 2];
+        ai += ur[f] * Qs[((r * N + s) * NH + f) * 2 + 1];
+        br += us * Qs[((s * N + r) * NH + f) * 2];
+        bi += us * Qs[((s * N + r) * NH + f) * 2 + 1];
+      }
+      ss += T(2) * (ar * br - ai * bi);
+    }
+  }
+#undef UH
+  const T lap = t2 - (ss + T(2) * cross + (wbr * wbr - wbi * wbi)) + jd2 + acc;
+
+  // ------------------------------------------------------------------ outputs
+  const T gd = dir ? g : T(0);
+  const T sumsq = wave_sum(gd * gd);
+  if (ka.grad && dir) ((T*)ka.grad)[(size_t)conf * 3 * N + 3 * le + lc] = g;
+  const T kin = T(-0.5) * (wave_sum(dir ? lap : T(0)) + Lc[LC::scal] + sumsq);   // hamiltonian.py:126-127
+  const T pot = wave_sum(vv) + P[Ly::vnn];
+  if (lane == 0) {
+    if (ka.el) ((T*)ka.el)[conf] = pot + kin;
+    if (ka.sumsq) ((T*)ka.sumsq)[conf] = sumsq;
+  }
+}
+
+}  // namespace aq

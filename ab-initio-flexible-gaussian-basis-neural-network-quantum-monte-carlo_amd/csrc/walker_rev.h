@@ -194,15 +194,21 @@ __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
 
 // Occupancy hint per instantiation: fp32 N2 (14, 2) lands one VGPR above the
 // 4-waves/SIMD budget (128) without it and fits it without spilling with it.
-template <typename T, int N, int A> struct RevWaves {
-  static constexpr int value = (sizeof(T) == 4 && N == 14 && A == 2) ? 4 : 1;
+// PREP (the adjoint pass of the local energy, walker_lap.h) asks for 2.
+template <typename T, int N, int A, bool PREP> struct RevWaves {
+  static constexpr int value = PREP ? 2 : ((sizeof(T) == 4 && N == 14 && A == 2) ? 4 : 1);
 };
 
-template <typename T, int N, int A>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, N, A>::value))) void k_walker_rev(
-    KArgs ka) {
+// PREP = false: value + gradient (Metropolis walker and proposal launches).
+// PREP = true : first launch of the local energy (walker_lap.h): values, the adjoint pass
+//   through the h stream, and the pair stream's derivative sums and curvature, written to
+//   the walker's LapCache; no gradient (B3/B4) and no Metropolis cache.
+template <typename T, int N, int A, bool PREP = false>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, N, A, PREP>::value))) void
+k_walker_rev(KArgs ka) {
   using Ly = Lay<N, A>;
   using SM = SmemRev<T, N, A>;
+  using LCc = LapCache<N, A>;
   constexpr int D0 = SM::D0;
   const cptr<T> P = param_ptr<T>(ka.prm);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -249,8 +255,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, 
   // Walker cache: read (proposal with reuse: this proposal's walker pb) or written (by conf).
   using WC = WCache<N, A>;
   using EC = ECache<N, A>;
-  const bool reuse = ka.proposal && ka.ecache != nullptr;
+  const bool reuse = !PREP && ka.proposal && ka.ecache != nullptr;
   T* Wc = (T*)ka.wcache + (size_t)(reuse ? pb : conf) * WC::size;
+  T* Lw = PREP ? (T*)ka.lapcache + (size_t)conf * LCc::size : nullptr;
   const T* Eq = reuse ? (const T*)ka.ecache + (size_t)conf * EC::size : nullptr;
   T* Yv = sm + SM::yv;
   T* g2 = sm + SM::g2;
@@ -300,23 +307,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, 
 #pragma unroll
       for (int m = 1; m < NYW; ++m) sy = sy + P[Ly::wy + m * N + col] * eo.yst[m];
       const PJ<T> yt = eo.env * sy;
-      if (lane < 48) Wl[col * 48] = yt.d1;
+      if (!PREP && lane < 48) Wl[col * 48] = yt.d1;
       if (val && live) Yv[er * N + col] = yt.v;
     }
 #pragma unroll
     for (int m = 0; m < D0; ++m) {
-      if (lane < 48) Wl[(N + m) * 48] = eo.hf[m].d1;
+      if (!PREP && lane < 48) Wl[(N + m) * 48] = eo.hf[m].d1;
       if (val && live) sm[SM::hl + er * D0 + m] = eo.hf[m].v;
     }
     jv = (val && live) ? eo.jae.v : T(0);
     jd1 = dir ? eo.jae.d1 : T(0);
-    if (!ka.proposal) {
+    if (!PREP && !ka.proposal) {
       if (val && live) Wc[WC::jaev + er] = eo.jae.v;
       if (lane < 48) Wc[WC::jaed + lane] = jd1;
     }
   }
   __syncthreads();
-  if (!ka.proposal) {
+  if (!PREP && !ka.proposal) {
     for (int idx = lane; idx < N * N; idx += 64) Wc[WC::yv + idx] = Yv[idx];
     for (int idx = lane; idx < N * D0; idx += 64) Wc[WC::h0 + idx] = sm[SM::hl + idx];
   }
@@ -414,7 +421,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, 
               for (int m = 0; m < 4; ++m) s += p[m] * dw[m * 4 + o];
               q[o] = f_tanh(s);
             }
-            if (!ka.proposal && icol && !diag) {       // walker cache: t_{j+1} of pair (k, i)
+            if (!PREP && !ka.proposal && icol && !diag) {   // walker cache: t_{j+1} of pair (k, i)
               T* tp = Wc + WC::pt + (k * N + ii) * 8 + j * 4;
 #pragma unroll
               for (int o = 0; o < 4; ++o) tp[o] = q[o];
@@ -442,7 +449,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, 
     }
   }
   __syncthreads();
-  if (!ka.proposal) {
+  if (!PREP && !ka.proposal) {
     for (int idx = lane; idx < 3 * 2 * N * 4; idx += 64) Wc[WC::g2 + idx] = g2[idx];
     const T je = wave_sum(jve);
     if (lane == 0) Wc[WC::jee] = je;
@@ -578,10 +585,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, 
     }
     hbar[SM::hoff(3) + rowsrc[r] * 4 + f] = q;
   }
+  if constexpr (PREP) {
+    // B, Phi and Q_f[r,s] = sum_c W_{s(r)}[f,c] Yt[r,c] B[c,s] for the determinant terms
+    for (int idx = lane; idx < 2 * N * N; idx += 64) {
+      Lw[LCc::bm + idx] = Mx[idx];
+      Lw[LCc::ph + idx] = Ph[idx];
+    }
+    for (int idx = lane; idx < NH * N * N; idx += 64) {
+      const int rs = idx >> 2, f = idx & 3;
+      const int r = rs / N, s = rs - r * N;
+      const int sp = r < nup ? 0 : 1;
+      T qr = T(0), qi = T(0);
+      for (int c = 0; c < N; ++c) {
+        const T yv = Yv[r * N + c];
+        const T wr = P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2] * yv;
+        const T wi = P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 1] * yv;
+        qr += wr * BRE(c, s) - wi * BIM(c, s);
+        qi += wr * BIM(c, s) + wi * BRE(c, s);
+      }
+      Lw[LCc::qs + idx * 2] = qr;
+      Lw[LCc::qs + idx * 2 + 1] = qi;
+    }
+  }
   __syncthreads();   // ybar overwrites Yt
-  for (int idx = lane; idx < N * N; idx += 64) {
-    const int r = idx / N, c = idx - r * N;
-    ybar[idx] = BRE(c, r) * Ph[idx * 2] - BIM(c, r) * Ph[idx * 2 + 1];
+  if constexpr (!PREP) {
+    for (int idx = lane; idx < N * N; idx += 64) {
+      const int r = idx / N, c = idx - r * N;
+      ybar[idx] = BRE(c, r) * Ph[idx * 2] - BIM(c, r) * Ph[idx * 2 + 1];
+    }
   }
 #undef BRE
 #undef BIM
@@ -605,6 +636,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, 
       const T sval = sv[(l * N + ic) * 4 + ff];
       const T sb = (d1 == NH) ? hb * RSQ2 : hb;
       const T zs = sb * (T(1) - sval * sval);
+      if constexpr (PREP) {
+        // single node: tanh' and the curvature weight abar * tanh''(z) = sb * (-2 s (1 - s^2))
+        if (ilive) {
+          T* sn = Lw + l * LCc::layer_n + LCc::sn + (ic * NH + ff) * 2;
+          sn[0] = T(1) - sval * sval;
+          sn[1] = T(-2) * sval * zs;
+        }
+      }
       const T zq[4] = {quad_bcast<0>(zs), quad_bcast<1>(zs), quad_bcast<2>(zs), quad_bcast<3>(zs)};
       // conv: c = tanh(0.25 sum F w + b); fb[q] = adjoint of input 4q + f
       T fb[SM::QM];
@@ -616,6 +655,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, 
           for (int m = 0; m < 4; ++m) cb += zq[m] * sngw[q * 4 + m];
           const T c = cqv[(l * N + ic) * SM::QM + q];
           fb[q] = cb * (T(1) - c * c) * T(0.25) * convw[4 * q + ff];
+          if constexpr (PREP) {
+            // conv node (stored once, by the lane of its quad position): tanh', abar * tanh''
+            if (ilive && (q & 3) == ff) {
+              const T c1 = T(1) - c * c;
+              T* cn = Lw + l * LCc::layer_n + LCc::cn + (ic * LCc::QM + q) * 2;
+              cn[0] = c1;
+              cn[1] = T(-2) * c * c1 * cb;
+            }
+          }
         }
       }
       // g2 adjoints (inputs 3 d1 + 4G + f), consumed by B3
@@ -643,6 +691,99 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, 
     }
   }
   __syncthreads();
+
+  if constexpr (PREP) {
+    // ---------------------------------------------------------------- local-energy adjoint pass: tail
+    for (int idx = lane; idx < N * D0; idx += 64) Lw[LCc::h0b + idx] = hbar[idx];
+    // Pair stream in the direction-lane layout: lane (c, i) runs over k and propagates h2[k,i]
+    // with its first and second derivatives along d_c, d = x_i - x_k, through the double layers.
+    //  * sd[l][G][i][c][f] = sum_{k in G, k != i} d h2^{(l)}[k,i][f] / d d_c  (k_walker_lap: the
+    //    derivative of the column mean g2 along x_{i,c});
+    //  * pair-local Laplacian: sum over the pair terms of g2 of their adjoint (g2b, already
+    //    scaled by 1/|G|) times their Laplacian in (x_k, x_i) = 2 sum_c d^2/d d_c^2.
+    const int qc = lane >> 4, qi = lane & 15;
+    const bool plive = qc < 3 && qi < N;
+    const int ii = qi < N ? qi : N - 1;
+    const int c3 = qc < 3 ? qc : 0;
+    T pcurv = T(0);
+    T sdv[3][2][4];
+#pragma unroll
+    for (int l = 0; l < 3; ++l)
+#pragma unroll
+      for (int G = 0; G < 2; ++G)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) sdv[l][G][f] = T(0);
+#pragma unroll
+    for (int G = 0; G < 2; ++G) {
+      const int k0 = G ? nup : 0, k1 = G ? N : nup;
+      const T* gb = g2b + (G * N + ii) * 4;        // level l at + l * 2 * N * 4
+#pragma unroll 1
+      for (int k = k0; k < k1; ++k) {
+        const bool dg = (k == ii);
+        const T m = (plive && !dg) ? T(1) : T(0);
+        T d[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) d[c] = xs[ii * 3 + c] - xs[k * 3 + c];
+        const T r = f_sqrt(dg ? T(1) : d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+        const T ir = f_rcp(r);
+        const T u = (c3 == 0 ? d[0] : (c3 == 1 ? d[1] : d[2])) * ir;
+        T pv[4] = {r, d[0], d[1], d[2]};
+        T p1[4] = {u, c3 == 0 ? T(1) : T(0), c3 == 1 ? T(1) : T(0), c3 == 2 ? T(1) : T(0)};
+        T p2[4] = {(T(1) - u * u) * ir, T(0), T(0), T(0)};
+#pragma unroll
+        for (int f = 0; f < 4; ++f) sdv[0][G][f] += m * p1[f];
+        pcurv += m * gb[0] * p2[0];                 // level 0: only r has curvature
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const cptr<T> dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
+          const cptr<T> db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
+          T tv[4], z1[4], z2[4];
+#pragma unroll
+          for (int o = 0; o < 4; ++o) {
+            T zv = db[o], a1 = T(0), a2 = (j == 0) ? p2[0] * dw[o] : T(0);
+#pragma unroll
+            for (int mm = 0; mm < 4; ++mm) {
+              zv += pv[mm] * dw[mm * 4 + o];
+              a1 += p1[mm] * dw[mm * 4 + o];
+              if (j > 0) a2 += p2[mm] * dw[mm * 4 + o];
+            }
+            tv[o] = f_tanh(zv);
+            z1[o] = a1;
+            z2[o] = a2;
+          }
+          const T* gl = gb + (j + 1) * 2 * N * 4;
+#pragma unroll
+          for (int o = 0; o < 4; ++o) {
+            const T s = T(1) - tv[o] * tv[o];
+            const T t1 = s * z1[o];
+            const T t2 = s * (z2[o] - T(2) * tv[o] * z1[o] * z1[o]);
+            pv[o] = (pv[o] + tv[o]) * RSQ2;
+            p1[o] = (p1[o] + t1) * RSQ2;
+            p2[o] = (p2[o] + t2) * RSQ2;
+            sdv[j + 1][G][o] += m * p1[o];
+            pcurv += m * gl[o] * p2[o];
+          }
+        }
+      }
+    }
+    if (plive) {
+#pragma unroll
+      for (int l = 0; l < 3; ++l)
+#pragma unroll
+        for (int G = 0; G < 2; ++G)
+#pragma unroll
+          for (int f = 0; f < 4; ++f) Lw[l * LCc::layer_n + LCc::sd + ((G * N + ii) * 3 + c3) * 4 + f] = sdv[l][G][f];
+    }
+    // x2: the second derivatives along x_{k,c} equal those along x_{i,c}
+    pcurv = T(2) * wave_sum(pcurv);
+    const T lpsi = logdet + wave_sum(jv + jve);
+    if (lane == 0) {
+      Lw[LCc::scal] = pcurv;
+      if (ka.logabs) ((T*)ka.logabs)[conf] = lpsi;
+      if (ka.phase) ((T*)ka.phase)[conf] = f_atan2(phi, phr);
+    }
+    return;
+  }
 
   AQ_PH(6);
   // ------------------------------------------------------------------ B3 pair adjoints d(logpsi)/d(x_i - x_k)

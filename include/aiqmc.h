@@ -119,6 +119,12 @@ int aiqmc_profile_read(aiqmc_ctx* ctx, int32_t slot, double* total_ms, int64_t* 
 int aiqmc_debug_logpsi_grad_forward(aiqmc_ctx* ctx, const void* pos, int32_t B, void* logabs, void* grad,
                                     void* stream);
 
+/* Diagnostics: aiqmc_local_energy through the single-launch forward-Laplacian
+ * kernel (second-order jets carried through the whole network).  The production
+ * path (adjoint pass + first-derivative pass) must agree with it to rounding. */
+int aiqmc_debug_local_energy_forward(aiqmc_ctx* ctx, const void* pos, int32_t B, void* e_l, void* logabs,
+                                     void* grad, void* stream);
+
 /* Diagnostics: aiqmc_mc_step evaluates each single-electron proposal from the
  * walker's cached electron stage and pair sums, recomputing only the moved
  * electron and its 2(N-1) pairs (default, on = 1).  on = 0 recomputes every

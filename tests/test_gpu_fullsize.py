@@ -144,3 +144,36 @@ def test_proposal_reuse_matches_recompute_f32_4096():
     # fp32 rounding may flip an acceptance whose ratio sits within ~1e-6 of its uniform
     differ = ((a - b).abs().reshape(4096, -1).amax(1) > 1e-4).float().mean()
     assert float(differ) < 2e-3, float(differ)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_local_energy_adjoint_vs_forward_laplacian_4096(dtype):
+    """Production local energy (adjoint pass + first-derivative pass) == the single-launch
+    forward-Laplacian kernel (second-order jets through the whole network) on every walker."""
+    s, ctx = _ctx("N2", dtype)
+    pos = torch.tensor(_walkers(s, 4096, seed=12), dtype=dtype, device="cuda")
+    e1, l1, g1 = ctx.local_energy(pos, want_logabs=True, want_grad=True)
+    e0, l0, g0 = ctx.local_energy_forward_mode(pos, want_logabs=True, want_grad=True)
+    torch.cuda.synchronize()
+    e1, e0 = e1.double().cpu().numpy(), e0.double().cpu().numpy()
+    rel = np.abs(e1 - e0) / (np.abs(e0) + 1.0)
+    scale = g0.abs().amax(dim=1, keepdim=True) + 1.0
+    if dtype == torch.float64:
+        assert rel.max() < 1e-8, rel.max()
+        assert torch.all((g1 - g0).abs() <= 1e-9 * scale)
+        assert torch.allclose(l1, l0, rtol=1e-10, atol=1e-10)
+    else:
+        assert np.median(rel) < 1e-5, np.median(rel)
+        assert np.mean(rel < 1e-3) > 0.99
+        assert torch.all((g1 - g0).abs() <= 2e-3 * scale)
+
+
+@pytest.mark.parametrize("name", ["H2", "Be", "C", "Ne", "C2"])
+def test_other_shapes_local_energy_adjoint_vs_forward(name):
+    s, ctx = _ctx(name, torch.float64)
+    pos = torch.tensor(_walkers(s, 256, seed=13), device="cuda")
+    e1, _, g1 = ctx.local_energy(pos, want_grad=True)
+    e0, _, g0 = ctx.local_energy_forward_mode(pos, want_grad=True)
+    torch.cuda.synchronize()
+    assert torch.allclose(e1, e0, rtol=1e-9, atol=1e-8), float((e1 - e0).abs().max())
+    assert torch.allclose(g1, g0, rtol=1e-8, atol=1e-8)
