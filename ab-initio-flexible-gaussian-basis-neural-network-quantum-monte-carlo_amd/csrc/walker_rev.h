@@ -151,16 +151,20 @@ __device__ __forceinline__ int xcd_major(int blk, int n) {
 }
 
 // Electron-local stage of the moved electron of proposals q = 16*block + s (lane = 16c + s).
+// The wave's 16 records are contiguous in the cache: they are assembled in LDS and written
+// with coalesced stores (direct per-lane stores scatter over 16 records x 4 lanes).
 template <typename T, int N, int A>
 __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
   using Ly = Lay<N, A>;
   using EC = ECache<N, A>;
   constexpr int D0 = 4 * A;
+  __shared__ T eb[16 * EC::size];
   const cptr<T> P = param_ptr<T>(ka.prm);
   const int lane = threadIdx.x;
   const int lc = lane >> 4, s = lane & 15;
-  const int q = xcd_major(blockIdx.x, gridDim.x) * 16 + s;
-  if (q >= ka.nconf) return;
+  const int blk = xcd_major(blockIdx.x, gridDim.x);
+  const int nrec = ka.nconf - blk * 16 < 16 ? ka.nconf - blk * 16 : 16;
+  const int q = blk * 16 + (s < nrec ? s : nrec - 1);
   const int b = q / N, i = q - b * N;
   const T tstep = (T)ka.tstep;
   const T te = (T)(*ka.taueff);
@@ -173,7 +177,7 @@ __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
   }
   ElecOut<T, A> eo;
   electron_stage<T, N, A>(P, xp, i, lc, eo);
-  T* E = (T*)ka.ecache + (size_t)q * EC::size;
+  T* E = eb + s * EC::size;
 #pragma unroll
   for (int col = 0; col < N; ++col) {
     PJ<T> sy = P[Ly::wy + col] * eo.yst[0];
@@ -190,6 +194,9 @@ __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
   }
   if (lc == 3) E[EC::jv] = eo.jae.v;
   else E[EC::jd + lc] = eo.jae.d1;
+  __syncthreads();
+  T* dst = (T*)ka.ecache + (size_t)blk * 16 * EC::size;
+  for (int idx = lane; idx < nrec * EC::size; idx += 64) dst[idx] = eb[idx];
 }
 
 // Occupancy hint per instantiation: fp32 N2 (14, 2) lands one VGPR above the
