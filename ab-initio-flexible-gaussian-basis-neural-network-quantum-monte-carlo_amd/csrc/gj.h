@@ -58,9 +58,11 @@ __device__ __forceinline__ unsigned key_bits(double x) {
   return (unsigned)(__builtin_bit_cast(unsigned long long, x) >> 32);
 }
 
+// rec (optional): the pivot sequence, recorded for gj_inverse_fixed: rec[k] = row of
+// step k, rec[N + k] = |pivot_k|^2, rec[2N] = permutation parity (written by lane 0).
 template <typename T, int N>
 __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, int lane, T& logdet, T& phr,
-                                           T& phi) {
+                                           T& phi, T* rec = nullptr) {
   constexpr int RW = (N + 3) / 4;
   const int c = lane & 15;
   const int rg = lane >> 4;
@@ -111,6 +113,10 @@ __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, in
     const T pr = rdlane(sr, 16 * g + k);
     const T pim = rdlane(si, 16 * g + k);
     const T den = pr * pr + pim * pim;
+    if (rec && lane == 0) {
+      rec[k] = T(p);
+      rec[N + k] = den;
+    }
     const T rden = f_rcp(den);
     ld += T(0.5) * f_log(den);                 // log|pivot|
     {
@@ -159,6 +165,7 @@ __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, in
       Bout[(myk[t] * N + myp) * 2 + 1] = ai[t];
     }
   }
+  if (rec && lane == 0) rec[2 * N] = T(inv & 1);
   if (inv & 1) {
     pr_ = -pr_;
     pi_ = -pi_;
@@ -166,6 +173,96 @@ __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, in
   logdet = ld;
   phr = pr_;
   phi = pi_;
+}
+
+// Gauss-Jordan with a prescribed pivot sequence (a Metropolis proposal reuses its
+// walker's partial-pivoting order, recorded by gj_inverse): rows are loaded permuted,
+// row slot k <- A row perm[k], so step k pivots on slot k (row group k / RW, register
+// k % RW), both compile-time: no pivot search, no runtime register selection, no
+// bookkeeping.  The result X = (PA)^{-1} gives B[i][perm[j]] = X[i][j]; det A =
+// sgn(perm) prod pivots.  bad = some |pivot_k|^2 < 1e-2 |walker pivot_k|^2 (the
+// order may not suit this matrix: the caller falls back to gj_inverse).
+// rec: the walker's record written by gj_inverse (LDS copy).
+template <typename T, int N>
+__device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bout, int lane, const T* rec,
+                                                 T& logdet, T& phr, T& phi, bool& bad) {
+  constexpr int RW = (N + 3) / 4;
+  const int c = lane & 15;
+  const int rg = lane >> 4;
+  const bool clive = c < N;
+  T ar[RW], ai[RW];
+#pragma unroll
+  for (int t = 0; t < RW; ++t) {
+    const int k = rg * RW + t;
+    T a = T(0), b = T(0);
+    if (k < N && clive) {
+      const int r = (int)rec[k];
+      const T y = Yv[r * N + c];
+      a = Ph[(r * N + c) * 2] * y;
+      b = Ph[(r * N + c) * 2 + 1] * y;
+    }
+    ar[t] = a;
+    ai[t] = b;
+  }
+  T ld = T(0), pr_ = T(1), pi_ = T(0);
+  bool small = false;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const int g = k / RW, ts = k % RW;
+    const T pr = rdlane(ar[ts], 16 * g + k);
+    const T pim = rdlane(ai[ts], 16 * g + k);
+    const T den = pr * pr + pim * pim;
+    small = small || (den < T(1e-2) * rec[N + k]);
+    const T rden = f_rcp(den);
+    ld += T(0.5) * f_log(den);
+    {
+      const T rm = f_sqrt(rden);
+      const T ur = pr * rm, ui = pim * rm;
+      const T nr = pr_ * ur - pi_ * ui, ni = pr_ * ui + pi_ * ur;
+      pr_ = nr;
+      pi_ = ni;
+    }
+    const T ir = pr * rden, ii = -pim * rden;   // 1 / pivot
+    const T q0r = __shfl(ar[ts], 16 * g + c), q0i = __shfl(ai[ts], 16 * g + c);
+    const bool ck = (c == k);
+    const T qr = ck ? ir : q0r * ir - q0i * ii;
+    const T qi = ck ? ii : q0r * ii + q0i * ir;
+    T mqr = -qr, mqi = -qi;
+    asm volatile("" : "+v"(mqr), "+v"(mqi));
+#pragma unroll
+    for (int t = 0; t < RW; ++t) {
+      const T fr = row_bcast(ar[t], k);
+      const T fi = row_bcast(ai[t], k);
+      T nr = ck ? T(0) : ar[t], ni = ck ? T(0) : ai[t];
+      nr = f_fma(fr, mqr, nr);
+      nr = f_fma(fi, qi, nr);
+      ni = f_fma(fr, mqi, ni);
+      ni = f_fma(fi, mqr, ni);
+      ar[t] = nr;
+      ai[t] = ni;
+    }
+    if (rg == g) {
+      ar[ts] = qr;
+      ai[ts] = qi;
+    }
+  }
+  const int pc = clive ? (int)rec[c] : 0;
+#pragma unroll
+  for (int t = 0; t < RW; ++t) {
+    const int i = rg * RW + t;
+    if (i < N && clive) {
+      Bout[(i * N + pc) * 2] = ar[t];
+      Bout[(i * N + pc) * 2 + 1] = ai[t];
+    }
+  }
+  if (rec[2 * N] != T(0)) {
+    pr_ = -pr_;
+    pi_ = -pi_;
+  }
+  logdet = ld;
+  phr = pr_;
+  phi = pi_;
+  bad = small;
 }
 
 }  // namespace aq

@@ -63,7 +63,8 @@ struct SmemRev {
   static constexpr int mx = R + N * N * 2;
   static constexpr int dbar = R;
   static constexpr int R_n = cmax(cmax(4 * N * N, 3 * N * N), 4 + 64 * 12);
-  static constexpr int end = R + R_n;
+  static constexpr int pv = R + R_n;             // [2N+1] the walker's pivot record (proposals)
+  static constexpr int end = pv + 2 * N + 2;
   static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
   static constexpr int hoff(int l) { return l == 0 ? 0 : N * D0 + (l - 1) * N * 4; }
 };
@@ -82,7 +83,8 @@ struct WCache {
   static constexpr int jaed = jaev + N;             // [48]       dJ_ae/dx per direction lane
   static constexpr int g2 = jaed + 48;              // [3][2][N][4]
   static constexpr int jee = g2 + 3 * 2 * N * 4;    // [1]        J_ee
-  static constexpr int pt = ((jee + 1 + 3) / 4) * 4; // [N][N][8]  tanh outputs t1, t2 of pair (k, i)
+  static constexpr int pv = jee + 1;                // [2N+1]     Gauss-Jordan pivot record (gj.h)
+  static constexpr int pt = ((pv + 2 * N + 1 + 3) / 4) * 4; // [N][N][8]  tanh outputs t1, t2 of pair (k, i)
   static constexpr int size = ((pt + 8 * N * N + 63) / 64) * 64;
 };
 // Per-proposal electron-local stage of the moved electron (k_moved_electron).
@@ -294,6 +296,7 @@ k_walker_rev(KArgs ka) {
     jv = (val && live) ? ((er == pi) ? Eq[EC::jv] : Wc[WC::jaev + er]) : T(0);
     jd1 = dir ? ((le == pi) ? Eq[EC::jd + lc] : Wc[WC::jaed + lane]) : T(0);
     jve = lane == 0 ? Wc[WC::jee] : T(0);
+    if (lane < 2 * N + 1) sm[SM::pv + lane] = Wc[WC::pv + lane];
 #pragma unroll
     for (int t = 0; t < NY; ++t)
       if (lane + 64 * t < N * N) Yv[lane + 64 * t] = ry[t];
@@ -571,7 +574,14 @@ k_walker_rev(KArgs ka) {
   }
   __syncthreads();
   T logdet, phr, phi;
-  gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi);   // Mx now holds B = A^{-1} [N][N][2]
+  if (reuse) {
+    // the walker's pivot order (partial pivoting rerun only if a pivot comes out small)
+    bool bad;
+    gj_inverse_fixed<T, N>(Ph, Yv, Mx, lane, sm + SM::pv, logdet, phr, phi, bad);
+    if (bad) gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi);
+  } else {
+    gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi, (!PREP && !ka.proposal) ? Wc + WC::pv : nullptr);
+  }
   __syncthreads();
 #define BRE(c, s) Mx[((c) * N + (s)) * 2]
 #define BIM(c, s) Mx[((c) * N + (s)) * 2 + 1]
