@@ -46,10 +46,10 @@ struct SmemRev {
   static constexpr int D0 = 4 * A;               // layer-0 h width
   static constexpr int DFM = 3 * D0 + 8;         // widest conv input (layer 0)
   static constexpr int QM = DFM / 4;
-  static constexpr int hl_n = N * D0 + 3 * N * 4;
+  static constexpr int hl_n = N * D0 + N * 4;     // h^0 and h^3 (h^1, h^2 stay in registers)
   static constexpr int cmax(int a, int b) { return a > b ? a : b; }
   static constexpr int xs = 0;                   // 48
-  static constexpr int hl = 48;                  // h^0 [N][D0], h^1..h^3 [N][4] (F1..F5)
+  static constexpr int hl = 48;                  // h^0 [N][D0], h^3 [N][4] (F1..F5)
   static constexpr int hbar = hl;                // their adjoints, same layout (B1..B4)
   static constexpr int cq = hl + hl_n;           // [3][N][QM]  conv outputs (kept for backward)
   static constexpr int sv = cq + 3 * N * QM;     // [3][N][4]   single outputs
@@ -66,7 +66,7 @@ struct SmemRev {
   static constexpr int pv = R + R_n;             // [2N+1] the walker's pivot record (proposals)
   static constexpr int end = pv + 2 * N + 2;
   static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
-  static constexpr int hoff(int l) { return l == 0 ? 0 : N * D0 + (l - 1) * N * 4; }
+  static constexpr int hoff(int l) { return l == 0 ? 0 : N * D0; }   // l = 0 or 3
 };
 
 // Per-walker cache written by the walker launch of a Metropolis sweep and read by
@@ -578,7 +578,12 @@ k_walker_rev(KArgs ka) {
     // the walker's pivot order (partial pivoting rerun only if a pivot comes out small)
     bool bad;
     gj_inverse_fixed<T, N>(Ph, Yv, Mx, lane, sm + SM::pv, logdet, phr, phi, bad);
-    if (bad) gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi);
+    if (bad) {
+#ifdef AQ_PHASE_PROF
+      if (lane == 0) atomicAdd(&aq_phase_cycles[15], 1ull);   // fallback count (diagnostics build)
+#endif
+      gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi);
+    }
   } else {
     gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi, (!PREP && !ka.proposal) ? Wc + WC::pv : nullptr);
   }

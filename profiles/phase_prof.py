@@ -49,6 +49,7 @@ def main():
             per = cyc[off:off + 10] / waves
             res[kind] = {PHASES[k]: round(float(per[k]), 1) for k in range(10)}
             res[kind]["total"] = round(float(per.sum()), 1)
+        res["gj_fallbacks_per_proposal"] = float(cyc[15]) / (B * s.nelectrons * sweeps)
         out["reuse" if reuse else "recompute"] = res
     ctx.set_proposal_reuse(True)
     print(json.dumps(out, indent=1))
