@@ -187,10 +187,12 @@ template <typename T, int N>
 __device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bout, int lane, const T* rec,
                                                  T& logdet, T& phr, T& phi, bool& bad) {
   constexpr int RW = (N + 3) / 4;
+  constexpr bool PK = sizeof(T) == 4;   // fp32: complex entries as packed pairs (v_pk_fma_f32)
+  using V2 = typename Pair<T>::type;
   const int c = lane & 15;
   const int rg = lane >> 4;
   const bool clive = c < N;
-  T ar[RW], ai[RW];
+  V2 a2[RW];
 #pragma unroll
   for (int t = 0; t < RW; ++t) {
     const int k = rg * RW + t;
@@ -201,16 +203,15 @@ __device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bo
       a = Ph[(r * N + c) * 2] * y;
       b = Ph[(r * N + c) * 2 + 1] * y;
     }
-    ar[t] = a;
-    ai[t] = b;
+    a2[t] = pair_make<T>(a, b);
   }
   T ld = T(0), pr_ = T(1), pi_ = T(0);
   bool small = false;
 #pragma unroll
   for (int k = 0; k < N; ++k) {
     const int g = k / RW, ts = k % RW;
-    const T pr = rdlane(ar[ts], 16 * g + k);
-    const T pim = rdlane(ai[ts], 16 * g + k);
+    const T pr = rdlane(pair_re<T>(a2[ts]), 16 * g + k);
+    const T pim = rdlane(pair_im<T>(a2[ts]), 16 * g + k);
     const T den = pr * pr + pim * pim;
     small = small || (den < T(1e-2) * rec[N + k]);
     const T rden = f_rcp(den);
@@ -223,36 +224,32 @@ __device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bo
       pi_ = ni;
     }
     const T ir = pr * rden, ii = -pim * rden;   // 1 / pivot
-    const T q0r = __shfl(ar[ts], 16 * g + c), q0i = __shfl(ai[ts], 16 * g + c);
+    const T q0r = __shfl(pair_re<T>(a2[ts]), 16 * g + c), q0i = __shfl(pair_im<T>(a2[ts]), 16 * g + c);
     const bool ck = (c == k);
     const T qr = ck ? ir : q0r * ir - q0i * ii;
     const T qi = ck ? ii : q0r * ii + q0i * ir;
-    T mqr = -qr, mqi = -qi;
-    asm volatile("" : "+v"(mqr), "+v"(mqi));
+    // a[r][c] <- keep * a[r][c] - a[r][k] q[c]:  [re, im] += fr [-qr, -qi] + fi [qi, -qr]
+    const V2 m1 = pair_make<T>(-qr, -qi), m2 = pair_make<T>(qi, -qr);
+    const T keep = ck ? T(0) : T(1);
 #pragma unroll
     for (int t = 0; t < RW; ++t) {
-      const T fr = row_bcast(ar[t], k);
-      const T fi = row_bcast(ai[t], k);
-      T nr = ck ? T(0) : ar[t], ni = ck ? T(0) : ai[t];
-      nr = f_fma(fr, mqr, nr);
-      nr = f_fma(fi, qi, nr);
-      ni = f_fma(fr, mqi, ni);
-      ni = f_fma(fi, mqr, ni);
-      ar[t] = nr;
-      ai[t] = ni;
+      const T fr = row_bcast(pair_re<T>(a2[t]), k);
+      const T fi = row_bcast(pair_im<T>(a2[t]), k);
+      V2 n = pair_scale<T>(a2[t], keep);
+      n = pair_fma<T>(fr, m1, n);
+      n = pair_fma<T>(fi, m2, n);
+      a2[t] = n;
     }
-    if (rg == g) {
-      ar[ts] = qr;
-      ai[ts] = qi;
-    }
+    if (rg == g) a2[ts] = pair_make<T>(qr, qi);
   }
+  (void)PK;
   const int pc = clive ? (int)rec[c] : 0;
 #pragma unroll
   for (int t = 0; t < RW; ++t) {
     const int i = rg * RW + t;
     if (i < N && clive) {
-      Bout[(i * N + pc) * 2] = ar[t];
-      Bout[(i * N + pc) * 2 + 1] = ai[t];
+      Bout[(i * N + pc) * 2] = pair_re<T>(a2[t]);
+      Bout[(i * N + pc) * 2 + 1] = pair_im<T>(a2[t]);
     }
   }
   if (rec[2 * N] != T(0)) {

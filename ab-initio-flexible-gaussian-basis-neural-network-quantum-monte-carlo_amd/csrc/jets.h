@@ -188,6 +188,35 @@ template <typename T> __device__ __forceinline__ T wave_sum(T x) {
 }
 
 // ---------------------------------------------------------------------------
+// Pair<T>: two values in adjacent registers.  fp32 uses a 2-vector so that the
+// backend issues packed VOP3P math (v_pk_fma_f32 / v_pk_mul_f32: two FMAs per
+// instruction, op_sel broadcasting a scalar operand); fp64 has no packed math.
+// ---------------------------------------------------------------------------
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+struct D2 { double x, y; };
+template <typename T> struct Pair;
+template <> struct Pair<float> { using type = f32x2; };
+template <> struct Pair<double> { using type = D2; };
+template <typename T> __device__ __forceinline__ typename Pair<T>::type pair_make(T a, T b);
+template <> __device__ __forceinline__ f32x2 pair_make<float>(float a, float b) { return f32x2{a, b}; }
+template <> __device__ __forceinline__ D2 pair_make<double>(double a, double b) { return D2{a, b}; }
+template <typename T> __device__ __forceinline__ T pair_re(typename Pair<T>::type v) { return v.x; }
+template <typename T> __device__ __forceinline__ T pair_im(typename Pair<T>::type v) { return v.y; }
+// s * v
+template <typename T> __device__ __forceinline__ typename Pair<T>::type pair_scale(typename Pair<T>::type v, T s);
+template <> __device__ __forceinline__ f32x2 pair_scale<float>(f32x2 v, float s) { return v * f32x2{s, s}; }
+template <> __device__ __forceinline__ D2 pair_scale<double>(D2 v, double s) { return D2{v.x * s, v.y * s}; }
+// s * v + w
+template <typename T>
+__device__ __forceinline__ typename Pair<T>::type pair_fma(T s, typename Pair<T>::type v, typename Pair<T>::type w);
+template <> __device__ __forceinline__ f32x2 pair_fma<float>(float s, f32x2 v, f32x2 w) {
+  return __builtin_elementwise_fma(f32x2{s, s}, v, w);
+}
+template <> __device__ __forceinline__ D2 pair_fma<double>(double s, D2 v, D2 w) {
+  return D2{__builtin_fma(s, v.x, w.x), __builtin_fma(s, v.y, w.y)};
+}
+
+// ---------------------------------------------------------------------------
 // DJ: wave-shared jet (direction lanes: derivatives, value row: value in d1)
 // ---------------------------------------------------------------------------
 template <typename T> struct DJ { T d1, d2; };
