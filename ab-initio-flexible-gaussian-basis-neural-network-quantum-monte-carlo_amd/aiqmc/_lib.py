@@ -30,11 +30,14 @@ EXPORTED_SYMBOLS = (
     "aiqmc_workspace_bytes", "aiqmc_last_error", "aiqmc_supported_shapes",
     "aiqmc_profile_enable", "aiqmc_profile_read", "aiqmc_debug_logpsi_grad_forward",
     "aiqmc_debug_set_proposal_reuse", "aiqmc_debug_phase_cycles", "aiqmc_debug_local_energy_forward",
+    "aiqmc_set_ecp", "aiqmc_local_energy_ecp",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
 PROF_MC_WALKER = 1     # walker gradient launches of aiqmc_mc_step
 PROF_LOCAL_ENERGY = 2  # aiqmc_local_energy launches
+PROF_ECP_QUAD = 3      # value-only launches over the ECP quadrature configurations
+ECP_NQ = 50            # quadrature points per (electron, atom) (pseudopotential.py:181-225)
 
 
 class AiqmcCfg(ctypes.Structure):
@@ -54,6 +57,20 @@ class AiqmcCfg(ctypes.Structure):
         ("n_antiparallel", ctypes.c_int32),
         ("hidden_dims", (ctypes.c_int32 * 2) * 3),
         ("hidden_dims_ynlm", ctypes.c_int32 * 3),
+    ]
+
+
+class AiqmcEcp(ctypes.Structure):
+    _fields_ = [
+        ("list_l", ctypes.c_int32),
+        ("n_local", ctypes.c_int32),
+        ("n_nonlocal", ctypes.c_int32),
+        ("rn_local", ctypes.POINTER(ctypes.c_double)),
+        ("local_coes", ctypes.POINTER(ctypes.c_double)),
+        ("local_exps", ctypes.POINTER(ctypes.c_double)),
+        ("rn_non_local", ctypes.POINTER(ctypes.c_double)),
+        ("non_local_coes", ctypes.POINTER(ctypes.c_double)),
+        ("non_local_exps", ctypes.POINTER(ctypes.c_double)),
     ]
 
 
@@ -91,13 +108,16 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_debug_set_proposal_reuse.restype = ctypes.c_int
     lib.aiqmc_debug_phase_cycles.argtypes = [vp, vp]
     lib.aiqmc_debug_phase_cycles.restype = ctypes.c_int
+    lib.aiqmc_set_ecp.argtypes = [vp, ctypes.POINTER(AiqmcEcp)]
+    lib.aiqmc_local_energy_ecp.argtypes = [vp, vp, i32, i32, vp, ctypes.c_uint64, ctypes.c_uint64, vp, vp, vp,
+                                           vp, vp]
     lib.aiqmc_profile_enable.argtypes = [vp, i32]
     lib.aiqmc_profile_read.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64)]
     lib.aiqmc_last_error.restype = ctypes.c_char_p
     lib.aiqmc_supported_shapes.restype = ctypes.c_char_p
     for name in ("aiqmc_create", "aiqmc_destroy", "aiqmc_set_params", "aiqmc_logpsi",
                  "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_mc_step", "aiqmc_profile_enable",
-                 "aiqmc_profile_read"):
+                 "aiqmc_profile_read", "aiqmc_set_ecp", "aiqmc_local_energy_ecp"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib
@@ -278,6 +298,53 @@ class Context:
         check(self._lib.aiqmc_debug_local_energy_forward(self._h, _ptr(p), B, _ptr(el), _ptr(logabs), _ptr(grad),
                                                          _stream(self.device)), "aiqmc_debug_local_energy_forward")
         return el, logabs, grad
+
+    def set_ecp(self, rn_local, local_coes, local_exps, rn_non_local, non_local_coes, non_local_exps,
+                list_l: int):
+        """Pseudopotential tables in the reference drivers' shapes (single_atom_C.py:13-23):
+        rn_local/local_coes/local_exps [A][KL], rn_non_local/... [A][list_l+1][KN]."""
+        A = self.A
+        loc = [np.ascontiguousarray(np.asarray(a, np.float64).reshape(A, -1)) for a in
+               (rn_local, local_coes, local_exps)]
+        nl = [np.ascontiguousarray(np.asarray(a, np.float64).reshape(A, int(list_l) + 1, -1)) for a in
+              (rn_non_local, non_local_coes, non_local_exps)]
+        if len({a.shape for a in loc}) != 1 or len({a.shape for a in nl}) != 1:
+            raise ValueError("ECP tables of one kind must share their shape")
+        self._ecp_keep = loc + nl
+        e = AiqmcEcp()
+        e.list_l = int(list_l)
+        e.n_local = loc[0].shape[1]
+        e.n_nonlocal = nl[0].shape[2]
+        dp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+        e.rn_local, e.local_coes, e.local_exps = (dp(a) for a in loc)
+        e.rn_non_local, e.non_local_coes, e.non_local_exps = (dp(a) for a in nl)
+        with torch.cuda.device(self.device):
+            check(self._lib.aiqmc_set_ecp(self._h, ctypes.byref(e)), "aiqmc_set_ecp")
+
+    def local_energy_ecp(self, pos: torch.Tensor, rot: Optional[torch.Tensor] = None, seed: int = 0,
+                         offset: int = 0, want_quadrature: bool = False):
+        """Complex pseudopotential local energy [B] (pphamiltonian.py:177-188).  rot [B,3,3]:
+        injected rotations (parity mode); None: Philox Haar draws from (seed, offset)."""
+        p = self._pos(pos)
+        B = p.shape[0]
+        er = torch.empty(B, dtype=self.dtype, device=self.device)
+        ei = torch.empty(B, dtype=self.dtype, device=self.device)
+        r = None
+        if rot is not None:
+            r = rot.to(self.device, self.dtype).contiguous()
+            if r.numel() != 9 * B:
+                raise ValueError("rot must be [B,3,3]")
+        nq = B * self.N * self.A * ECP_NQ
+        lq = torch.empty(nq, dtype=self.dtype, device=self.device) if want_quadrature else None
+        pq = torch.empty(nq, dtype=self.dtype, device=self.device) if want_quadrature else None
+        check(self._lib.aiqmc_local_energy_ecp(self._h, _ptr(p), B, AIQMC_RNG_HOST if r is not None else
+                                               AIQMC_RNG_PHILOX, _ptr(r), ctypes.c_uint64(seed),
+                                               ctypes.c_uint64(offset), _ptr(er), _ptr(ei), _ptr(lq), _ptr(pq),
+                                               _stream(self.device)), "aiqmc_local_energy_ecp")
+        e = torch.complex(er, ei)
+        if want_quadrature:
+            return e, lq.reshape(B, self.N, self.A, ECP_NQ), pq.reshape(B, self.N, self.A, ECP_NQ)
+        return e
 
     def mc_step(self, pos: torch.Tensor, nsteps: int, tstep: float, gauss1=None, gauss2=None, u=None,
                 seed: int = 0, offset: int = 0, count_accepts: bool = False):

@@ -16,6 +16,7 @@
 
 #include "aiqmc.h"
 #include "ctx.h"
+#include "ecp.h"
 
 using namespace aq;
 
@@ -159,6 +160,48 @@ static int ensure_ws(aiqmc_ctx* c, int B) {
   return 0;
 }
 
+// per-proposal walker-cache scratch for the reuse-off diagnostics path (n configurations)
+static int ensure_wcp(aiqmc_ctx* c, int64_t n, const ShapeOps& ops) {
+  if (c->wcp_n >= n) return 0;
+  if (c->d_wcp) (void)hipFree(c->d_wcp);
+  c->d_wcp = nullptr;
+  c->wcp_n = 0;
+  HIPCHK(hipMalloc(&c->d_wcp, (size_t)n * ops.wcache_n * (c->dtype == AIQMC_F32 ? 4 : 8)));
+  c->wcp_n = n;
+  return 0;
+}
+
+static void free_ecp_ws(aiqmc_ctx* c) {
+  void* ps[] = {c->d_ecp_rot, c->d_ecp_x, c->d_ecp_lq, c->d_ecp_pq, c->d_ecp_ec, c->d_ecp_el, c->d_ecp_lp0,
+                c->d_ecp_ph0};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+  c->d_ecp_rot = c->d_ecp_x = c->d_ecp_lq = c->d_ecp_pq = c->d_ecp_ec = nullptr;
+  c->d_ecp_el = c->d_ecp_lp0 = c->d_ecp_ph0 = nullptr;
+  c->ecp_B = 0;
+  c->ecp_bytes = 0;
+}
+
+// ECP workspace for B walkers: B*N*A*50 quadrature configurations
+static int ensure_ecp_ws(aiqmc_ctx* c, int B, const ShapeOps& ops) {
+  if (c->ecp_B >= B) return 0;
+  free_ecp_ws(c);
+  const size_t s = c->dtype == AIQMC_F32 ? 4 : 8;
+  const size_t nq = (size_t)B * c->N * c->A * ECP_NQ;
+  size_t bytes[8] = {(size_t)B * 9 * s, nq * 3 * s, nq * s, nq * s, nq * (size_t)ops.ecache_n * s,
+                     (size_t)B * s, (size_t)B * s, (size_t)B * s};
+  void** ptrs[8] = {&c->d_ecp_rot, &c->d_ecp_x, &c->d_ecp_lq, &c->d_ecp_pq, &c->d_ecp_ec, &c->d_ecp_el,
+                    &c->d_ecp_lp0, &c->d_ecp_ph0};
+  int64_t tot = 0;
+  for (int k = 0; k < 8; ++k) {
+    HIPCHK(hipMalloc(ptrs[k], bytes[k]));
+    tot += (int64_t)bytes[k];
+  }
+  c->ecp_B = B;
+  c->ecp_bytes = tot;
+  return 0;
+}
+
 // ============================================================================ C-ABI
 
 extern "C" {
@@ -248,6 +291,8 @@ int aiqmc_destroy(aiqmc_ctx* c) {
   if (!c) return AIQMC_OK;
   (void)hipSetDevice(c->device);
   free_ws(c);
+  free_ecp_ws(c);
+  if (c->d_ecp_tab) (void)hipFree(c->d_ecp_tab);
   if (c->d_wcp) (void)hipFree(c->d_wcp);
   if (c->d_lc) (void)hipFree(c->d_lc);
   for (auto& v : c->ev_used)
@@ -264,7 +309,7 @@ int aiqmc_destroy(aiqmc_ctx* c) {
 
 int64_t aiqmc_param_count(const aiqmc_ctx* c) { return c ? c->ncanon : -1; }
 int64_t aiqmc_workspace_bytes(const aiqmc_ctx* c) {
-  return c ? c->ws_bytes + (int64_t)c->lc_B * c->lc_n * (c->dtype == AIQMC_F32 ? 4 : 8) : -1;
+  return c ? c->ws_bytes + c->ecp_bytes + (int64_t)c->lc_B * c->lc_n * (c->dtype == AIQMC_F32 ? 4 : 8) : -1;
 }
 
 int aiqmc_set_params(aiqmc_ctx* c, const double* flat, int64_t n, void* stream) {
@@ -414,12 +459,9 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
   if (rc) return rc;
   ShapeOps ops;
   shape_ops(c->N, c->A, &ops);
-  if (!c->reuse && c->wcp_B < B) {
-    if (c->d_wcp) (void)hipFree(c->d_wcp);
-    c->d_wcp = nullptr;
-    c->wcp_B = 0;
-    HIPCHK(hipMalloc(&c->d_wcp, (size_t)B * c->N * ops.wcache_n * (c->dtype == AIQMC_F32 ? 4 : 8)));
-    c->wcp_B = B;
+  if (!c->reuse) {
+    rc = ensure_wcp(c, (int64_t)B * c->N, ops);
+    if (rc) return rc;
   }
   hipStream_t s = (hipStream_t)stream;
   const int N = c->N;
@@ -493,6 +535,138 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
     ops.accept(c->dtype, pos, c->d_grad, c->d_gown, c->d_lp, c->d_lpn, g1, g2, uu, c->d_taueff, B, tstep,
                accept_out, s);
   }
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_set_ecp(aiqmc_ctx* c, const aiqmc_ecp* e) {
+  if (!c || !e) return fail(AIQMC_EINVAL, "null argument");
+  if (e->list_l < 0 || e->list_l > 3) return fail(AIQMC_EUNSUPPORTED, "list_l must be in [0,3] (P_l, pseudopotential.py:250-269)");
+  if (e->n_local < 0 || e->n_nonlocal < 0) return fail(AIQMC_EINVAL, "negative table size");
+  if ((e->n_local && (!e->rn_local || !e->local_coes || !e->local_exps)) ||
+      (e->n_nonlocal && (!e->rn_non_local || !e->non_local_coes || !e->non_local_exps)))
+    return fail(AIQMC_EINVAL, "null ECP table");
+  const int A = c->A, KL = e->n_local, KN = e->n_nonlocal, L = e->list_l + 1;
+  // device table: atoms [A][3], charges [A], then per atom KL local and L*KN nonlocal (n, c, alpha)
+  std::vector<double> tab(4 * A + (size_t)A * 3 * (KL + L * KN));
+  for (int a = 0; a < A; ++a) {
+    for (int d = 0; d < 3; ++d) tab[a * 3 + d] = c->atoms[a * 3 + d];
+    tab[3 * A + a] = c->charges[a];
+    double* t = tab.data() + 4 * A + (size_t)a * 3 * (KL + L * KN);
+    for (int k = 0; k < KL; ++k) {
+      t[3 * k] = e->rn_local[a * KL + k];
+      t[3 * k + 1] = e->local_coes[a * KL + k];
+      t[3 * k + 2] = e->local_exps[a * KL + k];
+    }
+    t += 3 * KL;
+    for (int k = 0; k < L * KN; ++k) {
+      t[3 * k] = e->rn_non_local[(size_t)a * L * KN + k];
+      t[3 * k + 1] = e->non_local_coes[(size_t)a * L * KN + k];
+      t[3 * k + 2] = e->non_local_exps[(size_t)a * L * KN + k];
+    }
+  }
+  HIPCHK(hipSetDevice(c->device));
+  if (c->d_ecp_tab) (void)hipFree(c->d_ecp_tab);
+  c->d_ecp_tab = nullptr;
+  c->ecp_set = false;
+  HIPCHK(hipMalloc((void**)&c->d_ecp_tab, tab.size() * sizeof(double)));
+  HIPCHK(hipMemcpy(c->d_ecp_tab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice));
+  c->ecp_KL = KL;
+  c->ecp_KN = KN;
+  c->ecp_L = L;
+  c->ecp_set = true;
+  return AIQMC_OK;
+}
+
+int aiqmc_local_energy_ecp(aiqmc_ctx* c, const void* pos, int32_t B, int32_t rng_mode, const void* rot,
+                           uint64_t seed, uint64_t offset, void* e_re, void* e_im, void* logabs_q, void* phase_q,
+                           void* stream) {
+  int rc = check_call(c, pos, B);
+  if (rc) return rc;
+  if (!c->ecp_set) return fail(AIQMC_ESTATE, "aiqmc_set_ecp has not been called");
+  if (!e_re || !e_im) return fail(AIQMC_EINVAL, "null e_re / e_im");
+  if (rng_mode == AIQMC_RNG_HOST && !rot) return fail(AIQMC_EINVAL, "AIQMC_RNG_HOST needs rot");
+  if (rng_mode != AIQMC_RNG_HOST && rng_mode != AIQMC_RNG_PHILOX) return fail(AIQMC_EINVAL, "rng_mode");
+  if (B == 0) return AIQMC_OK;
+  const int64_t M = (int64_t)c->N * c->A * ECP_NQ;
+  if ((int64_t)B * M > INT32_MAX) return fail(AIQMC_EINVAL, "too many quadrature configurations for one call");
+  HIPCHK(hipSetDevice(c->device));
+  ShapeOps ops;
+  shape_ops(c->N, c->A, &ops);
+  rc = ensure_ws(c, B);
+  if (rc) return rc;
+  rc = ensure_ecp_ws(c, B, ops);
+  if (rc) return rc;
+  if (!c->reuse) {
+    rc = ensure_wcp(c, (int64_t)B * M, ops);
+    if (rc) return rc;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int nq = (int)(B * M);
+  void* lq = logabs_q ? logabs_q : c->d_ecp_lq;
+  void* pq = phase_q ? phase_q : c->d_ecp_pq;
+  // (1) all-electron local energy V + KE (walker_lap.h)
+  rc = aiqmc_local_energy(c, pos, B, c->d_ecp_el, nullptr, nullptr, stream);
+  if (rc) return rc;
+  // (2) rotations, quadrature positions
+  EcpArgs ea;
+  std::memset(&ea, 0, sizeof(ea));
+  ea.B = B;
+  ea.N = c->N;
+  ea.A = c->A;
+  ea.KL = c->ecp_KL;
+  ea.KN = c->ecp_KN;
+  ea.L = c->ecp_L;
+  ea.tab = c->d_ecp_tab;
+  ea.pos = pos;
+  ea.rot = rng_mode == AIQMC_RNG_HOST ? rot : c->d_ecp_rot;
+  ea.lp0 = c->d_ecp_lp0;
+  ea.ph0 = c->d_ecp_ph0;
+  ea.lpq = lq;
+  ea.phq = pq;
+  ea.eall = c->d_ecp_el;
+  ea.e_re = e_re;
+  ea.e_im = e_im;
+  ea.xnew = c->d_ecp_x;
+  ea.seed = seed;
+  ea.step = offset;
+  const bool f32 = c->dtype == AIQMC_F32;
+  if (rng_mode == AIQMC_RNG_PHILOX) {
+    if (f32) k_ecp_rot<float><<<dim3((B + 255) / 256), dim3(256), 0, s>>>(ea);
+    else k_ecp_rot<double><<<dim3((B + 255) / 256), dim3(256), 0, s>>>(ea);
+  }
+  if (f32) k_ecp_points<float><<<dim3((nq + 255) / 256), dim3(256), 0, s>>>(ea);
+  else k_ecp_points<double><<<dim3((nq + 255) / 256), dim3(256), 0, s>>>(ea);
+  // (3) walker launch: log psi at the walkers + the walker cache
+  KArgs ka = base_args(c);
+  ka.nconf = B;
+  ka.pos = pos;
+  ka.logabs = c->d_ecp_lp0;
+  ka.phase = c->d_ecp_ph0;
+  ka.wcache = c->d_wc;
+  ops.walker(c->dtype, MODE_GRAD, ka, B, s);
+  // (4) quadrature configurations: one moved electron each, value only
+  KArgs kp = base_args(c);
+  kp.nconf = nq;
+  kp.pos = pos;
+  kp.proposal = 1;
+  kp.mper = (int)M;
+  kp.mdiv = c->A * ECP_NQ;
+  kp.xnew = c->d_ecp_x;
+  kp.value_only = 1;
+  kp.logabs = lq;
+  kp.phase = pq;
+  if (c->reuse) {
+    kp.wcache = c->d_wc;
+    kp.ecache = c->d_ecp_ec;
+    ops.moved(c->dtype, kp, s);
+  } else {
+    kp.wcache = c->d_wcp;
+  }
+  timed(c, 3, s, [&] { ops.walker(c->dtype, MODE_GRAD, kp, nq, s); });
+  // (5) local pp part + nonlocal quadrature sum
+  if (f32) k_ecp_energy<float><<<dim3(B), dim3(64), 0, s>>>(ea);
+  else k_ecp_energy<double><<<dim3(B), dim3(64), 0, s>>>(ea);
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
 }

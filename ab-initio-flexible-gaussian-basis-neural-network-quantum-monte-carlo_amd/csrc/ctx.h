@@ -16,7 +16,7 @@
 int aiqmc_fail(int code, const std::string& msg);
 using aq::KArgs;
 #include <utility>
-#define AIQMC_PROF_SLOTS 3
+#define AIQMC_PROF_SLOTS 4
 
 struct aiqmc_ctx {
   int N = 0, A = 0, nup = 0, ndn = 0, dtype = 0, device = 0;
@@ -33,12 +33,20 @@ struct aiqmc_ctx {
   void *d_g1 = nullptr, *d_g2 = nullptr, *d_u = nullptr;   // per-sweep Philox draws
   void *d_wc = nullptr, *d_ec = nullptr;                    // Metropolis caches (walker_rev.h WCache/ECache)
   void* d_wcp = nullptr;                                    // per-proposal cache scratch (reuse off)
-  int wcp_B = 0;
+  int64_t wcp_n = 0;                                        // its capacity in configurations
   void* d_lc = nullptr;                                     // local-energy LapCache [B][lcache_n]
   int lc_B = 0, lc_n = 0;
   bool reuse = true;                                        // proposals reuse the walker's cached stage
   double* d_taueff = nullptr;
   int64_t ws_bytes = 0;
+  // pseudopotential (aiqmc_set_ecp / aiqmc_local_energy_ecp, ecp.h)
+  bool ecp_set = false;
+  int ecp_KL = 0, ecp_KN = 0, ecp_L = 0;
+  double* d_ecp_tab = nullptr;
+  int ecp_B = 0;
+  void *d_ecp_rot = nullptr, *d_ecp_x = nullptr, *d_ecp_lq = nullptr, *d_ecp_pq = nullptr, *d_ecp_ec = nullptr,
+       *d_ecp_el = nullptr, *d_ecp_lp0 = nullptr, *d_ecp_ph0 = nullptr;
+  int64_t ecp_bytes = 0;
   // optional per-kernel HIP-event timing (aiqmc_profile_*): slot -> recorded (start, stop) pairs
   bool prof = false;
   std::vector<hipEvent_t> ev_free;

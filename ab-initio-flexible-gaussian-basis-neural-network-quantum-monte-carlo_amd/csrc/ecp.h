@@ -1,0 +1,240 @@
+// ecp.h -- pseudopotential (ccECP) local energy of the AIQMC wavefunction
+// (AIQMCrelease3/Energy/pphamiltonian.py:130-190, pseudopotential/pseudopotential.py:86-318,
+// pseudopotential/pp_energy_test.py:45-105).
+//
+// Per walker b the nonlocal part needs log psi at N*A*50 configurations: electron i moved to
+// r_ia * (p_q R_b), p_q the 50-point octahedral grid (pseudopotential.py:181-225), R_b the
+// walker's random orthogonal matrix (get_rot :233-241).  Each of them differs from the walker
+// in ONE electron, so they run through the Metropolis proposal machinery (walker_rev.h): the
+// walker launch writes the walker cache, k_moved_electron the moved electron's stage, and a
+// value-only proposal launch of k_walker_rev patches the pair sums and reuses the walker's
+// Gauss-Jordan pivot order.  Kernels here:
+//   k_ecp_rot     Haar O(3) matrix per walker from Philox (production draws)
+//   k_ecp_points  moved-electron positions x' = r_ia p_q R_b, one thread per configuration
+//   k_ecp_energy  one wave per walker: local pp part, sum_{i,a,q} P_l(cos) v_l(r) ratio,
+//                 added to the all-electron local energy of the same walker
+// Reference quirks (oracle/pphamiltonian.py E1-E7) are reproduced; the ECP arithmetic itself is
+// done in double for both dtypes (it is < 1% of the launch time).
+#pragma once
+#include "jets.h"
+
+namespace aq {
+
+constexpr int ECP_NQ = 50;   // 6 (OA) + 12 (OB) + 8 (OC) + 24 (OD) points
+
+// Grid points in the reference's order and its 8-digit literals (pseudopotential.py:197-223).
+__device__ __forceinline__ void ecp_point(int q, double p[3], int& grp) {
+  const double s2 = 0.70710678, s3 = 0.57735027;
+  if (q < 6) {
+    grp = 0;
+    const int ax[6] = {0, 1, 2, 2, 1, 0};
+    const double sg[6] = {-1.0, -1.0, -1.0, 1.0, 1.0, 1.0};
+    p[0] = p[1] = p[2] = 0.0;
+    p[ax[q]] = sg[q];
+    return;
+  }
+  if (q < 18) {
+    grp = 1;
+    // OB rows: (-,-,0) (-,0,-) (-,0,+) (-,+,0) (0,-,-) (0,-,+) (0,+,-) (0,+,+) (+,-,0) (+,0,-) (+,0,+) (+,+,0)
+    const signed char t[12][3] = {{-1, -1, 0}, {-1, 0, -1}, {-1, 0, 1}, {-1, 1, 0}, {0, -1, -1}, {0, -1, 1},
+                                  {0, 1, -1},  {0, 1, 1},   {1, -1, 0}, {1, 0, -1}, {1, 0, 1},  {1, 1, 0}};
+    for (int d = 0; d < 3; ++d) p[d] = t[q - 6][d] * s2;
+    return;
+  }
+  // OC rows in binary order of (x, y, z) signs, - before +
+  const int c = q < 26 ? q - 18 : (q - 26) % 8;
+  double o[3] = {(c & 4) ? s3 : -s3, (c & 2) ? s3 : -s3, (c & 1) ? s3 : -s3};
+  if (q < 26) {
+    grp = 2;
+    for (int d = 0; d < 3; ++d) p[d] = o[d];
+    return;
+  }
+  // OD = [OD1; OD2; OD3], d1 = OC sqrt(3/11), component 2 / 1 / 0 tripled (:219-223)
+  grp = 3;
+  const double f = sqrt(3.0 / 11.0);
+  const int tri = 2 - (q - 26) / 8;
+  for (int d = 0; d < 3; ++d) p[d] = (o[d] * f) * (d == tri ? 3.0 : 1.0);
+}
+
+__device__ __forceinline__ int ecp_group_begin(int g) { return g == 0 ? 0 : (g == 1 ? 6 : (g == 2 ? 18 : 26)); }
+__device__ __forceinline__ int ecp_group_end(int g) { return g == 0 ? 6 : (g == 1 ? 18 : (g == 2 ? 26 : 50)); }
+__device__ __forceinline__ double ecp_weight(int g) {
+  return g == 0 ? 4.0 / 315.0 : (g == 1 ? 64.0 / 2835.0 : (g == 2 ? 27.0 / 1280.0 : 14641.0 / 725760.0));
+}
+
+// p' = p R  (einsum 'jkl,ik->jil', pseudopotential.py:237-240), R row-major [k][l]
+template <typename T>
+__device__ __forceinline__ void ecp_rotate(const T* R, const double p[3], double out[3]) {
+#pragma unroll
+  for (int l = 0; l < 3; ++l) out[l] = p[0] * (double)R[l] + p[1] * (double)R[3 + l] + p[2] * (double)R[6 + l];
+}
+
+// Device tables (double): atoms [A][3], charges [A], then per atom KL local triplets
+// (n, coefficient, exponent) and L*KN nonlocal triplets.
+struct EcpArgs {
+  int B, N, A, KL, KN, L;
+  const double* tab;
+  const void* pos;      // [B][3N]
+  const void* rot;      // [B][9]
+  const void* lp0;      // [B] log|psi| at the walker
+  const void* ph0;      // [B] phase at the walker
+  const void* lpq;      // [B][N][A][50] log|psi| at the quadrature configurations
+  const void* phq;      // [B][N][A][50] phase
+  const void* eall;     // [B] all-electron local energy (V_ee + V_en + V_nn + KE)
+  void* e_re;           // [B] outputs
+  void* e_im;
+  void* xnew;           // k_ecp_points output [B*N*A*50][3]
+  uint64_t seed, step;  // k_ecp_rot
+};
+
+// Uniform Haar O(3): a uniformly random unit quaternion (4 normals, normalised) gives SO(3);
+// an independent fair sign makes it O(3), the support of jax.random.orthogonal.
+template <typename T>
+__global__ __launch_bounds__(256) void k_ecp_rot(EcpArgs ea) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= ea.B) return;
+  float g[3], h[3], u[4];
+  philox_normal3f(ea.seed, ea.step, (uint32_t)b, 16u, g);
+  philox_normal3f(ea.seed, ea.step, (uint32_t)b, 17u, h);
+  philox_u4(ea.seed, ea.step, (uint32_t)b, 18u, u);
+  double w = g[0], x = g[1], y = g[2], z = h[0];
+  const double n = 1.0 / sqrt(w * w + x * x + y * y + z * z);
+  w *= n; x *= n; y *= n; z *= n;
+  const double s = u[0] < 0.5f ? -1.0 : 1.0;
+  const double m[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - z * w),     2 * (x * z + y * w),
+                       2 * (x * y + z * w),     1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
+                       2 * (x * z - y * w),     2 * (y * z + x * w),     1 - 2 * (x * x + y * y)};
+  T* R = (T*)ea.rot + (size_t)b * 9;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) R[k] = (T)(s * m[k]);
+}
+
+// x'[conf] = r_ia p_q R_b with conf = ((b N + i) A + a) 50 + q  (E2: not offset by R_a)
+template <typename T>
+__global__ __launch_bounds__(256) void k_ecp_points(EcpArgs ea) {
+  const int M = ea.N * ea.A * ECP_NQ;
+  const size_t conf = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (conf >= (size_t)ea.B * M) return;
+  const int b = (int)(conf / M);
+  const int rem = (int)(conf - (size_t)b * M);
+  const int i = rem / (ea.A * ECP_NQ);
+  const int a = (rem / ECP_NQ) % ea.A;
+  const int q = rem % ECP_NQ;
+  const T* x = (const T*)ea.pos + (size_t)b * 3 * ea.N + 3 * i;
+  double r2 = 0.0;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const double t = (double)x[d] - ea.tab[a * 3 + d];
+    r2 += t * t;
+  }
+  const double r = sqrt(r2);
+  double p[3], pr[3];
+  int grp;
+  ecp_point(q, p, grp);
+  ecp_rotate<T>((const T*)ea.rot + (size_t)b * 9, p, pr);
+  T* o = (T*)ea.xnew + conf * 3;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) o[d] = (T)(r * pr[d]);
+}
+
+__device__ __forceinline__ double ecp_radial(const double* t, int K, double r, double nshift) {
+  double s = 0.0;
+  for (int k = 0; k < K; ++k) s += t[3 * k + 1] * pow(r, t[3 * k] + nshift) * exp(-t[3 * k + 2] * r * r);
+  return s;
+}
+
+// P_l(x) of pseudopotential.py:250-269 (1/(4 pi) included, E5)
+__device__ __forceinline__ double ecp_pl(int l, double x) {
+  const double c = 0.079577471545947668;   // 1/(4 pi)
+  if (l == 0) return c;
+  if (l == 1) return 3.0 * c * x;
+  if (l == 2) return 5.0 * c * 0.5 * (3.0 * x * x - 1.0);
+  return 7.0 * c * 0.5 * (5.0 * x * x * x - 3.0 * x);
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void k_ecp_energy(EcpArgs ea) {
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int N = ea.N, A = ea.A;
+  const int M = N * A * ECP_NQ;
+  const double* atoms = ea.tab;
+  const double* charges = ea.tab + 3 * A;
+  const int stride = 3 * (ea.KL + ea.L * ea.KN);
+  const double* tabs = ea.tab + 4 * A;
+  const T* x = (const T*)ea.pos + (size_t)b * 3 * N;
+  const T* R = (const T*)ea.rot + (size_t)b * 9;
+  const double la0 = (double)((const T*)ea.lp0)[b], ph0 = (double)((const T*)ea.ph0)[b];
+  const double dn = 1.0 / (la0 * la0 + ph0 * ph0);   // 1 / den, den = la0 + i ph0 (E4)
+  double er = 0.0, ei = 0.0;
+  for (int idx = lane; idx < M; idx += 64) {
+    const int i = idx / (A * ECP_NQ);
+    const int a = (idx / ECP_NQ) % A;
+    const int q = idx % ECP_NQ;
+    double ae[3], r2 = 0.0;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      ae[d] = (double)x[3 * i + d] - atoms[a * 3 + d];
+      r2 += ae[d] * ae[d];
+    }
+    const double r = sqrt(r2);
+    double p[3], pr[3];
+    int grp;
+    ecp_point(q, p, grp);
+    ecp_rotate<T>(R, p, pr);
+    // Frobenius norm of the group's rotated coordinates r p'_q (E3)
+    double fro2 = 0.0;
+    for (int qq = ecp_group_begin(grp); qq < ecp_group_end(grp); ++qq) {
+      double pp[3], ppr[3];
+      int gg;
+      ecp_point(qq, pp, gg);
+      ecp_rotate<T>(R, pp, ppr);
+#pragma unroll
+      for (int d = 0; d < 3; ++d) fro2 += (r * ppr[d]) * (r * ppr[d]);
+    }
+    const double dot = ae[0] * (r * pr[0]) + ae[1] * (r * pr[1]) + ae[2] * (r * pr[2]);
+    const double cs = dot / (r * sqrt(fro2));
+    const size_t conf = (size_t)b * M + idx;
+    const double la = (double)((const T*)ea.lpq)[conf], ph = (double)((const T*)ea.phq)[conf];
+    const double w = ecp_weight(grp);
+    // ratio = (la + i ph) / (la0 + i ph0) * w
+    const double rr = (la * la0 + ph * ph0) * dn * w, ri = (ph * la0 - la * ph0) * dn * w;
+    const double* tnl = tabs + a * stride + 3 * ea.KL;
+    double s = 0.0;
+    for (int l = 0; l < ea.L; ++l) s += ecp_pl(l, cs) * ecp_radial(tnl + 3 * ea.KN * l, ea.KN, r, 0.0);   // E1
+    er += s * rr;
+    ei += s * ri;
+  }
+  // local part: -Z_a / r_ia + sum_k c r^(n-2) e^{-alpha r^2}  (pseudopotential.py:95-116)
+  for (int idx = lane; idx < N * A; idx += 64) {
+    const int i = idx / A, a = idx - (idx / A) * A;
+    double r2 = 0.0;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const double t = (double)x[3 * i + d] - atoms[a * 3 + d];
+      r2 += t * t;
+    }
+    const double r = sqrt(r2);
+    er += -charges[a] / r + ecp_radial(tabs + a * stride, ea.KL, r, -2.0);
+  }
+  er = wave_sum(er);
+  ei = wave_sum(ei);
+  if (lane == 0) {
+    // the all-electron E_L carries -sum Z/r already; the pp Hamiltonian has it once, in the
+    // local part (E7): remove the all-electron copy
+    double ven = 0.0;
+    for (int i = 0; i < N; ++i)
+      for (int a = 0; a < A; ++a) {
+        double r2 = 0.0;
+        for (int d = 0; d < 3; ++d) {
+          const double t = (double)x[3 * i + d] - atoms[a * 3 + d];
+          r2 += t * t;
+        }
+        ven -= charges[a] / sqrt(r2);
+      }
+    ((T*)ea.e_re)[b] = (T)((double)((const T*)ea.eall)[b] - ven + er);
+    ((T*)ea.e_im)[b] = (T)ei;
+  }
+}
+
+}  // namespace aq

@@ -47,6 +47,13 @@ struct KArgs {
   const double* taueff;   // device scalar: limdrift factor of pgrad (VMCmcstep.py:11-14)
   double tstep;
   uint64_t seed, step;
+  // single-electron-move layout (proposal != 0, k_walker_rev / k_moved_electron): configuration
+  // conf is walker conf / mper with electron (conf % mper) / mdiv moved; 0 means mper = N,
+  // mdiv = 1 (the Metropolis proposals).  xnew [nconf][3]: the moved electron's position
+  // (ECP quadrature points); nullptr: x + limdrift(grad) tstep + sqrt(tstep) gauss1.
+  int mper, mdiv;
+  const void* xnew;
+  int value_only;         // k_walker_rev: log|psi| and phase only (no backward pass)
   // Metropolis caches (walker_rev.h WCache / ECache); nullptr outside aiqmc_mc_step
   void* wcache;
   void* ecache;

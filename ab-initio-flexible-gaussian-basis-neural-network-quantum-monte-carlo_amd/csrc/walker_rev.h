@@ -167,15 +167,21 @@ __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
   const int blk = xcd_major(blockIdx.x, gridDim.x);
   const int nrec = ka.nconf - blk * 16 < 16 ? ka.nconf - blk * 16 : 16;
   const int q = blk * 16 + (s < nrec ? s : nrec - 1);
-  const int b = q / N, i = q - b * N;
-  const T tstep = (T)ka.tstep;
-  const T te = (T)(*ka.taueff);
+  const int mper = ka.mper ? ka.mper : N, mdiv = ka.mdiv ? ka.mdiv : 1;
+  const int b = q / mper, i = (q - b * mper) / mdiv;
   T xp[3];
+  if (ka.xnew) {
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const size_t o = (size_t)b * 3 * N + 3 * i + c;
-    const T ge = ((const T*)ka.pgrad)[o] * te;
-    xp[c] = ((const T*)ka.pos)[o] + (ge * tstep + f_sqrt(tstep) * ((const T*)ka.gauss1)[o]);
+    for (int c = 0; c < 3; ++c) xp[c] = ((const T*)ka.xnew)[(size_t)q * 3 + c];
+  } else {
+    const T tstep = (T)ka.tstep;
+    const T te = (T)(*ka.taueff);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const size_t o = (size_t)b * 3 * N + 3 * i + c;
+      const T ge = ((const T*)ka.pgrad)[o] * te;
+      xp[c] = ((const T*)ka.pos)[o] + (ge * tstep + f_sqrt(tstep) * ((const T*)ka.gauss1)[o]);
+    }
   }
   ElecOut<T, A> eo;
   electron_stage<T, N, A>(P, xp, i, lc, eo);
@@ -244,16 +250,21 @@ k_walker_rev(KArgs ka) {
   // ------------------------------------------------------------------ F0 positions (as k_walker)
   int pb = conf, pi = -1;
   if (ka.proposal) {
-    pb = conf / N;
-    pi = conf - pb * N;
+    const int mper = ka.mper ? ka.mper : N, mdiv = ka.mdiv ? ka.mdiv : 1;
+    pb = conf / mper;
+    pi = (conf - pb * mper) / mdiv;
   }
   if (lane < 3 * N) {
     T x = ((const T*)ka.pos)[(size_t)pb * 3 * N + lane];
     if (ka.proposal && lane / 3 == pi) {
-      const T z = ((const T*)ka.gauss1)[(size_t)pb * 3 * N + lane];   // drawn by the host or k_draws
-      const T ge = ((const T*)ka.pgrad)[(size_t)pb * 3 * N + lane] * (T)(*ka.taueff);
       sm[SM::R + (lane - 3 * pi)] = x;                       // old position of the moved electron
-      x = x + (ge * tstep + f_sqrt(tstep) * z);
+      if (ka.xnew) {
+        x = ((const T*)ka.xnew)[(size_t)conf * 3 + (lane - 3 * pi)];
+      } else {
+        const T z = ((const T*)ka.gauss1)[(size_t)pb * 3 * N + lane];   // drawn by the host or k_draws
+        const T ge = ((const T*)ka.pgrad)[(size_t)pb * 3 * N + lane] * (T)(*ka.taueff);
+        x = x + (ge * tstep + f_sqrt(tstep) * z);
+      }
     }
     xs[lane] = x;
   }
@@ -586,6 +597,16 @@ k_walker_rev(KArgs ka) {
     }
   } else {
     gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi, (!PREP && !ka.proposal) ? Wc + WC::pv : nullptr);
+  }
+  if constexpr (!PREP) {
+    if (ka.value_only) {   // ECP quadrature configurations: log|psi| and phase only
+      const T lpsi = logdet + wave_sum(jv + jve);
+      if (lane == 0) {
+        if (ka.logabs) ((T*)ka.logabs)[conf] = lpsi;
+        if (ka.phase) ((T*)ka.phase)[conf] = f_atan2(phi, phr);
+      }
+      return;
+    }
   }
   __syncthreads();
 #define BRE(c, s) Mx[((c) * N + (s)) * 2]

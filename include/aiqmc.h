@@ -104,10 +104,48 @@ int aiqmc_mc_step(aiqmc_ctx* ctx, void* pos_inout, int32_t B, int32_t nsteps, do
                   int32_t rng_mode, const void* gauss1, const void* gauss2, const void* u,
                   uint64_t seed, uint64_t offset, int32_t* accept_out, void* stream);
 
+/* Pseudopotential tables (pphamiltonian.local_energy arguments,
+ * Energy/pphamiltonian.py:130-146; shapes as the example drivers pass them,
+ * example/single_atom_C/single_atom_C.py:13-23).  All HOST pointers; the
+ * nonlocal arrays have list_l + 1 angular channels (P_l of
+ * pseudopotential.py:250-269 returns list_l + 1 terms). */
+typedef struct aiqmc_ecp {
+  int32_t list_l;               /* 0..3                                       */
+  int32_t n_local;              /* KL = Rn_local.shape[1]                     */
+  int32_t n_nonlocal;           /* KN = Rn_non_local.shape[2]                 */
+  const double* rn_local;       /* [A][KL]  (r**(n-2), pseudopotential.py:95) */
+  const double* local_coes;     /* [A][KL]                                    */
+  const double* local_exps;     /* [A][KL]                                    */
+  const double* rn_non_local;   /* [A][list_l+1][KN]  (r**n, :150)            */
+  const double* non_local_coes; /* [A][list_l+1][KN]                          */
+  const double* non_local_exps; /* [A][list_l+1][KN]                          */
+} aiqmc_ecp;
+
+/* Attach pseudopotential tables to the context (replaces the closure
+ * arguments of pphamiltonian.local_energy).  The potential charges of the
+ * context (aiqmc_cfg.charges) are the effective core charges Z_eff. */
+int aiqmc_set_ecp(aiqmc_ctx* ctx, const aiqmc_ecp* ecp);
+
+/* Complex pseudopotential local energy of B walkers (the reference's
+ * pphamiltonian.local_energy(...) -> _e_l(params, key, data), vmapped with one
+ * key per walker, loss.py:203-204):
+ *   e_re + i e_im = V_ee + V_nn + KE + local pp + nonlocal pp
+ * with the nonlocal quadrature over the 50-point grid rotated by one random
+ * orthogonal matrix per walker (pseudopotential.py:233-241).
+ * rng_mode AIQMC_RNG_HOST: rot = device [B][3][3] (row-major, ctx dtype), the
+ *   matrix jax.random.orthogonal would return; AIQMC_RNG_PHILOX: rot may be
+ *   NULL, Haar O(3) matrices are drawn from (seed, offset).
+ * logabs_q / phase_q (optional, [B][N][A][50]): log|psi| and phase at the
+ * quadrature configurations, electron i moved to r_ia * (p_q R). */
+int aiqmc_local_energy_ecp(aiqmc_ctx* ctx, const void* pos, int32_t B, int32_t rng_mode, const void* rot,
+                           uint64_t seed, uint64_t offset, void* e_re, void* e_im, void* logabs_q,
+                           void* phase_q, void* stream);
+
 /* Optional HIP-event timing of the hot kernels, recorded on the caller's
  * stream around each launch while enabled.  Slots: 0 = proposal
  * value+gradient launches of aiqmc_mc_step, 1 = walker gradient launches of
- * aiqmc_mc_step, 2 = aiqmc_local_energy launches.  aiqmc_profile_read waits
+ * aiqmc_mc_step, 2 = aiqmc_local_energy launches, 3 = value-only launches of
+ * the ECP quadrature configurations.  aiqmc_profile_read waits
  * for the recorded events, returns the summed kernel time in ms and the launch
  * count of one slot, and clears it. */
 int aiqmc_profile_enable(aiqmc_ctx* ctx, int32_t on);

@@ -92,6 +92,10 @@ def make_system(name: str) -> System:
     elif name == "C":
         atoms = np.zeros((1, 3))
         charges = np.array([6.0])
+    elif name == "C_ecp":
+        # ccECP carbon: Z_eff = 4 at the origin, 4 valence electrons (single_atom_C.py:9-11)
+        atoms = np.zeros((1, 3))
+        charges = np.array([4.0])
     elif name == "Ne":
         atoms = np.zeros((1, 3))
         charges = np.array([10.0])

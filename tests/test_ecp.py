@@ -1,0 +1,205 @@
+"""Pseudopotential (ccECP) local energy: oracle known answers (CPU) and HIP parity (GPU).
+
+Reference: AIQMCrelease3/Energy/pphamiltonian.py:130-190,
+pseudopotential/pseudopotential.py:86-318, pseudopotential/pp_energy_test.py:45-105;
+config example/single_atom_C/single_atom_C.py (C atom, Z_eff = 4, list_l = 2).
+The reference has no ECP tests and cannot run here (JAX absent): the oracle is
+pinned by quadrature identities and closed forms below, and the kernels by the
+oracle's golden fixture tests/golden/C_ecp.npz (make_golden_ecp.py).
+
+Tolerances: float64 kernels |dE| <= 1e-6 Ha (the north_star bound; observed
+~1e-12), quadrature log psi to 1e-9; float32 kernels 2e-4 relative on Re E_L.
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import pphamiltonian as pp
+
+
+# ----------------------------------------------------------------------------- CPU: oracle
+
+def test_grid_weights_and_norms():
+    groups, w = pp.quadrature_grids()
+    assert [g.shape[0] for g in groups] == [6, 12, 8, 24]
+    assert abs(sum(len(g) * wi for g, wi in zip(groups, w)) - 1.0) < 1e-15
+    for g in groups:
+        np.testing.assert_allclose(np.linalg.norm(g, axis=1), 1.0, atol=2e-8)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_grid_integrates_legendre(seed):
+    """The 50-point octahedral rule (Mitas-Shirley-Ceperley) integrates P_l(u.p) exactly
+    for l <= 11 (weights already normalised to the sphere average)."""
+    rng = np.random.default_rng(seed)
+    u = rng.standard_normal(3)
+    u /= np.linalg.norm(u)
+    groups, w = pp.quadrature_grids()
+    rot = pp.haar_rotations(rng, 1)[0]
+    for l in range(1, 8):
+        s = 0.0
+        for g, wi in zip(groups, w):
+            x = pp.rotate_points(rot, g) @ u
+            s += wi * np.polynomial.legendre.legval(x, [0] * l + [1]).sum()
+        assert abs(s) < 1e-7, (l, s)
+
+
+def test_local_pp_closed_form():
+    ecp = pp.c_atom_ccecp()
+    pos = torch.tensor([0.3, -0.2, 0.9, 1.1, 0.4, -0.5], dtype=torch.float64)
+    atoms = torch.zeros(1, 3, dtype=torch.float64)
+    charges = torch.tensor([4.0], dtype=torch.float64)
+    got = pp.local_pp_energy(ecp, pos, atoms, charges).item()
+    want = 0.0
+    for i in range(2):
+        r = float(np.linalg.norm(pos.numpy()[3 * i:3 * i + 3]))
+        want += -4.0 / r
+        for n, c, a in zip([1.0, 3.0, 2.0], [4.0, 57.74008, -25.81955], [14.43502, 8.39889, 7.38188]):
+            want += c * r ** (n - 2) * math.exp(-a * r * r)      # pseudopotential.py:95,101-102
+    assert abs(got - want) < 1e-13
+
+
+class _ConstNet:
+    """log psi = const: every ratio is the group weight."""
+
+    def __init__(self, N):
+        self.N, self.A = N, 1
+        self.atoms = torch.zeros(1, 3, dtype=torch.float64)
+        self.charges = torch.tensor([4.0], dtype=torch.float64)
+
+    def apply(self, params, x):
+        return torch.tensor(0.3, dtype=torch.float64), torch.tensor(-1.7, dtype=torch.float64)
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_nonlocal_constant_wavefunction(seed):
+    """ratio == w: sum_q w P_0 = 1/(4 pi) (E5); the l = 1 term vanishes by inversion
+    symmetry of every grid group; so E_nl = sum_i v_0(r_i) / (4 pi), any rotation."""
+    rng = np.random.default_rng(seed)
+    ecp = pp.ECP([[1.0]], [[0.0]], [[1.0]], [[[2.0], [1.0]]], [[[3.0], [5.0]]], [[[0.7], [0.4]]], 1)
+    net = _ConstNet(2)
+    pos = torch.tensor(rng.standard_normal(6))
+    rot = pp.haar_rotations(rng, 1)[0]
+    nl, _ = pp.nonlocal_pp_energy(net, None, ecp, pos, rot)
+    want = 0.0
+    for i in range(2):
+        r = float(np.linalg.norm(pos.numpy()[3 * i:3 * i + 3]))
+        want += 3.0 * r ** 2 * math.exp(-0.7 * r * r) / (4 * math.pi)
+    assert abs(nl.real.item() - want) < 1e-12 and abs(nl.imag.item()) < 1e-12
+
+
+def test_cos_theta_quirk():
+    """E3: cos(theta) is the true cosine divided by sqrt(points in the group)."""
+    pos = torch.tensor([0.3, -0.2, 0.9], dtype=torch.float64)
+    atoms = torch.zeros(1, 3, dtype=torch.float64)
+    groups, _ = pp.quadrature_grids()
+    for g in groups:
+        cos, cfg = pp.rotated_configurations(pos, atoms, g)
+        u = pos.numpy() / np.linalg.norm(pos.numpy())
+        true = g @ u / np.linalg.norm(g, axis=1)
+        np.testing.assert_allclose(cos[0, 0].numpy(), true / math.sqrt(len(g)), rtol=1e-7, atol=1e-9)
+        # E2: the moved electron sits at r p_q (atom at the origin here)
+        np.testing.assert_allclose(cfg[0, 0].numpy(), np.linalg.norm(pos.numpy()) * g, rtol=1e-15)
+
+
+def test_golden_fixture_consistent(golden_dir):
+    g = dict(np.load(os.path.join(golden_dir, "C_ecp.npz")))
+    assert g["pos"].shape == (4, 12) and g["rot"].shape == (4, 3, 3)
+    np.testing.assert_allclose(np.einsum("bij,bkj->bik", g["rot"], g["rot"]), np.broadcast_to(np.eye(3), (4, 3, 3)),
+                               atol=1e-12)
+    assert np.all(np.isfinite(g["e_re"])) and np.all(np.isfinite(g["logq_re"]))
+
+
+# ----------------------------------------------------------------------------- GPU: HIP vs oracle
+
+def _ecp_ctx(dtype):
+    from oracle import system
+    from aiqmc import _lib
+    s = system.make_system("C_ecp")
+    t = s.tables()
+    ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
+                       t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"], dtype=dtype, device=0)
+    e = pp.c_atom_ccecp()
+    ctx.set_ecp(e.rn_local, e.local_coes, e.local_exps, e.rn_non_local, e.non_local_coes, e.non_local_exps, e.list_l)
+    return s, ctx
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_ecp_local_energy_golden(golden_dir, dtype):
+    g = dict(np.load(os.path.join(golden_dir, "C_ecp.npz")))
+    s, ctx = _ecp_ctx(dtype)
+    ctx.set_params(g["params_flat"])
+    pos = torch.tensor(g["pos"], dtype=dtype, device="cuda")
+    rot = torch.tensor(g["rot"], dtype=dtype, device="cuda")
+    e, lq, pq = ctx.local_energy_ecp(pos, rot=rot, want_quadrature=True)
+    torch.cuda.synchronize()
+    er, ei = e.real.double().cpu().numpy(), e.imag.double().cpu().numpy()
+    if dtype == torch.float64:
+        assert np.max(np.abs(er - g["e_re"])) <= 1e-6, (er, g["e_re"])
+        assert np.max(np.abs(ei - g["e_im"])) <= 1e-6, (ei, g["e_im"])
+        np.testing.assert_allclose(lq.cpu().numpy(), g["logq_re"], rtol=1e-9, atol=1e-9)
+        ph = pq.cpu().numpy()
+        np.testing.assert_allclose(np.cos(ph), np.cos(g["logq_im"]), atol=1e-9)
+        np.testing.assert_allclose(np.sin(ph), np.sin(g["logq_im"]), atol=1e-9)
+    else:
+        np.testing.assert_allclose(er, g["e_re"], rtol=2e-4, atol=2e-3)
+        assert np.max(np.abs(ei - g["e_im"])) <= 2e-3
+
+
+@pytest.mark.gpu
+def test_ecp_reuse_matches_scratch(golden_dir):
+    """Quadrature configurations from the walker cache == evaluated from scratch (fp64)."""
+    g = dict(np.load(os.path.join(golden_dir, "C_ecp.npz")))
+    s, ctx = _ecp_ctx(torch.float64)
+    ctx.set_params(g["params_flat"])
+    pos = torch.tensor(g["pos"], device="cuda")
+    rot = torch.tensor(g["rot"], device="cuda")
+    e1, l1, p1 = ctx.local_energy_ecp(pos, rot=rot, want_quadrature=True)
+    ctx.set_proposal_reuse(False)
+    e2, l2, p2 = ctx.local_energy_ecp(pos, rot=rot, want_quadrature=True)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(l1.cpu().numpy(), l2.cpu().numpy(), rtol=1e-11, atol=1e-11)
+    assert torch.max(torch.abs(e1 - e2)).item() < 1e-10
+
+
+@pytest.mark.gpu
+def test_ecp_full_batch_walker_independent():
+    """4096 fp32 walkers with Philox rotations: finite, and a walker's energy does not depend
+    on the rest of the batch (no batch coupling in the pp Hamiltonian) given its rotation."""
+    from oracle import system
+    s, ctx = _ecp_ctx(torch.float64)
+    rng = np.random.default_rng(7)
+    ctx.set_params(system.flatten_params(system.init_params(rng, s, randomize_aux=True)))
+    B = 4096
+    pos = torch.tensor(system.init_electrons(rng, s.atoms, s.charges, B, 1.0), device="cuda")
+    e = ctx.local_energy_ecp(pos, seed=5, offset=0)
+    rot = torch.tensor(pp.haar_rotations(rng, B), device="cuda")
+    eh = ctx.local_energy_ecp(pos, rot=rot)
+    sub = torch.arange(0, B, 97, device="cuda")
+    es = ctx.local_energy_ecp(pos[sub].contiguous(), rot=rot[sub].contiguous())
+    torch.cuda.synchronize()
+    assert torch.isfinite(e.real).all() and torch.isfinite(e.imag).all()
+    assert torch.max(torch.abs(eh[sub] - es)).item() < 1e-9
+
+
+@pytest.mark.gpu
+def test_ecp_errors():
+    from oracle import system
+    from aiqmc import _lib
+    s = system.make_system("C_ecp")
+    t = s.tables()
+    ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
+                       t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"],
+                       dtype=torch.float64, device=0)
+    ctx.set_params(system.flatten_params(system.init_params(np.random.default_rng(0), s)))
+    pos = torch.zeros(2, 12, dtype=torch.float64, device="cuda")
+    with pytest.raises(RuntimeError, match="aiqmc_set_ecp has not been called"):
+        ctx.local_energy_ecp(pos)
+    e = pp.c_atom_ccecp()
+    with pytest.raises(RuntimeError, match="list_l"):
+        ctx.set_ecp(e.rn_local, e.local_coes, e.local_exps, np.zeros((1, 5, 2)), np.zeros((1, 5, 2)),
+                    np.zeros((1, 5, 2)), 4)
