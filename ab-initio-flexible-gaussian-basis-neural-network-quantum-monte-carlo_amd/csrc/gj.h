@@ -59,7 +59,8 @@ __device__ __forceinline__ unsigned key_bits(double x) {
 }
 
 // rec (optional): the pivot sequence, recorded for gj_inverse_fixed: rec[k] = row of
-// step k, rec[N + k] = |pivot_k|^2, rec[2N] = permutation parity (written by lane 0).
+// step k, rec[N + k] = 1 / |pivot_k|, rec[2N] = permutation parity, rec[2N + 1] = log|det A|
+// (written by lane 0).
 template <typename T, int N>
 __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, int lane, T& logdet, T& phr,
                                            T& phi, T* rec = nullptr) {
@@ -115,7 +116,7 @@ __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, in
     const T den = pr * pr + pim * pim;
     if (rec && lane == 0) {
       rec[k] = T(p);
-      rec[N + k] = den;
+      rec[N + k] = f_sqrt(f_rcp(den));
     }
     const T rden = f_rcp(den);
     ld += T(0.5) * f_log(den);                 // log|pivot|
@@ -165,7 +166,10 @@ __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, in
       Bout[(myk[t] * N + myp) * 2 + 1] = ai[t];
     }
   }
-  if (rec && lane == 0) rec[2 * N] = T(inv & 1);
+  if (rec && lane == 0) {
+    rec[2 * N] = T(inv & 1);
+    rec[2 * N + 1] = ld;
+  }
   if (inv & 1) {
     pr_ = -pr_;
     pi_ = -pi_;
@@ -180,14 +184,16 @@ __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, in
 // row slot k <- A row perm[k], so step k pivots on slot k (row group k / RW, register
 // k % RW), both compile-time: no pivot search, no runtime register selection, no
 // bookkeeping.  The result X = (PA)^{-1} gives B[i][perm[j]] = X[i][j]; det A =
-// sgn(perm) prod pivots.  bad = some |pivot_k|^2 < 1e-2 |walker pivot_k|^2 (the
-// order may not suit this matrix: the caller falls back to gj_inverse).
+// sgn(perm) prod pivots, accumulated relative to the walker's pivots:
+// z = prod_k pivot_k / |walker pivot_k| (O(1) for a one-electron move), so
+// log|det A| = log|det A_walker| + log|z| and the phase is z / |z| -- one log and one
+// sqrt per matrix instead of per step.  bad = some |pivot_k| < 0.1 |walker pivot_k| or z
+// not finite (the order may not suit this matrix: the caller falls back to gj_inverse).
 // rec: the walker's record written by gj_inverse (LDS copy).
 template <typename T, int N>
 __device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bout, int lane, const T* rec,
                                                  T& logdet, T& phr, T& phi, bool& bad) {
   constexpr int RW = (N + 3) / 4;
-  constexpr bool PK = sizeof(T) == 4;   // fp32: complex entries as packed pairs (v_pk_fma_f32)
   using V2 = typename Pair<T>::type;
   const int c = lane & 15;
   const int rg = lane >> 4;
@@ -205,7 +211,7 @@ __device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bo
     }
     a2[t] = pair_make<T>(a, b);
   }
-  T ld = T(0), pr_ = T(1), pi_ = T(0);
+  T zr = T(1), zi = T(0);
   bool small = false;
 #pragma unroll
   for (int k = 0; k < N; ++k) {
@@ -213,36 +219,35 @@ __device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bo
     const T pr = rdlane(pair_re<T>(a2[ts]), 16 * g + k);
     const T pim = rdlane(pair_im<T>(a2[ts]), 16 * g + k);
     const T den = pr * pr + pim * pim;
-    small = small || (den < T(1e-2) * rec[N + k]);
-    const T rden = f_rcp(den);
-    ld += T(0.5) * f_log(den);
     {
-      const T rm = f_sqrt(rden);
-      const T ur = pr * rm, ui = pim * rm;
-      const T nr = pr_ * ur - pi_ * ui, ni = pr_ * ui + pi_ * ur;
-      pr_ = nr;
-      pi_ = ni;
+      const T sk = rec[N + k];
+      const T ur = pr * sk, ui = pim * sk;
+      small = small || (ur * ur + ui * ui < T(1e-2));
+      const T nr = zr * ur - zi * ui, ni = zr * ui + zi * ur;
+      zr = nr;
+      zi = ni;
     }
+    const T rden = f_rcp(den);
     const T ir = pr * rden, ii = -pim * rden;   // 1 / pivot
     const T q0r = __shfl(pair_re<T>(a2[ts]), 16 * g + c), q0i = __shfl(pair_im<T>(a2[ts]), 16 * g + c);
     const bool ck = (c == k);
     const T qr = ck ? ir : q0r * ir - q0i * ii;
     const T qi = ck ? ii : q0r * ii + q0i * ir;
-    // a[r][c] <- keep * a[r][c] - a[r][k] q[c]:  [re, im] += fr [-qr, -qi] + fi [qi, -qr]
-    const V2 m1 = pair_make<T>(-qr, -qi), m2 = pair_make<T>(qi, -qr);
-    const T keep = ck ? T(0) : T(1);
+    // a[r][c] <- a[r][c] + a[r][k] m with m = -q[c] (c != k) or -q[k] - 1 (c == k: there
+    // a[r][k] is the lane's own entry and the result is -a[r][k] / pivot):
+    //   [re, im] += fr [mr, mi] + fi [-mi, mr]
+    const T mr = ck ? -qr - T(1) : -qr, mi = -qi;
+    const V2 m1 = pair_make<T>(mr, mi), m2 = pair_make<T>(-mi, mr);
 #pragma unroll
     for (int t = 0; t < RW; ++t) {
       const T fr = row_bcast(pair_re<T>(a2[t]), k);
       const T fi = row_bcast(pair_im<T>(a2[t]), k);
-      V2 n = pair_scale<T>(a2[t], keep);
-      n = pair_fma<T>(fr, m1, n);
+      V2 n = pair_fma<T>(fr, m1, a2[t]);
       n = pair_fma<T>(fi, m2, n);
       a2[t] = n;
     }
     if (rg == g) a2[ts] = pair_make<T>(qr, qi);
   }
-  (void)PK;
   const int pc = clive ? (int)rec[c] : 0;
 #pragma unroll
   for (int t = 0; t < RW; ++t) {
@@ -252,14 +257,14 @@ __device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bo
       Bout[(i * N + pc) * 2 + 1] = pair_im<T>(a2[t]);
     }
   }
-  if (rec[2 * N] != T(0)) {
-    pr_ = -pr_;
-    pi_ = -pi_;
-  }
-  logdet = ld;
-  phr = pr_;
-  phi = pi_;
-  bad = small;
+  const T z2 = zr * zr + zi * zi;
+  const bool zok = z2 > T(0) && z2 < T(1e30);
+  const T rz = f_rcp(f_sqrt(zok ? z2 : T(1)));
+  const T sg = rec[2 * N] != T(0) ? -rz : rz;
+  logdet = rec[2 * N + 1] + T(0.5) * f_log(zok ? z2 : T(1));
+  phr = zr * sg;
+  phi = zi * sg;
+  bad = small || !zok;
 }
 
 }  // namespace aq

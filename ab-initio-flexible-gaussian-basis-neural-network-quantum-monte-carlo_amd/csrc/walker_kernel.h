@@ -267,7 +267,9 @@ __device__ __forceinline__ void h_layer(cptr<T> P, const T* xs, T* hb, const PJ<
 }
 
 template <typename T, int N, int A, int MODE>
-__global__ __launch_bounds__(64) void k_walker(KArgs ka) {
+// Diagnostics-only kernels (forward-mode gradient and Laplacian): one wave per SIMD, so that
+// register overflow goes to the AGPR half of the register file instead of scratch.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_walker(KArgs ka) {
   constexpr bool LAP = (MODE == MODE_LAP);
   using Ly = Lay<N, A>;
   using SM = Smem<T, N, LAP>;

@@ -35,6 +35,9 @@ static __device__ unsigned long long aq_phase_cycles[32];
     if (lane == 0) atomicAdd(&aq_phase_cycles[(ka.proposal ? 16 : 0) + (k)], t_ - t_ph); \
     t_ph = t_;                                                                           \
   } while (0)
+#elif defined(AQ_PHASE_MARK)
+// ISA-inspection build: a marker comment in the assembly at each phase boundary
+#define AQ_PH(k) asm volatile(";AQMARK " #k)
 #else
 #define AQ_PH(k) \
   do {           \
@@ -63,7 +66,7 @@ struct SmemRev {
   static constexpr int mx = R + N * N * 2;
   static constexpr int dbar = R;
   static constexpr int R_n = cmax(cmax(4 * N * N, 3 * N * N), 4 + 64 * 12);
-  static constexpr int pv = R + R_n;             // [2N+1] the walker's pivot record (proposals)
+  static constexpr int pv = R + R_n;             // [2N+2] the walker's pivot record (proposals)
   static constexpr int end = pv + 2 * N + 2;
   static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
   static constexpr int hoff(int l) { return l == 0 ? 0 : N * D0; }   // l = 0 or 3
@@ -83,8 +86,8 @@ struct WCache {
   static constexpr int jaed = jaev + N;             // [48]       dJ_ae/dx per direction lane
   static constexpr int g2 = jaed + 48;              // [3][2][N][4]
   static constexpr int jee = g2 + 3 * 2 * N * 4;    // [1]        J_ee
-  static constexpr int pv = jee + 1;                // [2N+1]     Gauss-Jordan pivot record (gj.h)
-  static constexpr int pt = ((pv + 2 * N + 1 + 3) / 4) * 4; // [N][N][8]  tanh outputs t1, t2 of pair (k, i)
+  static constexpr int pv = jee + 1;                // [2N+2]     Gauss-Jordan pivot record (gj.h)
+  static constexpr int pt = ((pv + 2 * N + 2 + 3) / 4) * 4; // [N][N][8]  tanh outputs t1, t2 of pair (k, i)
   static constexpr int size = ((pt + 8 * N * N + 63) / 64) * 64;
 };
 // Per-proposal electron-local stage of the moved electron (k_moved_electron).
@@ -307,7 +310,7 @@ k_walker_rev(KArgs ka) {
     jv = (val && live) ? ((er == pi) ? Eq[EC::jv] : Wc[WC::jaev + er]) : T(0);
     jd1 = dir ? ((le == pi) ? Eq[EC::jd + lc] : Wc[WC::jaed + lane]) : T(0);
     jve = lane == 0 ? Wc[WC::jee] : T(0);
-    if (lane < 2 * N + 1) sm[SM::pv + lane] = Wc[WC::pv + lane];
+    if (lane < 2 * N + 2) sm[SM::pv + lane] = Wc[WC::pv + lane];
 #pragma unroll
     for (int t = 0; t < NY; ++t)
       if (lane + 64 * t < N * N) Yv[lane + 64 * t] = ry[t];
@@ -480,7 +483,7 @@ k_walker_rev(KArgs ka) {
   // ------------------------------------------------------------------ F4 h-stream layers (values)
   // lane = 4i + f (electron i, unit f): h^l[i][f] stays in a register across layers; the
   // spin-group means are class sums over lanes of equal f; the four lanes of electron i
-  // each evaluate all of its conv outputs (no LDS round trip, no barrier).
+  // share its conv outputs through quad DPP sums (no LDS round trip, no barrier).
   T* hl = sm + SM::hl;
   T* cqv = sm + SM::cq;
   T* sv = sm + SM::sv;
@@ -499,53 +502,38 @@ k_walker_rev(KArgs ka) {
     const cptr<T> convb = P + (l == 0 ? Ly::conv_b0 : (l == 1 ? Ly::conv_b1 : Ly::conv_b2)) + ic * Q;
     const cptr<T> sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
     const cptr<T> sngb = P + (l == 0 ? Ly::sng_b0 : (l == 1 ? Ly::sng_b1 : Ly::sng_b2));
-    T hrow[D0];
-    T gs[2][D0 / 4];
+    // conv output q = tanh(mean_4(f w) + b) over the input quad 4q..4q+3
+    // (network_blocks.py:106-116): lane f of electron ic holds input 4q + f (h^l unit
+    // 4t + f, a group mean of unit 4t + f, or a g2 unit f) and the quad adds the four
+    // products by DPP, so each product is computed once
+    T hown[D0 / 4];
     if (l == 0) {
 #pragma unroll
-      for (int m = 0; m < D0; ++m) hrow[m] = hl[ic * D0 + m];
-#pragma unroll
-      for (int t = 0; t < D0 / 4; ++t) {
-        const T x = ilive ? hl[ic * D0 + ff + 4 * t] : T(0);
-        gs[0][t] = class4_sum(inG1 ? T(0) : x);
-        gs[1][t] = class4_sum(inG1 ? x : T(0));
-      }
+      for (int t = 0; t < D0 / 4; ++t) hown[t] = hl[ic * D0 + ff + 4 * t];
     } else {
-      hrow[0] = quad_bcast<0>(hreg);
-      hrow[1] = quad_bcast<1>(hreg);
-      hrow[2] = quad_bcast<2>(hreg);
-      hrow[3] = quad_bcast<3>(hreg);
-      const T x = ilive ? hreg : T(0);
-      gs[0][0] = class4_sum(inG1 ? T(0) : x);
-      gs[1][0] = class4_sum(inG1 ? x : T(0));
+#pragma unroll
+      for (int t = 0; t < D0 / 4; ++t) hown[t] = hreg;
     }
-    T g1v[2][D0];
+    T gown[2][D0 / 4];
 #pragma unroll
-    for (int G = 0; G < 2; ++G)
-#pragma unroll
-      for (int t = 0; t < D0 / 4; ++t) {
-        if (t < T4) {
-          const T gw = G ? ginv1 : ginv0;
-          g1v[G][4 * t + 0] = quad_bcast<0>(gs[G][t]) * gw;
-          g1v[G][4 * t + 1] = quad_bcast<1>(gs[G][t]) * gw;
-          g1v[G][4 * t + 2] = quad_bcast<2>(gs[G][t]) * gw;
-          g1v[G][4 * t + 3] = quad_bcast<3>(gs[G][t]) * gw;
-        }
+    for (int t = 0; t < D0 / 4; ++t) {
+      if (t < T4) {
+        const T x = ilive ? hown[t] : T(0);
+        gown[0][t] = class4_sum(inG1 ? T(0) : x) * ginv0;
+        gown[1][t] = class4_sum(inG1 ? x : T(0)) * ginv1;
       }
+    }
     T cq[SM::QM];
 #pragma unroll
     for (int q = 0; q < SM::QM; ++q) {
       if (q < Q) {
-        T z = T(0);
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          const int j = 4 * q + s4;
-          T F;
-          if (j < d1) F = hrow[j];
-          else if (j < 3 * d1) F = g1v[(j - d1) / d1][(j - d1) % d1];
-          else F = g2[((l * 2 + (j - 3 * d1) / 4) * N + ic) * 4 + ((j - 3 * d1) & 3)];
-          z += F * convw[j];
-        }
+        T F;
+        if (q < T4) F = hown[q];
+        else if (q < 3 * T4) F = gown[(q - T4) / T4][(q - T4) % T4];
+        else F = g2[((l * 2 + (q - 3 * T4)) * N + ic) * 4 + ff];
+        T z = F * convw[4 * q + ff];
+        z += dpp<0xB1>(z);
+        z += dpp<0x4E>(z);
         cq[q] = f_tanh(z * T(0.25) + convb[q]);
         if (ilive && (q & 3) == ff) cqv[(l * N + ic) * SM::QM + q] = cq[q];
       }

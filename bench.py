@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-walkers", type=int, default=8)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
+    ap.add_argument("--no-ecp", action="store_true", help="skip the C-atom ccECP local-energy side measurement")
     return ap.parse_args()
 
 
@@ -116,6 +117,54 @@ def cpu_baseline(name, params, atoms, charges, nsteps_unused, tstep, sample_walk
                   f"1 Metropolis sweep of {B} walkers ({t_mc:.1f}s) + local energy of {max(1, B // 2)} "
                   f"walkers ({t_el:.1f}s)",
     }
+
+
+def ecp_side_bench(dtype, device, walkers, steps, cpu_baseline_on):
+    """BASELINE.json config 'C atom with ccECP pseudopotential, 4096 walkers, 1xMI355X': complex
+    pp local energy (pphamiltonian.py:177-188) of the whole batch, Philox grid rotations."""
+    sys.path.insert(0, ROOT)
+    from aiqmc import _lib
+    from aiqmc.initial_electrons_positions.init import init_electrons
+    from oracle import pphamiltonian as opp, system as osys
+    s = osys.make_system("C_ecp")
+    t = s.tables()
+    ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
+                       t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"], dtype=dtype,
+                       device=device.index)
+    params = osys.init_params(np.random.default_rng(1), s)
+    ctx.set_params(osys.flatten_params(params))
+    e = opp.c_atom_ccecp()
+    ctx.set_ecp(e.rn_local, e.local_coes, e.local_exps, e.rn_non_local, e.non_local_coes, e.non_local_exps, e.list_l)
+    pos, _ = init_electrons(77, None, s.atoms, s.charges, s.spins, walkers, 1.0)
+    pos = pos.to(device, dtype).contiguous()
+    for k in range(2):
+        ctx.local_energy_ecp(pos, seed=3, offset=k)
+    torch.cuda.synchronize()
+    ctx.profile(True)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        out = ctx.local_energy_ecp(pos, seed=3, offset=100 + k)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ctx.profile(False)
+    q_ms, q_n = ctx.profile_read(_lib.PROF_ECP_QUAD)
+    nq = walkers * s.nelectrons * s.natoms * _lib.ECP_NQ
+    res = {"config": "C atom ccECP (Z_eff=4, 4 e-, list_l=2), complex E_L incl. 50-point nonlocal quadrature",
+           "walkers": walkers, "local_energy_evals_per_s": walkers * steps / dt, "ms_per_eval_batch": 1e3 * dt / steps,
+           "quadrature_configs_per_launch": nq, "quadrature_launch_avg_ms": q_ms / max(q_n, 1),
+           "mean_energy_re": float(out.real.mean()), "finite": bool(torch.isfinite(out.real).all())}
+    if cpu_baseline_on:
+        net = __import__("oracle.network", fromlist=["Network"]).Network(s)
+        pt = __import__("oracle.network", fromlist=["to_torch"]).to_torch(params)
+        rng = np.random.default_rng(9)
+        x = torch.tensor(osys.init_electrons(rng, s.atoms, s.charges, 2, 1.0))
+        rots = opp.haar_rotations(rng, 2)
+        t0 = time.perf_counter()
+        opp.batch_local_energy_pp(net, pt, e, x, rots)
+        tc = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": 2 / tc, "unit": "local-energy evals/s", "cores": torch.get_num_threads(),
+                               "kind": "port", "sample": f"float64 oracle, 2 walkers ({tc:.1f}s)"}
+    return res
 
 
 def main():
@@ -235,6 +284,11 @@ def main():
             "walker_grad_avg_ms": walk_ms / max(walk_n, 1),
             "mean_energy": mean_e, "energy_variance": var_e, "finite": finite,
         }
+        if world == 1 and not args.no_ecp:
+            try:
+                out["ecp_c_atom"] = ecp_side_bench(dtype, dev, 4096, 5, not args.no_cpu_baseline)
+            except Exception as e:  # a side measurement, never a failure of the headline bench
+                out["ecp_c_atom"] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(args.system, params, atoms, charges, args.nsteps, args.tstep,

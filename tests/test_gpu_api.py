@@ -67,3 +67,38 @@ def test_param_update_is_picked_up():
     params["orbitals"][0]["b"] = params["orbitals"][0]["b"] + 0.5
     _, l2 = network.apply(params, data.positions, None, data.atoms, None)
     assert not torch.allclose(l1, l2)
+
+
+def test_pphamiltonian_drop_in_matches_golden(golden_dir):
+    """pphamiltonian.local_energy driven like main_pp_adam_muti_GPU.py:119-148 (C atom ccECP)."""
+    import os
+    from oracle import pphamiltonian as opp, system
+    from aiqmc import spin_indices
+    from aiqmc.Energy import pphamiltonian
+    from aiqmc.wavefunction_Ynlm import nn
+    g = dict(np.load(os.path.join(golden_dir, "C_ecp.npz")))
+    s = system.make_system("C_ecp")
+    par, anti, npar, nanti = spin_indices.jastrow_indices_ee(spins=s.spins, nelectrons=s.nelectrons)
+    up, dn = spin_indices.spin_indices_h(s.spins)
+    network = nn.make_ai_net(ndim=3, nelectrons=4, natoms=1, nspins=(2, 2), determinants=1, charges=s.charges,
+                             parallel_indices=par, antiparallel_indices=anti, n_parallel=npar,
+                             n_antiparallel=nanti, spin_up_indices=up, spin_down_indices=dn)
+    params = system.unflatten_params(system.init_params(np.random.default_rng(0), s), g["params_flat"])
+    e = opp.c_atom_ccecp()
+
+    def log_network(*args, **kwargs):
+        phase, mag = network.apply(*args, **kwargs)
+        return mag + 1.j * phase
+
+    el = pphamiltonian.local_energy(f=network.apply, lognetwork=log_network, charges=s.charges, nspins=s.spins,
+                                    rn_local=e.rn_local, local_coes=e.local_coes, local_exps=e.local_exps,
+                                    rn_non_local=e.rn_non_local, non_local_coes=e.non_local_coes,
+                                    non_local_exps=e.non_local_exps, natoms=1, nelectrons=4, ndim=3, list_l=2)
+    data = nn.AINetData(positions=torch.tensor(g["pos"], device="cuda"), spins=s.spins, atoms=s.atoms,
+                        charges=s.charges)
+    out, mat = el(params, pphamiltonian.HostRotations(torch.tensor(g["rot"])), data)
+    assert mat is None and out.is_complex()
+    assert np.max(np.abs(out.real.cpu().numpy() - g["e_re"])) < 1e-6
+    assert np.max(np.abs(out.imag.cpu().numpy() - g["e_im"])) < 1e-6
+    out2, _ = el(params, 11, data)                      # Philox rotations
+    assert torch.isfinite(out2.real).all()
