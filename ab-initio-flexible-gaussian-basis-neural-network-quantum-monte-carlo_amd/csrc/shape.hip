@@ -202,6 +202,8 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
   if (dtype == AIQMC_F32) {
     if (mode == MODE_LAP)
       k_walker<float, N, A, MODE_LAP><<<dim3(nconf), dim3(64), Smem<float, N, true>::bytes, s>>>(ka);
+    else if (mode == MODE_GRAD && ka.proposal)
+      k_walker_rev<float, N, A, false, true><<<dim3(nconf), dim3(64), SmemRev<float, N, A>::bytes, s>>>(ka);
     else if (mode == MODE_GRAD)
       k_walker_rev<float, N, A><<<dim3(nconf), dim3(64), SmemRev<float, N, A>::bytes, s>>>(ka);
     else
@@ -209,6 +211,8 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
   } else {
     if (mode == MODE_LAP)
       k_walker<double, N, A, MODE_LAP><<<dim3(nconf), dim3(64), Smem<double, N, true>::bytes, s>>>(ka);
+    else if (mode == MODE_GRAD && ka.proposal)
+      k_walker_rev<double, N, A, false, true><<<dim3(nconf), dim3(64), SmemRev<double, N, A>::bytes, s>>>(ka);
     else if (mode == MODE_GRAD)
       k_walker_rev<double, N, A><<<dim3(nconf), dim3(64), SmemRev<double, N, A>::bytes, s>>>(ka);
     else

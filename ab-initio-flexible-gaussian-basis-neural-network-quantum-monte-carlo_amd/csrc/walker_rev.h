@@ -66,8 +66,10 @@ struct SmemRev {
   static constexpr int mx = R + N * N * 2;
   static constexpr int dbar = R;
   static constexpr int R_n = cmax(cmax(4 * N * N, 3 * N * N), 4 + 64 * 12);
-  static constexpr int pv = R + R_n;             // [2N+2] the walker's pivot record (proposals)
-  static constexpr int end = pv + 2 * N + 2;
+  // the walker's pivot record [2N+2] (proposals) lives in the g2 region during F5: the g2
+  // values are dead after F4 and their adjoints are written from B2 on
+  static constexpr int pv = g2;
+  static constexpr int end = R + R_n;
   static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
   static constexpr int hoff(int l) { return l == 0 ? 0 : N * D0; }   // l = 0 or 3
 };
@@ -213,16 +215,20 @@ __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
 // Occupancy hint per instantiation: fp32 N2 (14, 2) lands one VGPR above the
 // 4-waves/SIMD budget (128) without it and fits it without spilling with it.
 // PREP (the adjoint pass of the local energy, walker_lap.h) asks for 2.
-template <typename T, int N, int A, bool PREP> struct RevWaves {
-  static constexpr int value = PREP ? 2 : ((sizeof(T) == 4 && N == 14 && A == 2) ? 4 : 1);
+template <typename T, int N, int A, bool PREP, bool PROP> struct RevWaves {
+  static constexpr int value = PREP ? 2 : ((sizeof(T) == 4 && N == 14 && A == 2) ? (PROP ? 5 : 4) : 1);
 };
 
-// PREP = false: value + gradient (Metropolis walker and proposal launches).
+// PREP = false: value + gradient (Metropolis walker launches and single-electron proposal / ECP
+//   quadrature launches; ka.proposal selects the path at run time).  PROP only selects the
+//   occupancy target of the instantiation: fp32 N2 proposals fit 5 waves/SIMD (90 VGPRs, 8.1 KB
+//   LDS), the walker launch (4096 waves, one round) is faster compiled for 4.  Making the path a
+//   compile-time choice was measured worse: the proposal-only code spilled at the 5-wave budget.
 // PREP = true : first launch of the local energy (walker_lap.h): values, the adjoint pass
 //   through the h stream, and the pair stream's derivative sums and curvature, written to
 //   the walker's LapCache; no gradient (B3/B4) and no Metropolis cache.
-template <typename T, int N, int A, bool PREP = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, N, A, PREP>::value))) void
+template <typename T, int N, int A, bool PREP = false, bool PROP = false>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, N, A, PREP, PROP>::value))) void
 k_walker_rev(KArgs ka) {
   using Ly = Lay<N, A>;
   using SM = SmemRev<T, N, A>;
@@ -285,6 +291,7 @@ k_walker_rev(KArgs ka) {
   T* Yv = sm + SM::yv;
   T* g2 = sm + SM::g2;
   T jv = T(0), jd1 = T(0), jve = T(0);
+  T pvr = T(0);
   if (reuse) {
     // walker pb's cached stage and pair sums, electron pi's entries from k_moved_electron;
     // all loads issued before the first LDS store
@@ -310,7 +317,7 @@ k_walker_rev(KArgs ka) {
     jv = (val && live) ? ((er == pi) ? Eq[EC::jv] : Wc[WC::jaev + er]) : T(0);
     jd1 = dir ? ((le == pi) ? Eq[EC::jd + lc] : Wc[WC::jaed + lane]) : T(0);
     jve = lane == 0 ? Wc[WC::jee] : T(0);
-    if (lane < 2 * N + 2) sm[SM::pv + lane] = Wc[WC::pv + lane];
+    pvr = lane < 2 * N + 2 ? Wc[WC::pv + lane] : T(0);   // to LDS after F4 (SmemRev::pv)
 #pragma unroll
     for (int t = 0; t < NY; ++t)
       if (lane + 64 * t < N * N) Yv[lane + 64 * t] = ry[t];
@@ -549,6 +556,7 @@ k_walker_rev(KArgs ka) {
   }
   if (ilive) hl[SM::hoff(3) + ic * 4 + ff] = hreg;
   __syncthreads();
+  if (reuse && lane < 2 * N + 2) sm[SM::pv + lane] = pvr;   // read by the Gauss-Jordan after the Phi barrier
 
   AQ_PH(3);
   // ------------------------------------------------------------------ F5 Phi, A = Phi * Yt, Gauss-Jordan -> B = A^{-1}

@@ -278,7 +278,7 @@ def main():
                 "flop_per_launch": flop_prop,
                 "flop_model": "B*N*3*F_fwd, F_fwd=4.9e4 (SURVEY 8d)"},
             "roofline_local_energy": {
-                "kernel": "k_walker<float,14,2,LAP>", "achieved": achieved_el, "peak": peak, "unit": "TFLOP/s",
+                "kernel": "k_walker_rev<float,14,2,PREP> + k_walker_lap<float,14,2> (local energy, 2 launches)", "achieved": achieved_el, "peak": peak, "unit": "TFLOP/s",
                 "frac": (achieved_el / peak) if achieved_el else None, "avg_launch_ms": lap_avg_ms,
                 "launches": lap_n, "flop_model": "B*2.55e6 (SURVEY 8d)"},
             "walker_grad_avg_ms": walk_ms / max(walk_n, 1),
