@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_workspace_bytes", "aiqmc_last_error", "aiqmc_supported_shapes",
     "aiqmc_profile_enable", "aiqmc_profile_read", "aiqmc_debug_logpsi_grad_forward",
     "aiqmc_debug_set_proposal_reuse", "aiqmc_debug_phase_cycles", "aiqmc_debug_local_energy_forward",
-    "aiqmc_set_ecp", "aiqmc_local_energy_ecp",
+    "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -108,6 +108,7 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_debug_set_proposal_reuse.restype = ctypes.c_int
     lib.aiqmc_debug_phase_cycles.argtypes = [vp, vp]
     lib.aiqmc_debug_phase_cycles.restype = ctypes.c_int
+    lib.aiqmc_logpsi_param_grad.argtypes = [vp, vp, i32, vp, vp, vp, vp]
     lib.aiqmc_set_ecp.argtypes = [vp, ctypes.POINTER(AiqmcEcp)]
     lib.aiqmc_local_energy_ecp.argtypes = [vp, vp, i32, i32, vp, ctypes.c_uint64, ctypes.c_uint64, vp, vp, vp,
                                            vp, vp]
@@ -117,7 +118,7 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_supported_shapes.restype = ctypes.c_char_p
     for name in ("aiqmc_create", "aiqmc_destroy", "aiqmc_set_params", "aiqmc_logpsi",
                  "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_mc_step", "aiqmc_profile_enable",
-                 "aiqmc_profile_read", "aiqmc_set_ecp", "aiqmc_local_energy_ecp"):
+                 "aiqmc_profile_read", "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib
@@ -298,6 +299,25 @@ class Context:
         check(self._lib.aiqmc_debug_local_energy_forward(self._h, _ptr(p), B, _ptr(el), _ptr(logabs), _ptr(grad),
                                                          _stream(self.device)), "aiqmc_debug_local_energy_forward")
         return el, logabs, grad
+
+    def logpsi_param_grad(self, pos: torch.Tensor, weights: Optional[torch.Tensor] = None,
+                          want_logabs: bool = False):
+        """d log|psi| / d theta in canonical (tree_flatten) order: [B, P] per walker, or [P] =
+        sum_b weights[b] d log|psi_b| / d theta when weights [B] are given."""
+        p = self._pos(pos)
+        B = p.shape[0]
+        w = None
+        if weights is not None:
+            w = weights.to(self.device, self.dtype).contiguous()
+            if w.numel() != B:
+                raise ValueError("weights must have one entry per walker")
+            out = torch.empty(self.nparams, dtype=self.dtype, device=self.device)
+        else:
+            out = torch.empty(B, self.nparams, dtype=self.dtype, device=self.device)
+        la = torch.empty(B, dtype=self.dtype, device=self.device) if want_logabs else None
+        check(self._lib.aiqmc_logpsi_param_grad(self._h, _ptr(p), B, _ptr(w), _ptr(out), _ptr(la),
+                                                _stream(self.device)), "aiqmc_logpsi_param_grad")
+        return (out, la) if want_logabs else out
 
     def set_ecp(self, rn_local, local_coes, local_exps, rn_non_local, non_local_coes, non_local_exps,
                 list_l: int):

@@ -17,6 +17,7 @@
 #include "aiqmc.h"
 #include "ctx.h"
 #include "ecp.h"
+#include "walker_pgrad.h"
 
 using namespace aq;
 
@@ -293,6 +294,9 @@ int aiqmc_destroy(aiqmc_ctx* c) {
   free_ws(c);
   free_ecp_ws(c);
   if (c->d_ecp_tab) (void)hipFree(c->d_ecp_tab);
+  void* pgp[] = {c->d_gmap, c->d_wnorm, c->d_pg, c->d_pgr};
+  for (void* p : pgp)
+    if (p) (void)hipFree(p);
   if (c->d_wcp) (void)hipFree(c->d_wcp);
   if (c->d_lc) (void)hipFree(c->d_lc);
   for (auto& v : c->ev_used)
@@ -330,6 +334,20 @@ int aiqmc_set_params(aiqmc_ctx* c, const double* flat, int64_t n, void* stream) 
     HIPCHK(hipMemcpyAsync(c->d_prm, lay.data(), lay.size() * 8, hipMemcpyHostToDevice, s));
     HIPCHK(hipStreamSynchronize(s));
   }
+  // |W_y row| (the y coefficients are the last 6N canonical entries, nn.py:449-451), for the
+  // canonical parameter gradient
+  double wn[NYW];
+  for (int m = 0; m < NYW; ++m) {
+    double a = 0.0;
+    for (int col = 0; col < c->N; ++col) {
+      const double w = flat[n - NYW * c->N + m * c->N + col];
+      a += w * w;
+    }
+    wn[m] = std::sqrt(a);
+  }
+  if (!c->d_wnorm) HIPCHK(hipMalloc((void**)&c->d_wnorm, NYW * sizeof(double)));
+  HIPCHK(hipMemcpyAsync(c->d_wnorm, wn, sizeof(wn), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
   c->params_set = true;
   return AIQMC_OK;
 }
@@ -535,6 +553,67 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
     ops.accept(c->dtype, pos, c->d_grad, c->d_gown, c->d_lp, c->d_lpn, g1, g2, uu, c->d_taueff, B, tstep,
                accept_out, s);
   }
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_logpsi_param_grad(aiqmc_ctx* c, const void* pos, int32_t B, const void* weights, void* out,
+                            void* logabs, void* stream) {
+  int rc = check_call(c, pos, B);
+  if (rc) return rc;
+  if (!out) return fail(AIQMC_EINVAL, "null out");
+  if (B == 0) return AIQMC_OK;
+  HIPCHK(hipSetDevice(c->device));
+  ShapeOps ops;
+  shape_ops(c->N, c->A, &ops);
+  const size_t es = c->dtype == AIQMC_F32 ? 4 : 8;
+  if (!c->d_gmap) {
+    std::vector<int> map;
+    ops.gmap(c, map);
+    if ((int64_t)map.size() != c->ncanon) return fail(AIQMC_EINVAL, "internal: gradient map size");
+    HIPCHK(hipMalloc((void**)&c->d_gmap, map.size() * sizeof(int)));
+    HIPCHK(hipMemcpy(c->d_gmap, map.data(), map.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
+  if (c->pg_B < B) {
+    if (c->d_pg) (void)hipFree(c->d_pg);
+    if (c->d_pgr) (void)hipFree(c->d_pgr);
+    c->d_pg = c->d_pgr = nullptr;
+    c->pg_B = 0;
+    HIPCHK(hipMalloc(&c->d_pg, (size_t)B * c->nkern * es));
+    HIPCHK(hipMalloc(&c->d_pgr, (size_t)c->nkern * es));
+    c->pg_B = B;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  KArgs ka = base_args(c);
+  ka.nconf = B;
+  ka.pos = pos;
+  ka.grad = c->d_pg;
+  ka.logabs = logabs;
+  rc = ops.pgrad(c->dtype, ka, B, s);
+  if (rc) return rc;
+  const int nk = (int)c->nkern, nc = (int)c->ncanon;
+  const void* G = c->d_pg;
+  int rows = B;
+  if (weights) {
+    if (c->dtype == AIQMC_F32)
+      k_grad_reduce<float><<<dim3((nk + 63) / 64), dim3(256), 0, s>>>((const float*)c->d_pg, (const float*)weights, B,
+                                                                     nk, (float*)c->d_pgr);
+    else
+      k_grad_reduce<double><<<dim3((nk + 63) / 64), dim3(256), 0, s>>>((const double*)c->d_pg, (const double*)weights,
+                                                                      B, nk, (double*)c->d_pgr);
+    G = c->d_pgr;
+    rows = 1;
+  }
+  const size_t nt = (size_t)rows * nc;
+  const int nb = (int)((nt + 255) / 256);
+  if (c->dtype == AIQMC_F32)
+    k_grad_canon<float><<<dim3(nb), dim3(256), 0, s>>>((const float*)G, nk, c->d_gmap, nc,
+                                                        (const float*)c->d_prm + ops.wy_off, ops.wy_off, c->d_wnorm,
+                                                        c->N, rows, (float*)out);
+  else
+    k_grad_canon<double><<<dim3(nb), dim3(256), 0, s>>>((const double*)G, nk, c->d_gmap, nc,
+                                                         (const double*)c->d_prm + ops.wy_off, ops.wy_off,
+                                                         c->d_wnorm, c->N, rows, (double*)out);
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
 }

@@ -47,6 +47,12 @@ struct aiqmc_ctx {
   void *d_ecp_rot = nullptr, *d_ecp_x = nullptr, *d_ecp_lq = nullptr, *d_ecp_pq = nullptr, *d_ecp_ec = nullptr,
        *d_ecp_el = nullptr, *d_ecp_lp0 = nullptr, *d_ecp_ph0 = nullptr;
   int64_t ecp_bytes = 0;
+  // parameter gradients (aiqmc_logpsi_param_grad, walker_pgrad.h)
+  int* d_gmap = nullptr;            // [ncanon]
+  double* d_wnorm = nullptr;        // [6] |W_y row| of the current parameters
+  void* d_pg = nullptr;             // [pg_B][nkern] per-walker kernel-layout gradients
+  void* d_pgr = nullptr;            // [nkern] weighted sum
+  int pg_B = 0;
   // optional per-kernel HIP-event timing (aiqmc_profile_*): slot -> recorded (start, stop) pairs
   bool prof = false;
   std::vector<hipEvent_t> ev_free;
@@ -68,6 +74,9 @@ struct ShapeOps {
   int64_t nkern;
   long (*ncanon)(int npar, int nanti);
   void (*pack)(const aiqmc_ctx* c, const double* flat, std::vector<double>& out);
+  void (*gmap)(const aiqmc_ctx* c, std::vector<int>& map);                        // canonical -> kernel index
+  int (*pgrad)(int dtype, const KArgs& ka, int nconf, hipStream_t s);            // k_param_grad
+  int wy_off;                                                                      // Lay::wy
 };
 
 

@@ -7,6 +7,7 @@
 
 #include "ctx.h"
 #include "walker_lap.h"
+#include "walker_pgrad.h"
 
 using namespace aq;
 
@@ -179,6 +180,67 @@ static void pack_params(const aiqmc_ctx* c, const double* flat, std::vector<doub
   out[Ly::vnn] = vnn;
 }
 
+// Canonical (tree_flatten) index -> kernel-layout index of the same parameter, the transpose of
+// pack_params (see k_grad_canon for the -1 / <= -2 codes).
+template <int N, int A>
+static void gmap_impl(const aiqmc_ctx* c, std::vector<int>& map) {
+  using Ly = Lay<N, A>;
+  map.clear();
+  auto put = [&](int k) { map.push_back(k); };
+  for (int i = 0; i < N; ++i) {
+    put(Ly::env_alpha + i);
+    for (int a = 0; a < A; ++a) put(Ly::env_beta + i * A + a);
+    for (int k = 0; k < 3 * A; ++k) put(-1);   // eplion
+    for (int k = 0; k < A; ++k) put(-1);       // mu
+    for (int k = 0; k < A; ++k) put(-1);       // nu
+    for (int k = 0; k < 3 * A; ++k) put(Ly::env_pi + i * A * 3 + k);
+    for (int k = 0; k < 3 * A; ++k) put(Ly::env_sigma + i * A * 3 + k);
+    put(Ly::env_xi + i);
+  }
+  for (int k = 0; k < N * A; ++k) put(Ly::jae_b + k);
+  auto pairs = [&](const std::vector<int>& t, int n) {
+    for (int q = 0; q < n; ++q) {
+      const int i = t[q], j = t[n + q];
+      put(Ly::jee_a + (i < j ? i * N + j : j * N + i));
+    }
+  };
+  pairs(c->anti, c->nanti);
+  pairs(c->par, c->npar);
+  const int D[3] = {Ly::D0, Ly::D1, Ly::D1};
+  const int Q[3] = {Ly::Q0, Ly::Q1, Ly::Q1};
+  const int cw[3] = {Ly::conv_w0, Ly::conv_w1, Ly::conv_w2};
+  const int cb[3] = {Ly::conv_b0, Ly::conv_b1, Ly::conv_b2};
+  const int sw[3] = {Ly::sng_w0, Ly::sng_w1, Ly::sng_w2};
+  const int sb[3] = {Ly::sng_b0, Ly::sng_b1, Ly::sng_b2};
+  const int dw[2] = {Ly::dbl_w0, Ly::dbl_w1};
+  const int db[2] = {Ly::dbl_b0, Ly::dbl_b1};
+  for (int l = 0; l < 3; ++l) {
+    for (int k = 0; k < N * Q[l]; ++k) put(cb[l] + k);
+    for (int k = 0; k < N * D[l]; ++k) put(cw[l] + k);
+    if (l < 2) {
+      for (int k = 0; k < NH2; ++k) put(db[l] + k);
+      for (int k = 0; k < NH2 * NH2; ++k) put(dw[l] + k);
+    }
+    for (int k = 0; k < NH; ++k) put(sb[l] + k);
+    for (int k = 0; k < Q[l] * NH; ++k) put(sw[l] + k);
+  }
+  const int yin[3] = {Ly::DY0, NYW, NYW};
+  const int yw[3] = {Ly::y_w0, Ly::y_w1, Ly::y_w2};
+  const int yb[3] = {Ly::y_b0, Ly::y_b1, Ly::y_b2};
+  for (int l = 0; l < 3; ++l) {
+    for (int k = 0; k < NYW; ++k) put(yb[l] + k);
+    for (int k = 0; k < yin[l] * NYW; ++k) put(yw[l] + k);
+  }
+  for (int sp = 0; sp < 2; ++sp) {
+    for (int k = 0; k < 2 * N; ++k) put(Ly::orb_b + (sp * N + k / 2) * 2 + (k & 1));
+    for (int k = 0; k < NH * 2 * N; ++k) {
+      const int f = k / (2 * N), r = k - f * 2 * N;
+      put(Ly::orb_w + ((sp * NH + f) * N + r / 2) * 2 + (r & 1));
+    }
+  }
+  for (int k = 0; k < NYW * N; ++k) put(-2 - k);
+}
+
 template <int N, int A>
 static int set_lds_impl() {
   const int sizes[6] = {Smem<float, N, false>::bytes,  Smem<float, N, true>::bytes,  Smem<double, N, false>::bytes,
@@ -254,6 +316,29 @@ static void accept_impl(int dtype, void* pos, const void* grad, const void* gown
 }
 
 
+// per-walker parameter gradients in the kernel layout: out [nconf][Lay::total]
+template <int N, int A>
+static int pgrad_impl(int dtype, const KArgs& ka, int nconf, hipStream_t s) {
+  if (dtype == AIQMC_F32) {
+    constexpr int bytes = SmemPG<float, N, A>::bytes;
+    if (bytes > 65536) {
+      hipError_t e = hipFuncSetAttribute((const void*)&k_param_grad<float, N, A>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+      if (e != hipSuccess) return fail(AIQMC_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+    }
+    k_param_grad<float, N, A><<<dim3(nconf), dim3(64), bytes, s>>>(ka);
+  } else {
+    constexpr int bytes = SmemPG<double, N, A>::bytes;
+    if (bytes > 65536) {
+      hipError_t e = hipFuncSetAttribute((const void*)&k_param_grad<double, N, A>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+      if (e != hipSuccess) return fail(AIQMC_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+    }
+    k_param_grad<double, N, A><<<dim3(nconf), dim3(64), bytes, s>>>(ka);
+  }
+  return 0;
+}
+
 static void phase_read_impl(unsigned long long* out) {
 #ifdef AQ_PHASE_PROF
   (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(aq_phase_cycles), 32 * sizeof(unsigned long long));
@@ -279,5 +364,8 @@ bool AQ_CAT(AQ_N, AQ_A)(ShapeOps* ops) {
   ops->nkern = Lay<AQ_N, AQ_A>::total;
   ops->ncanon = &Lay<AQ_N, AQ_A>::canon;
   ops->pack = &pack_params<AQ_N, AQ_A>;
+  ops->gmap = &gmap_impl<AQ_N, AQ_A>;
+  ops->pgrad = &pgrad_impl<AQ_N, AQ_A>;
+  ops->wy_off = Lay<AQ_N, AQ_A>::wy;
   return true;
 }

@@ -1,0 +1,569 @@
+// walker_pgrad.h -- per-walker parameter gradient O_b = d log|psi(x_b)| / d theta of the
+// AIQMC network (the psi_tangent of the energy-gradient custom JVP,
+// Loss/loss.py:242-265, and of the Adam step, Optimizer/adam.py:49-59).
+//
+// One wave per walker; not on the Metropolis hot path (one launch per optimisation step), so
+// the kernel favours clarity: a plain forward pass with every intermediate kept in LDS
+// (lanes over items: electrons, pairs, (electron, unit), (row, column)), Gauss-Jordan of
+// gj.h, then the reverse pass with the parameter adjoints accumulated in an LDS copy of the
+// kernel parameter layout (Lay<N,A>) by LDS atomics and written out per walker.
+//
+// Adjoints (L = log|det A| + J_ee + J_ae, Q11; B = A^{-1}, A = Phi (.) Yt):
+//   dL/dPhi_re[r,c] = Re B[c,r] Yt[r,c],  dL/dPhi_im[r,c] = -Im B[c,r] Yt[r,c],
+//   dL/dYt[r,c] = Re(B[c,r] Phi[r,c]);  Phi[r,:] = H[src r,:] W_s + b_s  (nn.py:432-456);
+//   Yt[r,c] = env_r sum_m y[r,m] What[m,c]  (What = row-normalised W_y, nn.py:449-452: the
+//   normalisation is undone on the canonical side, aiqmc_logpsi_param_grad);
+//   h stream (nn.py:280-311, network_blocks.py:106-116), pair stream (nn.py:305-309),
+//   Ynlm stream (nn.py:313-341), envelope (envelope.py:26-30), Pade Jastrows (Jastrow.py).
+#pragma once
+#include "electron.h"
+#include "gj.h"
+#include "jets.h"
+#include "layout.h"
+#include "walker_kernel.h"
+
+namespace aq {
+
+template <typename T, int N, int A>
+struct SmemPG {
+  static constexpr int D0 = 4 * A;
+  static constexpr int DFM = 3 * D0 + 2 * NH2;
+  static constexpr int QM = DFM / 4;
+  static constexpr int xs = 0;                            // [48]
+  static constexpr int pg = 48;                           // [Lay::total] d L / d (kernel parameter)
+  static constexpr int hl = pg + Lay<N, A>::total;        // [4][N][D0] h^0..h^3 (h^l width D0 for l = 0, 4 after)
+  static constexpr int g1 = hl + 4 * N * D0;              // [3][2][D0] group means of h^l
+  static constexpr int g2 = g1 + 6 * D0;                  // [3][2][N][4] column means of h2^(l)
+  static constexpr int cq = g2 + 24 * N;                  // [3][N][QM] conv outputs
+  static constexpr int sv = cq + 3 * N * QM;              // [3][N][4] single outputs
+  static constexpr int env = sv + 12 * N;                 // [N] envelope of row r
+  static constexpr int yst = env + N;                     // [N][6] Ynlm stream output
+  static constexpr int yv = yst + NYW * N;                // [N][N] Yt
+  static constexpr int ph = yv + N * N;                   // [N][N][2] Phi
+  static constexpr int mx = ph + 2 * N * N;               // [N][N][2] B = A^{-1}
+  static constexpr int hb = mx + 2 * N * N;               // [N][4] adjoint of h^{l+1}
+  static constexpr int hn = hb + 4 * N;                   // [N][4] adjoint of h^l
+  static constexpr int g2b = hn + 4 * N;                  // [3][2][N][4] adjoints of g2
+  static constexpr int ybar = g2b + 24 * N;               // [N][N] adjoint of Yt
+  static constexpr int fb = ybar + N * N;                 // [N][DFM] adjoints of the conv inputs
+  static constexpr int zc = fb + N * DFM;                 // [N][QM] conv pre-activation adjoints
+  static constexpr int zs = zc + N * QM;                  // [N][4]  single pre-activation adjoints
+  static constexpr int red = zs + 4 * N;                  // [2] J sums
+  static constexpr int end = red + 2;
+  static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
+  static constexpr int hoff(int l) { return l * N * D0; }
+};
+
+template <typename T> __device__ __forceinline__ void lds_add(T* p, T v) { atomicAdd(p, v); }
+
+template <typename T, int N, int A>
+__global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
+  using Ly = Lay<N, A>;
+  using SM = SmemPG<T, N, A>;
+  constexpr int D0 = SM::D0;
+  constexpr int QM = SM::QM;
+  const cptr<T> P = param_ptr<T>(ka.prm);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  T* sm = (T*)smem_raw;
+  T* xs = sm + SM::xs;
+  T* pg = sm + SM::pg;
+  const int conf = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int nup = ka.nup;
+  const T gw[2] = {T(1) / T(nup), T(1) / T(N - nup)};
+  const T RSQ2 = T(0.70710678118654752);
+  const int* rowsrc = ka.rowsrc;
+
+  if (lane < 3 * N) xs[lane] = ((const T*)ka.pos)[(size_t)conf * 3 * N + lane];
+  for (int idx = lane; idx < Ly::total; idx += 64) pg[idx] = T(0);
+  for (int idx = lane; idx < 24 * N; idx += 64) sm[SM::g2 + idx] = T(0);
+  if (lane < 2) sm[SM::red + lane] = T(0);
+  __syncthreads();
+
+  // ---------------------------------------------------------------- forward: electron stage
+  T jae_v = T(0);
+  if (lane < N) {
+    ElecOut<T, A> eo;
+    electron_stage<T, N, A>(P, xs + 3 * lane, lane, 3, eo);
+#pragma unroll
+    for (int m = 0; m < D0; ++m) sm[SM::hl + lane * D0 + m] = eo.hf[m].v;
+#pragma unroll
+    for (int m = 0; m < NYW; ++m) sm[SM::yst + lane * NYW + m] = eo.yst[m].v;
+    sm[SM::env + lane] = eo.env.v;
+    for (int c = 0; c < N; ++c) {
+      T y = T(0);
+#pragma unroll
+      for (int m = 0; m < NYW; ++m) y += eo.yst[m].v * P[Ly::wy + m * N + c];
+      sm[SM::yv + lane * N + c] = eo.env.v * y;
+    }
+    jae_v = eo.jae.v;
+  }
+  // ---------------------------------------------------------------- forward: pair stream column means
+  T jee_v = T(0);
+  for (int idx = lane; idx < N * N; idx += 64) {
+    const int k = idx / N, i = idx - k * N;
+    const bool diag = k == i;
+    T d[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) d[c] = xs[3 * i + c] - xs[3 * k + c];
+    const T r = f_sqrt(diag ? T(1) : d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    T p[4] = {diag ? T(0) : r, diag ? T(0) : d[0], diag ? T(0) : d[1], diag ? T(0) : d[2]};
+    if (k < i) jee_v += f_div(P[Ly::jee_c + k * N + i] * r, P[Ly::jee_a + k * N + i] * r + T(1));
+    const int G = k >= nup ? 1 : 0;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) lds_add(&sm[SM::g2 + ((0 * 2 + G) * N + i) * 4 + f], p[f] * gw[G]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const cptr<T> dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
+      const cptr<T> db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
+      T q[4];
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        T s = db[o];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) s += p[m] * dw[m * 4 + o];
+        q[o] = f_tanh(s);
+      }
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        p[o] = (p[o] + q[o]) * RSQ2;
+        lds_add(&sm[SM::g2 + (((j + 1) * 2 + G) * N + i) * 4 + o], p[o] * gw[G]);
+      }
+    }
+  }
+  __syncthreads();
+  // ---------------------------------------------------------------- forward: h stream (nn.py:280-311)
+#pragma unroll
+  for (int l = 0; l < 3; ++l) {
+    const int d = l == 0 ? D0 : NH;
+    const int DF = 3 * d + 2 * NH2, Q = DF / 4;
+    const T* h = sm + SM::hl + SM::hoff(l);
+    T* g1 = sm + SM::g1 + l * 2 * D0;
+    if (lane < 2 * d) {
+      const int G = lane / d, m = lane - G * d;
+      T s = T(0);
+      for (int k = (G ? nup : 0); k < (G ? N : nup); ++k) s += h[k * d + m];
+      g1[G * D0 + m] = s * gw[G];
+    }
+    __syncthreads();
+    const cptr<T> convw = P + (l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2));
+    const cptr<T> convb = P + (l == 0 ? Ly::conv_b0 : (l == 1 ? Ly::conv_b1 : Ly::conv_b2));
+    for (int idx = lane; idx < N * Q; idx += 64) {
+      const int i = idx / Q, q = idx - i * Q;
+      T z = T(0);
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int j = 4 * q + s4;
+        T F;
+        if (j < d) F = h[i * d + j];
+        else if (j < 3 * d) F = g1[((j - d) / d) * D0 + (j - d) % d];
+        else F = sm[SM::g2 + ((l * 2 + (j - 3 * d) / 4) * N + i) * 4 + ((j - 3 * d) & 3)];
+        z += F * convw[i * DF + j];
+      }
+      sm[SM::cq + (l * N + i) * QM + q] = f_tanh(z * T(0.25) + convb[i * Q + q]);
+    }
+    __syncthreads();
+    const cptr<T> sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
+    const cptr<T> sngb = P + (l == 0 ? Ly::sng_b0 : (l == 1 ? Ly::sng_b1 : Ly::sng_b2));
+    for (int idx = lane; idx < N * NH; idx += 64) {
+      const int i = idx / NH, f = idx - i * NH;
+      T z = sngb[f];
+      for (int q = 0; q < Q; ++q) z += sm[SM::cq + (l * N + i) * QM + q] * sngw[q * NH + f];
+      const T s = f_tanh(z);
+      sm[SM::sv + (l * N + i) * NH + f] = s;
+      sm[SM::hl + SM::hoff(l + 1) + i * NH + f] = (d == NH) ? (h[i * d + f] + s) * RSQ2 : s;
+    }
+    __syncthreads();
+  }
+  // ---------------------------------------------------------------- forward: Phi, Gauss-Jordan (nn.py:432-506)
+  T* Ph = sm + SM::ph;
+  T* Mx = sm + SM::mx;
+  T* Yv = sm + SM::yv;
+  const T* H3 = sm + SM::hl + SM::hoff(3);
+  for (int idx = lane; idx < N * N; idx += 64) {
+    const int r = idx / N, c = idx - r * N;
+    const int src = rowsrc[r], s = r < nup ? 0 : 1;
+    T re = P[Ly::orb_b + (s * N + c) * 2], im = P[Ly::orb_b + (s * N + c) * 2 + 1];
+#pragma unroll
+    for (int f = 0; f < NH; ++f) {
+      re += H3[src * NH + f] * P[Ly::orb_w + ((s * NH + f) * N + c) * 2];
+      im += H3[src * NH + f] * P[Ly::orb_w + ((s * NH + f) * N + c) * 2 + 1];
+    }
+    Ph[idx * 2] = re;
+    Ph[idx * 2 + 1] = im;
+  }
+  __syncthreads();
+  T logdet, phr, phi;
+  gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi);
+  __syncthreads();
+  // ---------------------------------------------------------------- reverse: orbitals (B1)
+  T* ybar = sm + SM::ybar;
+  T* hb = sm + SM::hb;
+  for (int idx = lane; idx < N * N; idx += 64) {
+    const int r = idx / N, c = idx - r * N;
+    const int src = rowsrc[r], s = r < nup ? 0 : 1;
+    const T br = Mx[(c * N + r) * 2], bi = Mx[(c * N + r) * 2 + 1];
+    const T yt = Yv[idx];
+    const T pr_ = br * yt, pi_ = -bi * yt;          // dL/dPhi_re, dL/dPhi_im
+    ybar[idx] = br * Ph[idx * 2] - bi * Ph[idx * 2 + 1];
+    lds_add(&pg[Ly::orb_b + (s * N + c) * 2], pr_);
+    lds_add(&pg[Ly::orb_b + (s * N + c) * 2 + 1], pi_);
+#pragma unroll
+    for (int f = 0; f < NH; ++f) {
+      lds_add(&pg[Ly::orb_w + ((s * NH + f) * N + c) * 2], H3[src * NH + f] * pr_);
+      lds_add(&pg[Ly::orb_w + ((s * NH + f) * N + c) * 2 + 1], H3[src * NH + f] * pi_);
+    }
+  }
+  for (int idx = lane; idx < N * NH; idx += 64) {
+    const int r = idx / NH, f = idx - r * NH;
+    const int s = r < nup ? 0 : 1;
+    T a = T(0);
+    for (int c = 0; c < N; ++c) {
+      const T br = Mx[(c * N + r) * 2], bi = Mx[(c * N + r) * 2 + 1];
+      const T yt = Yv[r * N + c];
+      a += P[Ly::orb_w + ((s * NH + f) * N + c) * 2] * br * yt - P[Ly::orb_w + ((s * NH + f) * N + c) * 2 + 1] * bi * yt;
+    }
+    hb[rowsrc[r] * NH + f] = a;
+  }
+  __syncthreads();
+  // ---------------------------------------------------------------- reverse: per electron (Yt row, envelope,
+  // e-n Jastrow, Ynlm stream), one lane per electron
+  if (lane < N) {
+    const int i = lane;
+    const T env = sm[SM::env + i];
+    T ystb[NYW];
+    T envb = T(0);
+#pragma unroll
+    for (int m = 0; m < NYW; ++m) ystb[m] = T(0);
+    for (int c = 0; c < N; ++c) {
+      const T yb = ybar[i * N + c];
+      T y = T(0);
+#pragma unroll
+      for (int m = 0; m < NYW; ++m) {
+        const T w = P[Ly::wy + m * N + c];
+        y += sm[SM::yst + i * NYW + m] * w;
+        ystb[m] += env * w * yb;
+        lds_add(&pg[Ly::wy + m * N + c], env * sm[SM::yst + i * NYW + m] * yb);
+      }
+      envb += yb * y;
+    }
+    // geometry of electron i
+    T ae[A][3], ra[A];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) ae[a][c] = xs[3 * i + c] - P[Ly::atoms + a * 3 + c];
+      ra[a] = f_sqrt(ae[a][0] * ae[a][0] + ae[a][1] * ae[a][1] + ae[a][2] * ae[a][2]);
+    }
+    // envelope.py:26-30: env = alpha sum_a e^{-beta r^2} + xi sum_{a,d} sigma e^{-pi ae}
+    const T alpha = P[Ly::env_alpha + i], xi = P[Ly::env_xi + i];
+    T da = T(0), dxi = T(0);
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      const T beta = P[Ly::env_beta + i * A + a];
+      const T e = f_exp(-beta * ra[a] * ra[a]);
+      da += e;
+      pg[Ly::env_beta + i * A + a] += envb * (-alpha * ra[a] * ra[a] * e);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const T pi_ = P[Ly::env_pi + (i * A + a) * 3 + c], sg = P[Ly::env_sigma + (i * A + a) * 3 + c];
+        const T e2 = f_exp(-pi_ * ae[a][c]);
+        dxi += sg * e2;
+        pg[Ly::env_sigma + (i * A + a) * 3 + c] += envb * xi * e2;
+        pg[Ly::env_pi + (i * A + a) * 3 + c] += envb * (-xi * sg * ae[a][c] * e2);
+      }
+      // Jastrow.py:84-93: ja = -c34 / (2 beta) (1 - e^{-c14 beta r})
+      const T bj = P[Ly::jae_b + i * A + a];
+      const T c34 = P[Ly::c34 + a], c14 = P[Ly::c14 + a];
+      const T ex = f_exp(-c14 * bj * ra[a]);
+      pg[Ly::jae_b + i * A + a] += c34 / (T(2) * bj * bj) * (T(1) - ex) - c34 / (T(2) * bj) * (c14 * ra[a] * ex);
+    }
+    pg[Ly::env_alpha + i] += envb * da;
+    pg[Ly::env_xi + i] += envb * dxi;
+    // Ynlm stream: recompute the three layers of electron i, then reverse (nn.py:313-341)
+    constexpr int DY0 = Ly::DY0;
+    T y0[DY0];
+    {
+      // input features (nn.py:156-193, the electron stage's formulas, values only)
+      const T PI = T(3.141592653589793);
+      const T c0 = T(0.5) * f_sqrt(T(1) / PI), c1 = f_sqrt(T(3) / (T(4) * PI));
+      const T k15h = T(0.5) * f_sqrt(T(15) / PI), k5q = T(0.25) * f_sqrt(T(5) / PI);
+      const T k15q = T(0.25) * f_sqrt(T(15) / PI), k35 = T(0.25) * f_sqrt(T(35) / (T(2) * PI));
+      const T k105h = T(0.5) * f_sqrt(T(105) / PI), k21 = T(0.25) * f_sqrt(T(21) / (T(2) * PI));
+      const T k7 = T(0.25) * f_sqrt(T(7) / PI), k105q = T(0.25) * f_sqrt(T(105) / PI);
+      T hisum = T(0), spsum = T(0);
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        const T rinv = T(1) / ra[a];
+        const T x0 = ae[a][0] * rinv, x1 = ae[a][1] * rinv, x2 = ae[a][2] * rinv;
+        y0[4 * a] = c0;
+        y0[4 * a + 1] = c1 * x0;
+        y0[4 * a + 2] = c1 * x1;
+        y0[4 * a + 3] = c1 * x2;
+        spsum += c0 + c1 * x0 + c1 * x1 + c1 * x2;
+        const T y2 = ra[a] * ra[a], inv2 = rinv * rinv, inv3 = inv2 * rinv;
+        const T x00 = x0 * x0, x11 = x1 * x1, x22 = x2 * x2, x01 = x0 * x1;
+        const T s2 = k15h * x01 + k15h * (x1 * x2) + k5q * (T(3) * x22 - y2) + k15h * (x0 * x2) + k15q * (x00 - x11);
+        const T f5 = T(5) * x22 - y2;
+        const T s3 = k35 * (x1 * (T(3) * x00 - x11)) + k105h * (x01 * x2) + k21 * (x1 * f5) +
+                     k7 * (x2 * (T(5) * x22 - T(3) * y2)) + k21 * (x0 * f5) + k105q * ((x00 - x11) * x2) +
+                     k35 * (x0 * (x00 - T(3) * x11));
+        hisum += s2 * inv2 + s3 * inv3;
+      }
+      y0[4 * A] = hisum * (T(1) / T(12 * A));
+      y0[4 * A + 1] = spsum * (T(1) / T(4 * A));
+    }
+    T t0[NYW], y1[NYW], t1[NYW], y2[NYW], t2[NYW];
+#pragma unroll
+    for (int q = 0; q < NYW; ++q) {
+      T s = P[Ly::y_b0 + q];
+#pragma unroll
+      for (int m = 0; m < DY0; ++m) s += P[Ly::y_w0 + m * NYW + q] * y0[m];
+      t0[q] = f_tanh(s);
+      y1[q] = (DY0 == NYW) ? RSQ2 * (y0[q < DY0 ? q : 0] + t0[q]) : t0[q];
+    }
+#pragma unroll
+    for (int q = 0; q < NYW; ++q) {
+      T s = P[Ly::y_b1 + q];
+#pragma unroll
+      for (int m = 0; m < NYW; ++m) s += P[Ly::y_w1 + m * NYW + q] * y1[m];
+      t1[q] = f_tanh(s);
+    }
+#pragma unroll
+    for (int q = 0; q < NYW; ++q) y2[q] = RSQ2 * (y1[q] + t1[q]);
+#pragma unroll
+    for (int q = 0; q < NYW; ++q) {
+      T s = P[Ly::y_b2 + q];
+#pragma unroll
+      for (int m = 0; m < NYW; ++m) s += P[Ly::y_w2 + m * NYW + q] * y2[m];
+      t2[q] = f_tanh(s);
+    }
+    // reverse: y3 = (y2 + t2)/sqrt2, y2 = (y1 + t1)/sqrt2, y1 = res(y0, t0)
+    T yb2[NYW], yb1[NYW], z[NYW];
+#pragma unroll
+    for (int q = 0; q < NYW; ++q) z[q] = ystb[q] * RSQ2 * (T(1) - t2[q] * t2[q]);
+#pragma unroll
+    for (int m = 0; m < NYW; ++m) {
+      T s = ystb[m] * RSQ2;
+#pragma unroll
+      for (int q = 0; q < NYW; ++q) {
+        s += P[Ly::y_w2 + m * NYW + q] * z[q];
+        lds_add(&pg[Ly::y_w2 + m * NYW + q], y2[m] * z[q]);
+      }
+      yb2[m] = s;
+    }
+#pragma unroll
+    for (int q = 0; q < NYW; ++q) lds_add(&pg[Ly::y_b2 + q], z[q]);
+#pragma unroll
+    for (int q = 0; q < NYW; ++q) z[q] = yb2[q] * RSQ2 * (T(1) - t1[q] * t1[q]);
+#pragma unroll
+    for (int m = 0; m < NYW; ++m) {
+      T s = yb2[m] * RSQ2;
+#pragma unroll
+      for (int q = 0; q < NYW; ++q) {
+        s += P[Ly::y_w1 + m * NYW + q] * z[q];
+        lds_add(&pg[Ly::y_w1 + m * NYW + q], y1[m] * z[q]);
+      }
+      yb1[m] = s;
+    }
+#pragma unroll
+    for (int q = 0; q < NYW; ++q) lds_add(&pg[Ly::y_b1 + q], z[q]);
+#pragma unroll
+    for (int q = 0; q < NYW; ++q) {
+      z[q] = (DY0 == NYW ? yb1[q] * RSQ2 : yb1[q]) * (T(1) - t0[q] * t0[q]);
+      lds_add(&pg[Ly::y_b0 + q], z[q]);
+    }
+#pragma unroll
+    for (int m = 0; m < DY0; ++m)
+#pragma unroll
+      for (int q = 0; q < NYW; ++q) lds_add(&pg[Ly::y_w0 + m * NYW + q], y0[m] * z[q]);
+  }
+  __syncthreads();
+  // ---------------------------------------------------------------- reverse: h stream (B2)
+  T* hn = sm + SM::hn;
+  T* fb = sm + SM::fb;
+  T* zc = sm + SM::zc;
+  T* zsv = sm + SM::zs;
+#pragma unroll
+  for (int l = 2; l >= 0; --l) {
+    const int d = l == 0 ? D0 : NH;
+    const int DF = 3 * d + 2 * NH2, Q = DF / 4;
+    const T* h = sm + SM::hl + SM::hoff(l);
+    const T* g1 = sm + SM::g1 + l * 2 * D0;
+    const cptr<T> convw = P + (l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2));
+    const cptr<T> sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
+    const int cw = l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2);
+    const int cb = l == 0 ? Ly::conv_b0 : (l == 1 ? Ly::conv_b1 : Ly::conv_b2);
+    const int sw = l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2);
+    const int sb = l == 0 ? Ly::sng_b0 : (l == 1 ? Ly::sng_b1 : Ly::sng_b2);
+    // single: s = tanh(c Ws + bs), h^{l+1} = res(h^l, s)
+    for (int idx = lane; idx < N * NH; idx += 64) {
+      const int i = idx / NH, f = idx - i * NH;
+      const T s = sm[SM::sv + (l * N + i) * NH + f];
+      const T sb_ = (d == NH) ? hb[idx] * RSQ2 : hb[idx];
+      zsv[idx] = sb_ * (T(1) - s * s);
+    }
+    __syncthreads();
+    for (int idx = lane; idx < Q * NH; idx += 64) {
+      const int q = idx / NH, f = idx - q * NH;
+      T a = T(0), b = T(0);
+      for (int i = 0; i < N; ++i) {
+        a += sm[SM::cq + (l * N + i) * QM + q] * zsv[i * NH + f];
+        if (q == 0) b += zsv[i * NH + f];
+      }
+      pg[sw + q * NH + f] += a;
+      if (q == 0) pg[sb + f] += b;
+    }
+    for (int idx = lane; idx < N * Q; idx += 64) {
+      const int i = idx / Q, q = idx - i * Q;
+      T a = T(0);
+#pragma unroll
+      for (int f = 0; f < NH; ++f) a += sngw[q * NH + f] * zsv[i * NH + f];
+      const T c = sm[SM::cq + (l * N + i) * QM + q];
+      const T z = a * (T(1) - c * c);
+      zc[i * QM + q] = z;
+      pg[cb + i * Q + q] += z;
+    }
+    __syncthreads();
+    // conv: c = tanh(0.25 sum_j F_j w_j + b)
+    for (int idx = lane; idx < N * DF; idx += 64) {
+      const int i = idx / DF, j = idx - i * DF;
+      T F;
+      if (j < d) F = h[i * d + j];
+      else if (j < 3 * d) F = g1[((j - d) / d) * D0 + (j - d) % d];
+      else F = sm[SM::g2 + ((l * 2 + (j - 3 * d) / 4) * N + i) * 4 + ((j - 3 * d) & 3)];
+      const T z = T(0.25) * zc[i * QM + j / 4];
+      pg[cw + i * DF + j] += z * F;
+      fb[i * SM::DFM + j] = z * convw[i * DF + j];
+    }
+    __syncthreads();
+    // inputs: h^l (direct + group means), g2 column means
+    for (int idx = lane; idx < 2 * N * NH2; idx += 64) {
+      const int G = idx / (N * NH2), rem = idx - G * N * NH2, i = rem / NH2, f = rem - i * NH2;
+      sm[SM::g2b + ((l * 2 + G) * N + i) * 4 + f] = fb[i * SM::DFM + 3 * d + 4 * G + f];
+    }
+    if (l > 0) {
+      for (int idx = lane; idx < N * NH; idx += 64) {
+        const int k = idx / NH, m = idx - k * NH;
+        const int G = k >= nup ? 1 : 0;
+        T a = fb[k * SM::DFM + m] + ((d == NH) ? hb[idx] * RSQ2 : T(0));
+        T s = T(0);
+        for (int i = 0; i < N; ++i) s += fb[i * SM::DFM + d + G * d + m];
+        hn[idx] = a + s * gw[G];
+      }
+    }
+    __syncthreads();
+    if (l > 0)
+      for (int idx = lane; idx < N * NH; idx += 64) hb[idx] = hn[idx];
+    __syncthreads();
+  }
+  // ---------------------------------------------------------------- reverse: pair stream (B3) + e-e Jastrow
+  for (int idx = lane; idx < N * N; idx += 64) {
+    const int k = idx / N, i = idx - k * N;
+    const bool diag = k == i;
+    const int G = k >= nup ? 1 : 0;
+    T d[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) d[c] = xs[3 * i + c] - xs[3 * k + c];
+    const T r = f_sqrt(diag ? T(1) : d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    T p0[4] = {diag ? T(0) : r, diag ? T(0) : d[0], diag ? T(0) : d[1], diag ? T(0) : d[2]};
+    T t1[4], p1[4], t2[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      T s = P[Ly::dbl_b0 + o];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) s += p0[m] * P[Ly::dbl_w0 + m * 4 + o];
+      t1[o] = f_tanh(s);
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) p1[o] = (p0[o] + t1[o]) * RSQ2;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      T s = P[Ly::dbl_b1 + o];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) s += p1[m] * P[Ly::dbl_w1 + m * 4 + o];
+      t2[o] = f_tanh(s);
+    }
+    T P2b[4], z2[4], P1b[4], z1[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) P2b[f] = sm[SM::g2b + ((2 * 2 + G) * N + i) * 4 + f] * gw[G];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      z2[o] = P2b[o] * RSQ2 * (T(1) - t2[o] * t2[o]);
+      lds_add(&pg[Ly::dbl_b1 + o], z2[o]);
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      T s = sm[SM::g2b + ((1 * 2 + G) * N + i) * 4 + m] * gw[G] + P2b[m] * RSQ2;
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        s += P[Ly::dbl_w1 + m * 4 + o] * z2[o];
+        lds_add(&pg[Ly::dbl_w1 + m * 4 + o], p1[m] * z2[o]);
+      }
+      P1b[m] = s;
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      z1[o] = P1b[o] * RSQ2 * (T(1) - t1[o] * t1[o]);
+      lds_add(&pg[Ly::dbl_b0 + o], z1[o]);
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int o = 0; o < 4; ++o) lds_add(&pg[Ly::dbl_w0 + m * 4 + o], p0[m] * z1[o]);
+    if (k < i) {   // Jastrow.py:23-52: cusp r / (1 + alpha r), alpha per unordered pair
+      const T cusp = P[Ly::jee_c + k * N + i], al = P[Ly::jee_a + k * N + i];
+      const T den = al * r + T(1);
+      pg[Ly::jee_a + k * N + i] += -cusp * r * r / (den * den);
+    }
+  }
+  __syncthreads();
+  // ---------------------------------------------------------------- outputs
+  T* out = (T*)ka.grad + (size_t)conf * Ly::total;
+  for (int idx = lane; idx < Ly::total; idx += 64) out[idx] = pg[idx];
+  const T lpsi = logdet + wave_sum(jae_v + jee_v);
+  if (lane == 0 && ka.logabs) ((T*)ka.logabs)[conf] = lpsi;
+}
+
+// out[j] = sum_b w[b] O[b][j] over the kernel layout (deterministic order): one block of 256
+// threads per 64 columns, thread (t / 64) strides the walkers.
+template <typename T>
+__global__ __launch_bounds__(256) void k_grad_reduce(const T* __restrict__ O, const T* __restrict__ w, int B, int n,
+                                                     T* __restrict__ out) {
+  __shared__ T part[4][64];
+  const int j = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int s = threadIdx.x >> 6;
+  T a = T(0);
+  if (j < n)
+    for (int b = s; b < B; b += 4) a += w[b] * O[(size_t)b * n + j];
+  part[s][threadIdx.x & 63] = a;
+  __syncthreads();
+  if (s == 0 && j < n) out[j] = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
+}
+
+// Kernel layout -> canonical (tree_flatten) order for `rows` gradient vectors.  map[k] >= 0: the
+// kernel entry of canonical parameter k; -1: unused by the network (eplion, mu, nu, envelope.py);
+// <= -2: the y coefficient W_y[m][c] (m*N + c = -2 - map[k]), whose kernel entry is the
+// row-normalised What = W / |W_m| (nn.py:449-451): dW = (dWhat - What (What . dWhat)) / |W_m|.
+template <typename T>
+__global__ __launch_bounds__(256) void k_grad_canon(const T* __restrict__ G, int nkern, const int* __restrict__ map,
+                                                    int ncanon, const T* __restrict__ what, int wy_off,
+                                                    const double* __restrict__ wnorm, int N, int rows,
+                                                    T* __restrict__ out) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)rows * ncanon) return;
+  const int row = (int)(t / ncanon), k = (int)(t - (size_t)row * ncanon);
+  const T* g = G + (size_t)row * nkern;
+  const int m_ = map[k];
+  T v = T(0);
+  if (m_ >= 0) {
+    v = g[m_];
+  } else if (m_ <= -2) {
+    const int mc = -2 - m_, m = mc / N, c = mc - m * N;
+    T dot = T(0);
+    for (int cc = 0; cc < N; ++cc) dot += what[m * N + cc] * g[wy_off + m * N + cc];
+    v = (g[wy_off + mc] - what[mc] * dot) / (T)wnorm[m];
+  }
+  out[t] = v;
+}
+
+}  // namespace aq

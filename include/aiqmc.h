@@ -104,6 +104,16 @@ int aiqmc_mc_step(aiqmc_ctx* ctx, void* pos_inout, int32_t B, int32_t nsteps, do
                   int32_t rng_mode, const void* gauss1, const void* gauss2, const void* u,
                   uint64_t seed, uint64_t offset, int32_t* accept_out, void* stream);
 
+/* Parameter gradient of log|psi| (the psi_tangent of the energy-gradient custom JVP,
+ * Loss/loss.py:242-265, differentiated wrt params as jax.value_and_grad does in
+ * Optimizer/adam.py:51-54).  Output in the canonical tree_flatten order of
+ * aiqmc_set_params (aiqmc_param_count entries; unused leaves eplion/mu/nu get 0):
+ *   weights == NULL: out[B][P] = d log|psi(x_b)| / d theta      (per walker)
+ *   weights != NULL: out[P]    = sum_b weights[b] d log|psi(x_b)| / d theta
+ * weights/out/logabs are device arrays of the context dtype; logabs[B] optional. */
+int aiqmc_logpsi_param_grad(aiqmc_ctx* ctx, const void* pos, int32_t B, const void* weights, void* out,
+                            void* logabs, void* stream);
+
 /* Pseudopotential tables (pphamiltonian.local_energy arguments,
  * Energy/pphamiltonian.py:130-146; shapes as the example drivers pass them,
  * example/single_atom_C/single_atom_C.py:13-23).  All HOST pointers; the

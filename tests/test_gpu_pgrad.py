@@ -1,0 +1,68 @@
+"""Parameter gradient of log|psi| (aiqmc_logpsi_param_grad) vs the float64 oracle
+(torch.func.grad of the oracle network wrt the parameter tree), and the energy gradient
+it feeds (Loss/loss.py:220-270).  Tolerances: fp64 1e-8 relative to the largest
+component of each walker's gradient; fp32 2e-3."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(name, dtype, B=4, seed=41):
+    from oracle import system
+    from aiqmc import _lib
+    s = system.make_system(name)
+    t = s.tables()
+    ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
+                       t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"], dtype=dtype, device=0)
+    rng = np.random.default_rng(seed)
+    params = system.init_params(rng, s, randomize_aux=True)
+    ctx.set_params(system.flatten_params(params))
+    pos = system.init_electrons(rng, s.atoms, s.charges, B, 1.0)
+    return s, ctx, params, pos
+
+
+@pytest.mark.parametrize("name", ["H2", "Be", "N2"])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_param_grad_matches_oracle(name, dtype):
+    from oracle import loss, network
+    s, ctx, params, pos = _setup(name, dtype)
+    g, la = ctx.logpsi_param_grad(torch.tensor(pos, dtype=dtype, device="cuda"), want_logabs=True)
+    torch.cuda.synchronize()
+    ref = loss.logabs_param_grad(network.Network(s), params, torch.tensor(pos))
+    got = g.double().cpu().numpy()
+    assert got.shape == ref.shape == (pos.shape[0], ctx.nparams)
+    tol = 1e-8 if dtype == torch.float64 else 2e-3
+    scale = np.abs(ref).max(axis=1, keepdims=True) + 1e-3
+    err = np.abs(got - ref) / scale
+    assert err.max() < tol, (err.max(), np.unravel_index(err.argmax(), err.shape))
+    la_ref, _ = ctx.logpsi(torch.tensor(pos, dtype=dtype, device="cuda"))
+    np.testing.assert_allclose(la.double().cpu().numpy(), la_ref.double().cpu().numpy(), rtol=1e-6, atol=1e-6)
+
+
+def test_weighted_sum_and_energy_gradient():
+    """sum_b w_b O_b on the device == the per-walker rows contracted on the host; the energy
+    gradient of loss.py:220-270 built from it == the oracle formula."""
+    from oracle import loss
+    s, ctx, params, pos = _setup("Be", torch.float64, B=64, seed=5)
+    x = torch.tensor(pos, device="cuda")
+    O = ctx.logpsi_param_grad(x)
+    e_l, _, _ = ctx.local_energy(x)
+    el = e_l.cpu().numpy()
+    l0, var0, g_ref = loss.energy_gradient(el, O.cpu().numpy(), clip_scale=5.0)
+    center, diff = loss.clip_local_values(el, l0, 5.0)
+    w = torch.tensor(2.0 * diff / len(el), device="cuda")
+    g = ctx.logpsi_param_grad(x, weights=w)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(g.cpu().numpy(), (w.cpu().numpy() @ O.cpu().numpy()), rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(g.cpu().numpy(), g_ref, rtol=1e-9, atol=1e-11)
+
+
+def test_param_grad_full_batch_finite():
+    s, ctx, params, pos = _setup("N2", torch.float32, B=4096, seed=9)
+    x = torch.tensor(pos, dtype=torch.float32, device="cuda")
+    g = ctx.logpsi_param_grad(x, weights=torch.full((4096,), 1.0 / 4096, device="cuda"))
+    O = ctx.logpsi_param_grad(x[:64])
+    torch.cuda.synchronize()
+    assert torch.isfinite(g).all() and torch.isfinite(O).all()

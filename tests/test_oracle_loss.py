@@ -1,0 +1,51 @@
+"""Energy-gradient / Adam oracle (oracle/loss.py) pinned by finite differences and closed forms."""
+import math
+
+import numpy as np
+import torch
+
+
+def test_param_grad_finite_differences():
+    from oracle import loss, network, system
+    s = system.make_system("H2")
+    rng = np.random.default_rng(3)
+    params = system.init_params(rng, s, randomize_aux=True)
+    pos = torch.tensor(system.init_electrons(rng, s.atoms, s.charges, 2, 1.0))
+    net = network.Network(s)
+    O = loss.logabs_param_grad(net, params, pos)
+    flat = system.flatten_params(params)
+    for k in rng.choice(flat.size, 25, replace=False):
+        h = 1e-6
+        fp, fm = flat.copy(), flat.copy()
+        fp[k] += h
+        fm[k] -= h
+        lp = net.logabs(network.to_torch(system.unflatten_params(params, fp)), pos[0]).item()
+        lm = net.logabs(network.to_torch(system.unflatten_params(params, fm)), pos[0]).item()
+        assert abs((lp - lm) / (2 * h) - O[0, k]) < 1e-6 * (1 + abs(O[0, k])), k
+
+
+def test_energy_gradient_closed_form():
+    from oracle import loss
+    rng = np.random.default_rng(0)
+    e = rng.standard_normal(50)
+    e[3] = 40.0                                          # an outlier the 5-TV window clips
+    O = rng.standard_normal((50, 7))
+    l, var, g = loss.energy_gradient(e, O, clip_scale=5.0)
+    tv = np.mean(np.abs(e - e.mean()))
+    c = np.clip(e, e.mean() - 5 * tv, e.mean() + 5 * tv)
+    assert c[3] < 40.0
+    np.testing.assert_allclose(g, 2.0 / 50 * ((c - c.mean()) @ O), rtol=1e-12)
+    assert abs(l - e.mean()) < 1e-14 and abs(var - e.var()) < 1e-12
+
+
+def test_adam_restatement():
+    from oracle import loss
+    opt = loss.Adam(3)
+    p = np.array([1.0, -2.0, 0.5])
+    g = np.array([0.3, -0.1, 0.0])
+    p1 = opt.update(g, p)
+    # first step: m_hat = g, v_hat = g^2 -> u = g / (|g| + eps) * 0.05
+    np.testing.assert_allclose(p1, p - 0.05 * g / (np.abs(g) + 1e-8), rtol=1e-12)
+    p2 = opt.update(g, p1)
+    assert loss.lr_schedule(1) == 0.05 * 2.0 ** -10000   # the reference schedule collapses after step 0
+    np.testing.assert_allclose(p2, p1, atol=1e-300)
