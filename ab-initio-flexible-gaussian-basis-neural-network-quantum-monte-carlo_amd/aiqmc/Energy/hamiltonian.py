@@ -109,4 +109,5 @@ def local_energy(f, charges, nspins: Sequence[int], use_scan: bool = False, comp
         ctx = net.bind(params, data.atoms, dtype)
         el, _, _ = ctx.local_energy(pos)
         return el.reshape(pos.shape[:-1]), None
+    _e_l._aiqmc_network = net
     return _e_l

@@ -69,4 +69,5 @@ def local_energy(f, lognetwork, charges, nspins, rn_local, local_coes, local_exp
             e = ctx.local_energy_ecp(pos, seed=k.seed, offset=k.offset)
         return e.reshape(pos.shape[:-1]), None
 
+    _e_l._aiqmc_network = net
     return _e_l

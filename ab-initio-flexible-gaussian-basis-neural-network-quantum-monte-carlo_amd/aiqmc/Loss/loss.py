@@ -1,0 +1,120 @@
+"""Energy loss with the unbiased energy gradient (drop-in for AIQMCrelease3/Loss/loss.py:73-272).
+
+``make_loss(network, local_energy, clip_local_energy, clip_from_median,
+center_at_clipped_energy, complex_output)`` returns ``total_energy(params, key, data) ->
+(loss, AuxiliaryLossData)``; the reference differentiates it with ``jax.value_and_grad``
+through a custom JVP (:220-270).  Here the derivative is explicit:
+``total_energy.value_and_grad(params, key, data) -> ((loss, aux), grad_tree)``, with
+
+    grad = pmean( (2 / B) sum_b diff_b d log|psi_b| / d theta )
+
+(diff = clipped local energy minus its batch mean, :73-135; for real E_L the complex_output
+formula (term1 - 2 term2).real / B reduces to this), computed on the GPU by
+aiqmc_logpsi_param_grad with weights 2 diff_b / B (one launch + a device reduction).
+Complex local energies (the pseudopotential driver) need d phase / d theta as well, which is
+not built: they raise.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Any, Optional
+
+import numpy as np
+import torch
+
+from .. import constants
+
+
+@dataclasses.dataclass
+class AuxiliaryLossData:
+    """loss.py:28-41."""
+    variance: Any
+    local_energy: Any
+    clipped_energy: Any
+    grad_local_energy: Any = None
+    local_energy_mat: Any = None
+
+
+def clip_local_values(local_values: torch.Tensor, mean_local_values: torch.Tensor, clip_scale: float,
+                      clip_from_median: bool, center_at_clipped_value: bool, complex_output: bool = False):
+    """loss.py:73-135: (diff_center, diff) with the total-variation window (pmean'd)."""
+    batch_mean = lambda v: constants.pmean(torch.mean(v))
+
+    def clip_at_total_variation(values, center, scale):
+        tv = batch_mean(torch.abs(values - center))
+        return torch.clamp(values, center - scale * tv, center + scale * tv)
+
+    if clip_from_median:
+        center = torch.median(constants.all_gather(local_values).real.reshape(-1))
+    else:
+        center = mean_local_values
+    if torch.is_complex(local_values):
+        clipped = torch.complex(clip_at_total_variation(local_values.real, center.real, clip_scale),
+                                clip_at_total_variation(local_values.imag, center.imag, clip_scale))
+    else:
+        clipped = clip_at_total_variation(local_values, center, clip_scale)
+    diff_center = batch_mean(clipped) if center_at_clipped_value else mean_local_values
+    return diff_center, clipped - diff_center
+
+
+def _unflatten_like(template, flat: np.ndarray):
+    pos = [0]
+
+    def build(tree):
+        if isinstance(tree, dict):
+            return {k: build(tree[k]) for k in sorted(tree.keys())}
+        if isinstance(tree, (list, tuple)):
+            return [build(v) for v in tree]
+        a = np.asarray(tree.detach().cpu() if isinstance(tree, torch.Tensor) else tree)
+        out = flat[pos[0]:pos[0] + a.size].reshape(a.shape)
+        pos[0] += a.size
+        return out
+    return build(template)
+
+
+def make_loss(network, local_energy, clip_local_energy: float = 0.0, clip_from_median: bool = True,
+              center_at_clipped_energy: bool = True, complex_output: bool = False):
+    """loss.py:138-272.  `network` is the (log) network closure of the driver; the AIQMC
+    network whose parameters are differentiated is taken from it or from `local_energy`."""
+    net = getattr(network, "_aiqmc_network", None) or getattr(local_energy, "_aiqmc_network", None)
+    if net is None:
+        raise TypeError("make_loss: local_energy must come from aiqmc.Energy (it carries the HIP network)")
+
+    def _energy(params, key, data):
+        e_l, e_mat = local_energy(params, key, data)
+        loss = constants.pmean(torch.mean(e_l))
+        d = e_l - loss
+        variance = constants.pmean(torch.mean(d * torch.conj(d))).real
+        return e_l, e_mat, loss, variance
+
+    def total_energy(params, key, data):
+        e_l, e_mat, loss, variance = _energy(params, key, data)
+        return loss, AuxiliaryLossData(variance=variance, local_energy=e_l, clipped_energy=e_l,
+                                       local_energy_mat=e_mat)
+
+    def value_and_grad(params, key, data):
+        e_l, e_mat, loss, variance = _energy(params, key, data)
+        if torch.is_complex(e_l) and bool(torch.any(e_l.imag != 0)):
+            raise NotImplementedError("complex local energies need d phase / d theta, which is not built")
+        e_r = e_l.real if torch.is_complex(e_l) else e_l
+        loss_r = loss.real if torch.is_complex(loss) else loss
+        if clip_local_energy > 0.0:
+            center, diff = clip_local_values(e_r, loss_r, clip_local_energy, clip_from_median,
+                                             center_at_clipped_energy)
+        else:
+            center, diff = loss_r, e_r - loss_r
+        pos = data.positions if isinstance(data.positions, torch.Tensor) else torch.as_tensor(
+            np.asarray(data.positions))
+        dtype = pos.dtype if pos.dtype in (torch.float32, torch.float64) else torch.float32
+        ctx = net.bind(params, data.atoms, dtype)
+        B = diff.numel()
+        w = (2.0 / B) * diff.reshape(-1).to(ctx.device, dtype)
+        g = ctx.logpsi_param_grad(pos.reshape(B, -1), weights=w)     # loss.py:256-265
+        aux = AuxiliaryLossData(variance=variance, local_energy=e_l, clipped_energy=center + diff,
+                                local_energy_mat=e_mat)
+        return (loss, aux), g
+
+    total_energy.value_and_grad = value_and_grad
+    total_energy.unflatten = lambda params, flat: _unflatten_like(params, flat)
+    total_energy._aiqmc_network = net
+    return total_energy

@@ -1,0 +1,46 @@
+"""Adam training step (drop-in for AIQMCrelease3/Optimizer/adam.py:49-81).
+
+``make_opt_update_step(evaluate_loss, optimizer)`` -> ``opt_update(params, data, opt_state,
+key) -> (params, opt_state, loss, aux)``: the energy gradient of ``evaluate_loss`` (aiqmc
+Loss.make_loss, computed on the GPU), ``constants.pmean`` of the gradient (ONE RCCL
+all-reduce of the parameter vector, adam.py:55), then the optimizer (Optimizer.optax_like).
+``make_training_step(opt_update)`` adds the NaN rollback of adam.py:74-79.  Parameters stay a
+reference-shaped pytree (numpy leaves); the optimizer runs on the flat device vector.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from .. import constants
+from ..wavefunction_Ynlm.nn import flatten_params
+
+
+def make_opt_update_step(evaluate_loss, optimizer):
+    vg = getattr(evaluate_loss, "value_and_grad", None)
+    if vg is None:
+        raise TypeError("evaluate_loss must come from aiqmc.Loss.loss.make_loss")
+
+    def opt_update(params, data, opt_state, key):
+        (loss, aux), grad = vg(params, key, data)
+        grad = constants.pmean(grad)
+        flat = torch.as_tensor(flatten_params(params), dtype=grad.dtype, device=grad.device)
+        if opt_state is None:
+            opt_state = optimizer.init(flat)
+        updates, opt_state = optimizer.update(grad, opt_state, flat)
+        new_flat = (flat + updates).detach().cpu().to(torch.float64).numpy()
+        return evaluate_loss.unflatten(params, new_flat), opt_state, loss, aux
+    return opt_update
+
+
+def make_training_step(optimizer_step):
+    """adam.py:62-81: one optimisation step; parameters/state roll back if the loss is NaN."""
+
+    def step(data, params, state, key):
+        new_params, new_state, loss, aux = optimizer_step(params, data, state, key)
+        if math.isnan(float(loss.real if torch.is_complex(loss) else loss)):
+            return data, params, state, loss, aux
+        return data, new_params, new_state, loss, aux
+    return step

@@ -102,3 +102,41 @@ def test_pphamiltonian_drop_in_matches_golden(golden_dir):
     assert np.max(np.abs(out.imag.cpu().numpy() - g["e_im"])) < 1e-6
     out2, _ = el(params, 11, data)                      # Philox rotations
     assert torch.isfinite(out2.real).all()
+
+
+def test_adam_training_step_matches_oracle():
+    """make_loss + Adam chain + make_training_step driven like
+    main_all_electrons_adam_muti_GPU.py:143-190 (clip 5.0, complex_output=True, Adam 0.9/0.999,
+    lr 0.05 (1+t)^-10000), one step, vs the oracle energy gradient and Adam restatement."""
+    from oracle import hamiltonian, loss as oloss, network as onet, system
+    from aiqmc.Energy import hamiltonian as H
+    from aiqmc.Loss import loss as L
+    from aiqmc.Optimizer import adam, optax_like as optax
+    s, network, params, data = _setup(B=16)
+
+    def log_network(*args, **kwargs):
+        phase, mag = network.apply(*args, **kwargs)
+        return mag + 1.j * phase
+
+    local_energy = H.local_energy(f=network.apply, charges=s.charges, nspins=s.spins, use_scan=False)
+    evaluate_loss = L.make_loss(network=log_network, local_energy=local_energy, clip_local_energy=5.0,
+                                clip_from_median=False, center_at_clipped_energy=True, complex_output=True)
+    sched = lambda t: 0.05 * (1.0 / (1.0 + t)) ** 10000
+    optimizer = optax.chain(optax.scale_by_adam(b1=0.9, b2=0.999, eps=1e-8, eps_root=0.0),
+                            optax.scale_by_schedule(sched), optax.scale(-1.))
+    step = adam.make_training_step(adam.make_opt_update_step(evaluate_loss, optimizer))
+    _, new_params, state, loss_v, aux = step(data, params, None, 0)
+    # oracle
+    net = onet.Network(s)
+    x = data.positions.cpu()
+    e_ref, _, _ = hamiltonian.batch_local_energy(net, onet.to_torch(params), x)
+    O = oloss.logabs_param_grad(net, params, x)
+    l_ref, var_ref, g_ref = oloss.energy_gradient(e_ref.numpy(), O, clip_scale=5.0)
+    flat = system.flatten_params(params)
+    p_ref = oloss.Adam(flat.size).update(g_ref, flat)
+    assert abs(float(loss_v) - l_ref) < 1e-6
+    assert abs(float(aux.variance) - var_ref) < 1e-5 * (1 + var_ref)
+    np.testing.assert_allclose(system.flatten_params(new_params), p_ref, rtol=1e-9, atol=1e-9)
+    # the reference schedule collapses after step 0: the second step leaves the parameters unchanged
+    _, p2, state, _, _ = step(data, new_params, state, 1)
+    np.testing.assert_allclose(system.flatten_params(p2), system.flatten_params(new_params), rtol=0, atol=1e-300)
