@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--cpu-sample-walkers", type=int, default=8)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     ap.add_argument("--no-ecp", action="store_true", help="skip the C-atom ccECP local-energy side measurement")
+    ap.add_argument("--no-adam", action="store_true", help="skip the Be-atom Adam training-step side measurement")
     return ap.parse_args()
 
 
@@ -165,6 +166,52 @@ def ecp_side_bench(dtype, device, walkers, steps, cpu_baseline_on):
         res["cpu_baseline"] = {"value": 2 / tc, "unit": "local-energy evals/s", "cores": torch.get_num_threads(),
                                "kind": "port", "sample": f"float64 oracle, 2 walkers ({tc:.1f}s)"}
     return res
+
+
+def adam_side_bench(dtype, device, walkers, steps):
+    """BASELINE.json config 'Be atom (4e-), 4096 walkers, Adam, 1xMI355X': one training iteration
+    of main_all_electrons_adam_muti_GPU.py:177-190 = mc_step (nsteps=10) + make_loss energy gradient
+    (local energy, clipping, GPU parameter gradient) + Adam update, through the drop-in API."""
+    from aiqmc import spin_indices
+    from aiqmc.Energy import hamiltonian as H
+    from aiqmc.Loss import loss as L
+    from aiqmc.Optimizer import adam, optax_like as optax
+    from aiqmc.VMC import VMCmcstep
+    from aiqmc.wavefunction_Ynlm import nn
+    from aiqmc.initial_electrons_positions.init import init_electrons
+    atoms, charges = system_def("Be")
+    n = 4
+    spins = np.array([1.0, -1.0, 1.0, -1.0])
+    par, anti, npar, nanti = spin_indices.jastrow_indices_ee(spins, n)
+    up, dn = spin_indices.spin_indices_h(spins)
+    network = nn.make_ai_net(nspins=(2, 2), charges=charges, parallel_indices=par, antiparallel_indices=anti,
+                             spin_up_indices=up, spin_down_indices=dn, n_parallel=npar, n_antiparallel=nanti,
+                             ndim=3, natoms=1, nelectrons=n)
+    params = network.init(2)
+    pos, sp = init_electrons(5, None, atoms, charges, spins, walkers, 1.0)
+    data = nn.AINetData(positions=pos.to(device, dtype).contiguous(), spins=sp, atoms=atoms, charges=charges)
+    mc_step = VMCmcstep.main_monte_carlo(f=network.apply, tstep=0.05, ndim=3, nelectrons=n, nsteps=10,
+                                         batch_size=walkers)
+    le = H.local_energy(f=network.apply, charges=charges, nspins=spins)
+    ev = L.make_loss(network=network.apply, local_energy=le, clip_local_energy=5.0, clip_from_median=False,
+                     center_at_clipped_energy=True, complex_output=True)
+    opt = optax.chain(optax.scale_by_adam(b1=0.9, b2=0.999, eps=1e-8, eps_root=0.0),
+                      optax.scale_by_schedule(lambda t: 0.05 * (1.0 / (1.0 + t)) ** 10000), optax.scale(-1.))
+    step = adam.make_training_step(adam.make_opt_update_step(ev, opt))
+    state = None
+    for t in range(2):
+        data = mc_step(params, data, VMCmcstep.PhiloxKey(9, 10 * t))
+        data, params, state, loss_v, aux = step(data, params, state, t)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(steps):
+        data = mc_step(params, data, VMCmcstep.PhiloxKey(9, 100 + 10 * t))
+        data, params, state, loss_v, aux = step(data, params, state, 2 + t)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    return {"config": "Be atom (4 e-), Adam: mc_step (10 sweeps) + energy gradient + Adam update, drop-in API",
+            "walkers": walkers, "ms_per_iteration": 1e3 * dt, "iterations_per_s": 1.0 / dt,
+            "walker_steps_per_s": walkers * 10 / dt, "energy": float(loss_v), "finite": bool(math.isfinite(float(loss_v)))}
 
 
 def main():
@@ -289,6 +336,11 @@ def main():
                 out["ecp_c_atom"] = ecp_side_bench(dtype, dev, 4096, 5, not args.no_cpu_baseline)
             except Exception as e:  # a side measurement, never a failure of the headline bench
                 out["ecp_c_atom"] = {"error": repr(e)}
+        if world == 1 and not args.no_adam:
+            try:
+                out["adam_be_atom"] = adam_side_bench(dtype, dev, 4096, 5)
+            except Exception as e:  # a side measurement, never a failure of the headline bench
+                out["adam_be_atom"] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(args.system, params, atoms, charges, args.nsteps, args.tstep,
