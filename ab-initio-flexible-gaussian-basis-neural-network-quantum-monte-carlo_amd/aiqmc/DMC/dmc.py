@@ -1,0 +1,47 @@
+"""One DMC propagation step (drop-in for AIQMCrelease3/DMC/dmc.py:13-93), T-moves excluded.
+
+``dmc_propagate(signed_network, log_network, logabs_f, list_l, nelectrons, natoms, ndim,
+batch_size, tstep, nsteps, charges, spins, Rn_local, ...)`` returns
+``dmc_propagate_run(params, key, data, weights, branchcut_start, e_trial, e_est) ->
+(eloc_new, weights, new_data)``: drift-diffusion (aiqmc_dmc_drift_diffusion), the complex
+pseudopotential local energies before and after (aiqmc_local_energy_ecp), and the weight
+update with the S factors (aiqmc_dmc_weights).  The reference first applies T-moves
+(DMC/Tmoves.py), whose amplitude bookkeeping hard-codes the slice layout of a 3-atom system
+(back_amplitudes[:, 1:19] ... [:, 79:151]) and compares complex amplitudes with `>`; they are
+not built here, so this step is the reference's propagation without the T-move proposal.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..Energy import pphamiltonian
+from ..VMC.VMCmcstep import PhiloxKey
+from .drift_diffusion import propose_drift_diffusion
+
+
+def dmc_propagate(signed_network, log_network, logabs_f, list_l: int, nelectrons: int, natoms: int, ndim: int,
+                  batch_size: int, tstep: float, nsteps: int, charges, spins, Rn_local, Local_coes, Local_exps,
+                  Rn_non_local, Non_local_coes, Non_local_exps):
+    del nsteps
+    dd = propose_drift_diffusion(signed_network, tstep, ndim, nelectrons, batch_size)
+    le = pphamiltonian.local_energy(f=signed_network, lognetwork=log_network, charges=charges, nspins=spins,
+                                    rn_local=Rn_local, local_coes=Local_coes, local_exps=Local_exps,
+                                    rn_non_local=Rn_non_local, non_local_coes=Non_local_coes,
+                                    non_local_exps=Non_local_exps, natoms=natoms, nelectrons=nelectrons, ndim=ndim,
+                                    list_l=list_l)
+    net = signed_network._aiqmc_network
+
+    def dmc_propagate_run(params, key, data, weights: torch.Tensor, branchcut_start, e_trial, e_est):
+        k = key if isinstance(key, PhiloxKey) else PhiloxKey(int(key), 0)
+        eloc_old, _ = le(params, PhiloxKey(k.seed + 1, k.offset), data)
+        new_data, _, tdamp_scalar, go, gn = dd(params, k, data)
+        eloc_new, _ = le(params, PhiloxKey(k.seed + 2, k.offset), new_data)
+        ctx = net.bind(params, data.atoms, go.dtype)
+        td = torch.zeros(3, dtype=torch.float64, device=go.device)
+        td[2] = tdamp_scalar
+        bc = float(torch.as_tensor(branchcut_start).reshape(-1)[0])
+        w = weights.to(go.device, go.dtype).contiguous().clone()
+        ctx.dmc_weights(w, eloc_old, eloc_new, go, gn, td, tstep, float(e_trial), float(e_est), bc)
+        return eloc_new, w, new_data
+
+    return dmc_propagate_run

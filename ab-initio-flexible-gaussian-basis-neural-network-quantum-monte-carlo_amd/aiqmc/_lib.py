@@ -31,6 +31,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_profile_enable", "aiqmc_profile_read", "aiqmc_debug_logpsi_grad_forward",
     "aiqmc_debug_set_proposal_reuse", "aiqmc_debug_phase_cycles", "aiqmc_debug_local_energy_forward",
     "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
+    "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -109,6 +110,10 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_debug_phase_cycles.argtypes = [vp, vp]
     lib.aiqmc_debug_phase_cycles.restype = ctypes.c_int
     lib.aiqmc_logpsi_param_grad.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+    dbl, u64 = ctypes.c_double, ctypes.c_uint64
+    lib.aiqmc_dmc_drift_diffusion.argtypes = [vp, vp, i32, dbl, i32, vp, vp, vp, u64, u64, vp, vp, vp, vp]
+    lib.aiqmc_dmc_weights.argtypes = [vp, i32, vp, vp, vp, vp, vp, dbl, dbl, dbl, dbl, vp, vp]
+    lib.aiqmc_dmc_branch.argtypes = [vp, i32, vp, dbl, vp, vp, vp]
     lib.aiqmc_set_ecp.argtypes = [vp, ctypes.POINTER(AiqmcEcp)]
     lib.aiqmc_local_energy_ecp.argtypes = [vp, vp, i32, i32, vp, ctypes.c_uint64, ctypes.c_uint64, vp, vp, vp,
                                            vp, vp]
@@ -118,7 +123,8 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_supported_shapes.restype = ctypes.c_char_p
     for name in ("aiqmc_create", "aiqmc_destroy", "aiqmc_set_params", "aiqmc_logpsi",
                  "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_mc_step", "aiqmc_profile_enable",
-                 "aiqmc_profile_read", "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad"):
+                 "aiqmc_profile_read", "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
+                 "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib
@@ -318,6 +324,48 @@ class Context:
         check(self._lib.aiqmc_logpsi_param_grad(self._h, _ptr(p), B, _ptr(w), _ptr(out), _ptr(la),
                                                 _stream(self.device)), "aiqmc_logpsi_param_grad")
         return (out, la) if want_logabs else out
+
+    # -- DMC (DMC/drift_diffusion.py, S_matrix.py, dmc.py, branch.py) -------------
+    def dmc_drift_diffusion(self, pos: torch.Tensor, tstep: float, gauss1=None, gauss2=None, u=None, seed: int = 0,
+                            offset: int = 0):
+        """In-place drift-diffusion step; returns (grad_eff_old, grad_new_eff, tdamp[3] float64)."""
+        if not (pos.is_cuda and pos.dtype == self.dtype and pos.is_contiguous()):
+            raise ValueError("dmc_drift_diffusion needs a contiguous device tensor of the context dtype")
+        B = pos.numel() // (3 * self.N)
+        host = gauss1 is not None
+        g1 = gauss1.to(self.device, self.dtype).contiguous() if host else None
+        g2 = gauss2.to(self.device, self.dtype).contiguous() if host else None
+        uu = u.to(self.device, self.dtype).contiguous() if host else None
+        go = torch.empty(B, 3 * self.N, dtype=self.dtype, device=self.device)
+        gn = torch.empty_like(go)
+        td = torch.zeros(3, dtype=torch.float64, device=self.device)
+        check(self._lib.aiqmc_dmc_drift_diffusion(self._h, _ptr(pos), B, float(tstep),
+                                                  AIQMC_RNG_HOST if host else AIQMC_RNG_PHILOX, _ptr(g1), _ptr(g2),
+                                                  _ptr(uu), ctypes.c_uint64(seed), ctypes.c_uint64(offset), _ptr(go),
+                                                  _ptr(gn), _ptr(td), _stream(self.device)), "aiqmc_dmc_drift_diffusion")
+        return go, gn, td
+
+    def dmc_weights(self, weights: torch.Tensor, eloc_old, eloc_new, grad_eff_old, grad_new_eff, tdamp, tstep: float,
+                    e_trial: float, e_est: float, branchcut: float):
+        """weights *= exp(tau tdamp (S_new + S_old) / 2), in place (S_matrix.py:4-24, dmc.py:88-92)."""
+        B = weights.numel()
+        eo = eloc_old.real.to(self.device, self.dtype).contiguous()
+        en = eloc_new.real.to(self.device, self.dtype).contiguous()
+        check(self._lib.aiqmc_dmc_weights(self._h, B, _ptr(eo), _ptr(en), _ptr(grad_eff_old.contiguous()),
+                                          _ptr(grad_new_eff.contiguous()), _ptr(tdamp), float(tstep), float(e_trial),
+                                          float(e_est), float(branchcut), _ptr(weights), _stream(self.device)),
+              "aiqmc_dmc_weights")
+        return weights
+
+    def dmc_branch(self, weights: torch.Tensor, u: float):
+        """Stochastic comb (branch.py:10-33): (new uniform weight [1], newinds [B] int32)."""
+        B = weights.numel()
+        w = weights.to(self.device, self.dtype).contiguous()
+        idx = torch.empty(B, dtype=torch.int32, device=self.device)
+        wo = torch.empty(1, dtype=self.dtype, device=self.device)
+        check(self._lib.aiqmc_dmc_branch(self._h, B, _ptr(w), float(u), _ptr(idx), _ptr(wo), _stream(self.device)),
+              "aiqmc_dmc_branch")
+        return wo, idx
 
     def set_ecp(self, rn_local, local_coes, local_exps, rn_non_local, non_local_coes, non_local_exps,
                 list_l: int):

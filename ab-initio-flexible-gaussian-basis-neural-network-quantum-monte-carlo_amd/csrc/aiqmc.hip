@@ -74,6 +74,116 @@ __global__ __launch_bounds__(256) void k_draws(uint64_t seed, uint64_t step, int
   u[t] = (T)(c[0] - 5.9604644775390625e-08f);   // [0,1)
 }
 
+// DMC drift-diffusion extras (DMC/drift_diffusion.py:15-22), one 1024-thread block, fixed order:
+// grad != nullptr: out[0] = sum over all coordinates of the proposed configuration
+//   x + limdrift(grad) tau + sqrt(tau) gauss1 (the `changed_configuration` of :66);
+// grad == nullptr: out[1] = sum of x (after acceptance), out[2] = tdamp = out[1] / out[0].
+template <typename T>
+__global__ __launch_bounds__(1024) void k_dmc_sum(const T* __restrict__ x, const T* __restrict__ grad,
+                                                  const T* __restrict__ g1, const double* __restrict__ taueff,
+                                                  double tstep_d, int n, double* out) {
+  __shared__ double red[1024];
+  const T tstep = (T)tstep_d;
+  const T sq = sqrt(tstep);
+  const T te = grad ? (T)taueff[0] : T(0);
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    T v = x[i];
+    if (grad) v = v + (grad[i] * te * tstep + sq * g1[i]);
+    acc += (double)v;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (grad) {
+      out[0] = red[0];
+    } else {
+      out[1] = red[0];
+      out[2] = red[0] / out[0];
+    }
+  }
+}
+
+// out[i] = grad[i] * taueff (limdrift, VMCmcstep.py:11-14 / drift_diffusion.py:9-12)
+template <typename T>
+__global__ __launch_bounds__(256) void k_scale_grad(const T* __restrict__ g, const double* __restrict__ taueff, int n,
+                                                    T* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = g[i] * (T)taueff[0];
+}
+
+// DMC weights (DMC/S_matrix.py:4-24, dmc.py:80-92), one block:
+//   S = e_trial - e_est + e_cut / (1 + (v2 tau / N)^2), v2 = |grad_eff|^2 per walker,
+//   e_cut = min(min_b |e_est - eloc_b|, branchcut) * sign(e_est - eloc_b)  (ONE minimum over the
+//   batch: jnp.min of the stacked array), w *= exp(tau tdamp (S_new + S_old) / 2).
+template <typename T>
+__global__ __launch_bounds__(1024) void k_dmc_weights(int B, int N, const T* __restrict__ eold, const T* __restrict__ enew,
+                                                      const T* __restrict__ gold, const T* __restrict__ gnew,
+                                                      const double* __restrict__ tdamp, double tau, double e_trial,
+                                                      double e_est, double branchcut, T* __restrict__ w) {
+  __shared__ double mo[1024], mn[1024];
+  double a = branchcut, b = branchcut;
+  for (int i = threadIdx.x; i < B; i += 1024) {
+    a = fmin(a, fabs(e_est - (double)eold[i]));
+    b = fmin(b, fabs(e_est - (double)enew[i]));
+  }
+  mo[threadIdx.x] = a;
+  mn[threadIdx.x] = b;
+  __syncthreads();
+  for (int s = 512; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      mo[threadIdx.x] = fmin(mo[threadIdx.x], mo[threadIdx.x + s]);
+      mn[threadIdx.x] = fmin(mn[threadIdx.x], mn[threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  const double cut_o = mo[0], cut_n = mn[0];
+  const double td = tdamp[2];   // [sum proposed, sum new, tdamp] of aiqmc_dmc_drift_diffusion
+  for (int i = threadIdx.x; i < B; i += 1024) {
+    double vo = 0.0, vn = 0.0;
+    for (int k = 0; k < 3 * N; ++k) {
+      const double x = (double)gold[(size_t)i * 3 * N + k], y = (double)gnew[(size_t)i * 3 * N + k];
+      vo += x * x;
+      vn += y * y;
+    }
+    const double co = e_est - (double)eold[i], cn = e_est - (double)enew[i];
+    const double so = e_trial - e_est + cut_o * (double)((co > 0) - (co < 0)) / (1.0 + (vo * tau / N) * (vo * tau / N));
+    const double sn = e_trial - e_est + cut_n * (double)((cn > 0) - (cn < 0)) / (1.0 + (vn * tau / N) * (vn * tau / N));
+    w[i] = (T)(exp(tau * td * (0.5 * sn + 0.5 * so)) * (double)w[i]);
+  }
+}
+
+// Stochastic comb (DMC/branch.py:10-33), one block: cumulative weights in a fixed order, then
+// newinds[j] = searchsorted_left(cumsum, (u wtot + j wtot / n) mod wtot); wout[0] = wtot / n.
+template <typename T>
+__global__ __launch_bounds__(1024) void k_dmc_branch(int n, const T* __restrict__ w, double u, double* __restrict__ csum,
+                                                     int32_t* __restrict__ newinds, T* __restrict__ wout) {
+  if (threadIdx.x == 0) {
+    double a = 0.0;
+    for (int i = 0; i < n; ++i) {
+      a += (double)w[i];
+      csum[i] = a;
+    }
+  }
+  __syncthreads();
+  const double wtot = csum[n - 1];
+  for (int j = threadIdx.x; j < n; j += 1024) {
+    const double t = fmod(u * wtot + (double)j * (wtot / (double)n), wtot);
+    int lo = 0, hi = n;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (csum[mid] < t) lo = mid + 1;
+      else hi = mid;
+    }
+    newinds[j] = lo;
+  }
+  if (threadIdx.x == 0) wout[0] = (T)(wtot / (double)n);
+}
+
 // ============================================================================ host side
 
 static thread_local std::string g_err;
@@ -461,6 +571,100 @@ int aiqmc_debug_local_energy_forward(aiqmc_ctx* c, const void* pos, int32_t B, v
   return AIQMC_OK;
 }
 
+// One drift-diffusion Metropolis sweep (VMCmcstep.py:28-111), 7 launches; step = Philox counter,
+// st = index into host draws.  dmc (optional, device doubles [3]): DMC drift-diffusion extras
+// (DMC/drift_diffusion.py:15-22): dmc[0] = sum of the proposed coordinates, dmc[2] = tdamp =
+// sum(x_new) / dmc[0].
+static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double tstep, int rng_mode, const void* gauss1,
+                    const void* gauss2, const void* u, int st, uint64_t seed, uint64_t step, int32_t* accept_out,
+                    double* dmc, hipStream_t s) {
+  const int N = c->N;
+  const size_t es = c->dtype == AIQMC_F32 ? 4 : 8;
+  const char* g1;
+  const char* g2;
+  const char* uu;
+  if (rng_mode == AIQMC_RNG_HOST) {
+    g1 = (const char*)gauss1 + (size_t)st * B * 3 * N * es;
+    g2 = (const char*)gauss2 + (size_t)st * B * N * 3 * es;
+    uu = (const char*)u + (size_t)st * B * N * es;
+  } else {
+    const int nb = (B * N + 255) / 256;
+    if (c->dtype == AIQMC_F32)
+      k_draws<float><<<dim3(nb), dim3(256), 0, s>>>(seed, step, B, N, (float*)c->d_g1, (float*)c->d_g2,
+                                                     (float*)c->d_u);
+    else
+      k_draws<double><<<dim3(nb), dim3(256), 0, s>>>(seed, step, B, N, (double*)c->d_g1, (double*)c->d_g2,
+                                                      (double*)c->d_u);
+    g1 = (const char*)c->d_g1;
+    g2 = (const char*)c->d_g2;
+    uu = (const char*)c->d_u;
+  }
+  // (1) grad log|psi| at the walkers (VMCmcstep.py:41-53)
+  KArgs ka = base_args(c);
+  ka.nconf = B;
+  ka.pos = pos;
+  ka.logabs = c->d_lp;
+  ka.grad = c->d_grad;
+  ka.sumsq = c->d_sq;
+  ka.wcache = c->d_wc;
+  timed(c, 1, s, [&] { ops.walker(c->dtype, MODE_GRAD, ka, B, s); });
+  // (2) limdrift factor over the device batch (:60)
+  if (c->dtype == AIQMC_F32)
+    k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)c->d_sq, B, tstep, c->d_taueff);
+  else
+    k_taueff<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)c->d_sq, B, tstep, c->d_taueff);
+  // (3) single-electron proposals x^(i): value + gradient (:55-79, :95-97)
+  KArgs kp = base_args(c);
+  kp.nconf = B * N;
+  kp.pos = pos;
+  kp.proposal = 1;
+  kp.pgrad = c->d_grad;
+  kp.gauss1 = g1;
+  kp.taueff = c->d_taueff;
+  kp.tstep = tstep;
+  kp.seed = seed;
+  kp.step = step;
+  kp.logabs = c->d_lpn;
+  kp.gown = c->d_gown;
+  kp.sumsq = c->d_sqn;
+  if (c->reuse) {
+    // moved electron's local stage for all B*N proposals, then proposals from the walker caches
+    kp.wcache = c->d_wc;
+    kp.ecache = c->d_ec;
+    ops.moved(c->dtype, kp, s);
+  } else {
+    kp.wcache = c->d_wcp;   // per-proposal scratch of the same layout
+  }
+  timed(c, 0, s, [&] { ops.walker(c->dtype, MODE_GRAD, kp, B * N, s); });
+  // (4) limdrift factor of the proposal gradients over all B*N*3N entries (:80)
+  if (c->dtype == AIQMC_F32)
+    k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)c->d_sqn, B * N, tstep,
+                       c->d_taueff + 1);
+  else
+    k_taueff<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)c->d_sqn, B * N, tstep,
+                       c->d_taueff + 1);
+  if (dmc) {
+    if (c->dtype == AIQMC_F32)
+      k_dmc_sum<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)pos, (const float*)c->d_grad, (const float*)g1,
+                                                       c->d_taueff, tstep, B * 3 * N, dmc);
+    else
+      k_dmc_sum<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)pos, (const double*)c->d_grad,
+                                                        (const double*)g1, c->d_taueff, tstep, B * 3 * N, dmc);
+  }
+  // (5) acceptance and move (:83-106)
+  ops.accept(c->dtype, pos, c->d_grad, c->d_gown, c->d_lp, c->d_lpn, g1, g2, uu, c->d_taueff, B, tstep,
+             accept_out, s);
+    if (dmc) {
+    if (c->dtype == AIQMC_F32)
+      k_dmc_sum<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)pos, nullptr, nullptr, nullptr, tstep, B * 3 * N,
+                                                       dmc);
+    else
+      k_dmc_sum<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)pos, nullptr, nullptr, nullptr, tstep,
+                                                        B * 3 * N, dmc);
+  }
+  return 0;
+}
+
 int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tstep, int32_t rng_mode,
                   const void* gauss1, const void* gauss2, const void* u, uint64_t seed, uint64_t offset,
                   int32_t* accept_out, void* stream) {
@@ -485,73 +689,9 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
   const int N = c->N;
   const size_t es = c->dtype == AIQMC_F32 ? 4 : 8;
   for (int st = 0; st < nsteps; ++st) {
-    const uint64_t step = offset + (uint64_t)st;
-    const char* g1;
-    const char* g2;
-    const char* uu;
-    if (rng_mode == AIQMC_RNG_HOST) {
-      g1 = (const char*)gauss1 + (size_t)st * B * 3 * N * es;
-      g2 = (const char*)gauss2 + (size_t)st * B * N * 3 * es;
-      uu = (const char*)u + (size_t)st * B * N * es;
-    } else {
-      const int nb = (B * N + 255) / 256;
-      if (c->dtype == AIQMC_F32)
-        k_draws<float><<<dim3(nb), dim3(256), 0, s>>>(seed, step, B, N, (float*)c->d_g1, (float*)c->d_g2,
-                                                       (float*)c->d_u);
-      else
-        k_draws<double><<<dim3(nb), dim3(256), 0, s>>>(seed, step, B, N, (double*)c->d_g1, (double*)c->d_g2,
-                                                        (double*)c->d_u);
-      g1 = (const char*)c->d_g1;
-      g2 = (const char*)c->d_g2;
-      uu = (const char*)c->d_u;
-    }
-    // (1) grad log|psi| at the walkers (VMCmcstep.py:41-53)
-    KArgs ka = base_args(c);
-    ka.nconf = B;
-    ka.pos = pos;
-    ka.logabs = c->d_lp;
-    ka.grad = c->d_grad;
-    ka.sumsq = c->d_sq;
-    ka.wcache = c->d_wc;
-    timed(c, 1, s, [&] { ops.walker(c->dtype, MODE_GRAD, ka, B, s); });
-    // (2) limdrift factor over the device batch (:60)
-    if (c->dtype == AIQMC_F32)
-      k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)c->d_sq, B, tstep, c->d_taueff);
-    else
-      k_taueff<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)c->d_sq, B, tstep, c->d_taueff);
-    // (3) single-electron proposals x^(i): value + gradient (:55-79, :95-97)
-    KArgs kp = base_args(c);
-    kp.nconf = B * N;
-    kp.pos = pos;
-    kp.proposal = 1;
-    kp.pgrad = c->d_grad;
-    kp.gauss1 = g1;
-    kp.taueff = c->d_taueff;
-    kp.tstep = tstep;
-    kp.seed = seed;
-    kp.step = step;
-    kp.logabs = c->d_lpn;
-    kp.gown = c->d_gown;
-    kp.sumsq = c->d_sqn;
-    if (c->reuse) {
-      // moved electron's local stage for all B*N proposals, then proposals from the walker caches
-      kp.wcache = c->d_wc;
-      kp.ecache = c->d_ec;
-      ops.moved(c->dtype, kp, s);
-    } else {
-      kp.wcache = c->d_wcp;   // per-proposal scratch of the same layout
-    }
-    timed(c, 0, s, [&] { ops.walker(c->dtype, MODE_GRAD, kp, B * N, s); });
-    // (4) limdrift factor of the proposal gradients over all B*N*3N entries (:80)
-    if (c->dtype == AIQMC_F32)
-      k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)c->d_sqn, B * N, tstep,
-                         c->d_taueff + 1);
-    else
-      k_taueff<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)c->d_sqn, B * N, tstep,
-                         c->d_taueff + 1);
-    // (5) acceptance and move (:83-106)
-    ops.accept(c->dtype, pos, c->d_grad, c->d_gown, c->d_lp, c->d_lpn, g1, g2, uu, c->d_taueff, B, tstep,
-               accept_out, s);
+    rc = mc_sweep(c, ops, pos, B, tstep, rng_mode, gauss1, gauss2, u, st, seed, offset + (uint64_t)st, accept_out,
+                  nullptr, s);
+    if (rc) return rc;
   }
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
@@ -746,6 +886,101 @@ int aiqmc_local_energy_ecp(aiqmc_ctx* c, const void* pos, int32_t B, int32_t rng
   // (5) local pp part + nonlocal quadrature sum
   if (f32) k_ecp_energy<float><<<dim3(B), dim3(64), 0, s>>>(ea);
   else k_ecp_energy<double><<<dim3(B), dim3(64), 0, s>>>(ea);
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_dmc_drift_diffusion(aiqmc_ctx* c, void* pos, int32_t B, double tstep, int32_t rng_mode, const void* gauss1,
+                              const void* gauss2, const void* u, uint64_t seed, uint64_t offset, void* grad_eff_old,
+                              void* grad_new_eff, double* tdamp, void* stream) {
+  int rc = check_call(c, pos, B);
+  if (rc) return rc;
+  if (!(tstep > 0.0)) return fail(AIQMC_EINVAL, "tstep must be > 0");
+  if (rng_mode == AIQMC_RNG_HOST && (!gauss1 || !gauss2 || !u))
+    return fail(AIQMC_EINVAL, "AIQMC_RNG_HOST needs gauss1, gauss2 and u");
+  if (rng_mode != AIQMC_RNG_HOST && rng_mode != AIQMC_RNG_PHILOX) return fail(AIQMC_EINVAL, "rng_mode");
+  if (!grad_eff_old || !grad_new_eff || !tdamp) return fail(AIQMC_EINVAL, "null output");
+  if (B == 0) return AIQMC_OK;
+  HIPCHK(hipSetDevice(c->device));
+  rc = ensure_ws(c, B);
+  if (rc) return rc;
+  ShapeOps ops;
+  shape_ops(c->N, c->A, &ops);
+  if (!c->reuse) {
+    rc = ensure_wcp(c, (int64_t)B * c->N, ops);
+    if (rc) return rc;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int n = B * 3 * c->N;
+  const int nb = (n + 255) / 256;
+  rc = mc_sweep(c, ops, pos, B, tstep, rng_mode, gauss1, gauss2, u, 0, seed, offset, nullptr, tdamp, s);
+  if (rc) return rc;
+  // grad_eff_old: limdrift of the walker gradients of this sweep (drift_diffusion.py:60-61)
+  if (c->dtype == AIQMC_F32)
+    k_scale_grad<float><<<dim3(nb), dim3(256), 0, s>>>((const float*)c->d_grad, c->d_taueff, n, (float*)grad_eff_old);
+  else
+    k_scale_grad<double><<<dim3(nb), dim3(256), 0, s>>>((const double*)c->d_grad, c->d_taueff, n,
+                                                         (double*)grad_eff_old);
+  // grad_new_eff_s: limdrift of the gradients at the moved walkers (:103-104)
+  KArgs ka = base_args(c);
+  ka.nconf = B;
+  ka.pos = pos;
+  ka.grad = grad_new_eff;
+  ka.sumsq = c->d_sq;
+  ka.wcache = c->d_wc;
+  ops.walker(c->dtype, MODE_GRAD, ka, B, s);
+  if (c->dtype == AIQMC_F32) {
+    k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)c->d_sq, B, tstep, c->d_taueff + 1);
+    k_scale_grad<float><<<dim3(nb), dim3(256), 0, s>>>((const float*)grad_new_eff, c->d_taueff + 1, n,
+                                                        (float*)grad_new_eff);
+  } else {
+    k_taueff<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)c->d_sq, B, tstep, c->d_taueff + 1);
+    k_scale_grad<double><<<dim3(nb), dim3(256), 0, s>>>((const double*)grad_new_eff, c->d_taueff + 1, n,
+                                                         (double*)grad_new_eff);
+  }
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_dmc_weights(aiqmc_ctx* c, int32_t B, const void* eloc_old, const void* eloc_new, const void* grad_eff_old,
+                      const void* grad_new_eff, const double* tdamp, double tstep, double e_trial, double e_est,
+                      double branchcut, void* weights_inout, void* stream) {
+  if (!c) return fail(AIQMC_EINVAL, "null context");
+  if (B < 0) return fail(AIQMC_EINVAL, "negative batch");
+  if (B == 0) return AIQMC_OK;
+  if (!eloc_old || !eloc_new || !grad_eff_old || !grad_new_eff || !tdamp || !weights_inout)
+    return fail(AIQMC_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (c->dtype == AIQMC_F32)
+    k_dmc_weights<float><<<dim3(1), dim3(1024), 0, s>>>(B, c->N, (const float*)eloc_old, (const float*)eloc_new,
+                                                         (const float*)grad_eff_old, (const float*)grad_new_eff, tdamp,
+                                                         tstep, e_trial, e_est, branchcut, (float*)weights_inout);
+  else
+    k_dmc_weights<double><<<dim3(1), dim3(1024), 0, s>>>(B, c->N, (const double*)eloc_old, (const double*)eloc_new,
+                                                          (const double*)grad_eff_old, (const double*)grad_new_eff,
+                                                          tdamp, tstep, e_trial, e_est, branchcut,
+                                                          (double*)weights_inout);
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_dmc_branch(aiqmc_ctx* c, int32_t B, const void* weights, double u, int32_t* newinds, void* weight_out,
+                     void* stream) {
+  if (!c) return fail(AIQMC_EINVAL, "null context");
+  if (B <= 0) return fail(AIQMC_EINVAL, "empty batch");
+  if (!weights || !newinds || !weight_out) return fail(AIQMC_EINVAL, "null argument");
+  if (!(u >= 0.0 && u < 1.0)) return fail(AIQMC_EINVAL, "u must be in [0, 1)");
+  HIPCHK(hipSetDevice(c->device));
+  double* csum = nullptr;
+  HIPCHK(hipMallocAsync((void**)&csum, (size_t)B * sizeof(double), (hipStream_t)stream));
+  hipStream_t s = (hipStream_t)stream;
+  if (c->dtype == AIQMC_F32)
+    k_dmc_branch<float><<<dim3(1), dim3(1024), 0, s>>>(B, (const float*)weights, u, csum, newinds, (float*)weight_out);
+  else
+    k_dmc_branch<double><<<dim3(1), dim3(1024), 0, s>>>(B, (const double*)weights, u, csum, newinds,
+                                                         (double*)weight_out);
+  HIPCHK(hipFreeAsync(csum, s));
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
 }

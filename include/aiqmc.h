@@ -114,6 +114,30 @@ int aiqmc_mc_step(aiqmc_ctx* ctx, void* pos_inout, int32_t B, int32_t nsteps, do
 int aiqmc_logpsi_param_grad(aiqmc_ctx* ctx, const void* pos, int32_t B, const void* weights, void* out,
                             void* logabs, void* stream);
 
+/* DMC drift-diffusion step (DMC/drift_diffusion.py:25-107): one Metropolis sweep
+ * exactly as aiqmc_mc_step with nsteps = 1 (same draws, in place), plus
+ *   grad_eff_old[B*3N]  limdrift(grad log|psi|) at the walkers before the move (:60-61),
+ *   grad_new_eff[B*3N]  limdrift(grad log|psi|) at the moved walkers (:103-104),
+ *   tdamp[3]            device doubles: [sum of proposed coordinates, sum of new
+ *                       coordinates, tdamp = their ratio] (walkers_accept :21). */
+int aiqmc_dmc_drift_diffusion(aiqmc_ctx* ctx, void* pos_inout, int32_t B, double tstep, int32_t rng_mode,
+                              const void* gauss1, const void* gauss2, const void* u, uint64_t seed, uint64_t offset,
+                              void* grad_eff_old, void* grad_new_eff, double* tdamp, void* stream);
+
+/* DMC weight update (DMC/S_matrix.py:4-24, dmc.py:80-92): with S from the real
+ * local energies eloc_old/eloc_new [B], v2 = |grad_eff|^2 per walker and the tdamp[3]
+ * array of aiqmc_dmc_drift_diffusion (its entry 2 is used),
+ * weights[B] *= exp(tstep tdamp (S_new + S_old)/2). */
+int aiqmc_dmc_weights(aiqmc_ctx* ctx, int32_t B, const void* eloc_old, const void* eloc_new, const void* grad_eff_old,
+                      const void* grad_new_eff, const double* tdamp, double tstep, double e_trial, double e_est,
+                      double branchcut, void* weights_inout, void* stream);
+
+/* Stochastic comb (DMC/branch.py:10-33) with the uniform draw u in [0,1):
+ * newinds[B] (int32, device) = searchsorted(cumsum(w), (u wtot + j wtot/B) mod wtot),
+ * weight_out[1] = wtot / B (device, ctx dtype). */
+int aiqmc_dmc_branch(aiqmc_ctx* ctx, int32_t B, const void* weights, double u, int32_t* newinds, void* weight_out,
+                     void* stream);
+
 /* Pseudopotential tables (pphamiltonian.local_energy arguments,
  * Energy/pphamiltonian.py:130-146; shapes as the example drivers pass them,
  * example/single_atom_C/single_atom_C.py:13-23).  All HOST pointers; the

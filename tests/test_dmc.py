@@ -1,0 +1,132 @@
+"""DMC pieces (AIQMCrelease3/DMC): drift-diffusion step, S / weight update, stochastic comb.
+CPU: the oracle against closed forms; GPU: the HIP path against the oracle (fp64; E_L,
+weights and positions to 1e-9, indices exact).  T-moves (DMC/Tmoves.py) are not built
+(see DESIGN.md)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import dmc as odmc
+
+
+def test_comb_closed_form():
+    w = np.array([0.5, 1.5, 1.0, 1.0])
+    wn, idx = odmc.branch(w, 0.1)
+    # cumsum [0.5, 2, 3, 4]; targets (0.4 + [0, 1, 2, 3]) % 4 = [0.4, 1.4, 2.4, 3.4]
+    np.testing.assert_array_equal(idx, [0, 1, 2, 3])
+    assert wn == 1.0
+    wn, idx = odmc.branch(np.array([3.0, 0.0, 0.5, 0.5]), 0.0)
+    np.testing.assert_array_equal(idx, [0, 0, 0, 0])   # cumsum [3, 3, 3.5, 4], targets [0, 1, 2, 3]
+
+
+def test_comput_S_single_global_cut():
+    eloc = np.array([-1.0, -3.0, -2.5])
+    v2 = np.zeros((3, 6))
+    S = odmc.comput_S(e_trial=-2.0, e_est=-2.0, branchcut=10.0, v2=v2, tau=0.01, eloc=eloc, nelec=2)
+    # e_est - eloc = [-1, 1, 0.5]; ONE cut = min(|.|, 10) = 0.5 for every walker (D1)
+    np.testing.assert_allclose(S, [-0.5, 0.5, 0.5])
+
+
+def _ctx(name, dtype=torch.float64):
+    from oracle import system
+    from aiqmc import _lib
+    s = system.make_system(name)
+    t = s.tables()
+    ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
+                       t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"], dtype=dtype, device=0)
+    return s, ctx
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["Be", "N2"])
+def test_drift_diffusion_matches_oracle(name):
+    from oracle import network, system
+    s, ctx = _ctx(name)
+    rng = np.random.default_rng(17)
+    params = system.init_params(rng, s, randomize_aux=True)
+    ctx.set_params(system.flatten_params(params))
+    B, N = 6, s.nelectrons
+    x = torch.tensor(system.init_electrons(rng, s.atoms, s.charges, B, 1.0))
+    g1 = torch.tensor(rng.standard_normal((B, 3 * N)))
+    g2 = torch.tensor(rng.standard_normal((B, N, 3 * N)))
+    u = torch.tensor(rng.uniform(size=(B, N)))
+    xr, td_r, go_r, gn_r = odmc.drift_diffusion(network.Network(s), network.to_torch(params), x.clone(), g1, g2, u, 0.05)
+    pos = x.cuda().contiguous()
+    idx = torch.arange(N)
+    g2d = g2.reshape(B, N, N, 3)[:, idx, idx, :].contiguous()
+    go, gn, td = ctx.dmc_drift_diffusion(pos, 0.05, gauss1=g1[None], gauss2=g2d[None], u=u[None])
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(pos.cpu().numpy(), xr.numpy(), rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(go.cpu().numpy(), go_r.numpy(), rtol=1e-8, atol=1e-9)
+    np.testing.assert_allclose(gn.cpu().numpy(), gn_r.numpy(), rtol=1e-8, atol=1e-9)
+    assert abs(td[2].item() - td_r.item()) < 1e-10
+
+
+@pytest.mark.gpu
+def test_weights_and_branch_match_oracle():
+    s, ctx = _ctx("Be")
+    rng = np.random.default_rng(4)
+    B, N = 300, s.nelectrons
+    eo, en = rng.normal(-14.6, 0.4, B), rng.normal(-14.6, 0.4, B)
+    go, gn = rng.standard_normal((B, 3 * N)), rng.standard_normal((B, 3 * N))
+    w0 = rng.uniform(0.5, 1.5, B)
+    tdamp = torch.tensor([0.0, 0.0, 0.97], dtype=torch.float64, device="cuda")
+    w = torch.tensor(w0, device="cuda")
+    ctx.dmc_weights(w, torch.tensor(eo), torch.tensor(en), torch.tensor(go, device="cuda"),
+                    torch.tensor(gn, device="cuda"), tdamp, 0.01, -14.5, -14.62, 0.3)
+    S_old = odmc.comput_S(-14.5, -14.62, 0.3, go ** 2, 0.01, eo, N)
+    S_new = odmc.comput_S(-14.5, -14.62, 0.3, gn ** 2, 0.01, en, N)
+    w_ref = odmc.update_weights(w0, 0.01, 0.97, S_new, S_old)
+    np.testing.assert_allclose(w.cpu().numpy(), w_ref, rtol=1e-12)
+    wn, idx = ctx.dmc_branch(w, 0.37)
+    wn_r, idx_r = odmc.branch(w_ref, 0.37)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(idx.cpu().numpy(), idx_r)
+    assert abs(wn.item() - wn_r) < 1e-12
+
+
+def test_comput_S_dropin_matches_oracle():
+    from aiqmc.DMC.S_matrix import comput_S
+    rng = np.random.default_rng(2)
+    eloc = rng.normal(-5, 1, 40)
+    v2 = rng.standard_normal((40, 12)) ** 2
+    got = comput_S(-5.1, -5.0, 0.7, torch.tensor(v2), 0.02, torch.tensor(eloc), 4).numpy()
+    np.testing.assert_allclose(got, odmc.comput_S(-5.1, -5.0, 0.7, v2, 0.02, eloc, 4), rtol=1e-14)
+
+
+@pytest.mark.gpu
+def test_dmc_propagate_step_c_atom():
+    """One dmc_propagate_run step (drift-diffusion + pp energies + weights) on the C-atom ccECP
+    config driven like main_dmc.py:123-177: finite energies, positive weights, and the same
+    positions as the stand-alone drift-diffusion step with the same Philox key."""
+    from oracle import pphamiltonian as opp, system
+    from aiqmc import spin_indices
+    from aiqmc.DMC import dmc
+    from aiqmc.DMC.drift_diffusion import propose_drift_diffusion
+    from aiqmc.VMC.VMCmcstep import PhiloxKey
+    from aiqmc.wavefunction_Ynlm import nn
+    s = system.make_system("C_ecp")
+    par, anti, npar, nanti = spin_indices.jastrow_indices_ee(spins=s.spins, nelectrons=4)
+    up, dn = spin_indices.spin_indices_h(s.spins)
+    network = nn.make_ai_net(ndim=3, nelectrons=4, natoms=1, nspins=(2, 2), charges=s.charges,
+                             parallel_indices=par, antiparallel_indices=anti, n_parallel=npar,
+                             n_antiparallel=nanti, spin_up_indices=up, spin_down_indices=dn)
+    params = system.init_params(np.random.default_rng(8), s, randomize_aux=True)
+    e = opp.c_atom_ccecp()
+    B = 256
+    pos = torch.tensor(system.init_electrons(np.random.default_rng(9), s.atoms, s.charges, B, 1.0), device="cuda")
+    data = nn.AINetData(positions=pos, spins=s.spins, atoms=s.atoms, charges=s.charges)
+    run = dmc.dmc_propagate(network.apply, None, network.apply, 2, 4, 1, 3, B, 0.01, 1, s.charges, s.spins,
+                            e.rn_local, e.local_coes, e.local_exps, e.rn_non_local, e.non_local_coes,
+                            e.non_local_exps)
+    w0 = torch.ones(B, dtype=torch.float64, device="cuda")
+    eloc, w, new = run(params, PhiloxKey(3, 0), data, w0, torch.full((B,), 10.0), -3.0, -3.1)
+    torch.cuda.synchronize()
+    assert torch.isfinite(eloc.real).all() and torch.isfinite(w).all() and bool((w > 0).all())
+    # same drift-diffusion step outside: identical positions (deterministic Philox draws)
+    dd = propose_drift_diffusion(network.apply, 0.01, 3, 4, B)
+    new2, _, td, go, gn = dd(params, PhiloxKey(3, 0), data)
+    torch.cuda.synchronize()
+    assert torch.equal(new.positions, new2.positions)
