@@ -266,6 +266,7 @@ static int ensure_ws(aiqmc_ctx* c, int B) {
     tot += (int64_t)bytes[k];
   }
   HIPCHK(hipMalloc((void**)&c->d_taueff, 2 * sizeof(double)));
+
   c->ws_B = B;
   c->ws_bytes = tot + 16;
   return 0;
@@ -571,7 +572,7 @@ int aiqmc_debug_local_energy_forward(aiqmc_ctx* c, const void* pos, int32_t B, v
   return AIQMC_OK;
 }
 
-// One drift-diffusion Metropolis sweep (VMCmcstep.py:28-111), 7 launches; step = Philox counter,
+// One drift-diffusion Metropolis sweep (VMCmcstep.py:28-111), 6 launches; step = Philox counter,
 // st = index into host draws.  dmc (optional, device doubles [3]): DMC drift-diffusion extras
 // (DMC/drift_diffusion.py:15-22): dmc[0] = sum of the proposed coordinates, dmc[2] = tdamp =
 // sum(x_new) / dmc[0].
@@ -587,14 +588,7 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
     g1 = (const char*)gauss1 + (size_t)st * B * 3 * N * es;
     g2 = (const char*)gauss2 + (size_t)st * B * N * 3 * es;
     uu = (const char*)u + (size_t)st * B * N * es;
-  } else {
-    const int nb = (B * N + 255) / 256;
-    if (c->dtype == AIQMC_F32)
-      k_draws<float><<<dim3(nb), dim3(256), 0, s>>>(seed, step, B, N, (float*)c->d_g1, (float*)c->d_g2,
-                                                     (float*)c->d_u);
-    else
-      k_draws<double><<<dim3(nb), dim3(256), 0, s>>>(seed, step, B, N, (double*)c->d_g1, (double*)c->d_g2,
-                                                      (double*)c->d_u);
+  } else {   // drawn by the walker launch below (k_draws' arithmetic, fused)
     g1 = (const char*)c->d_g1;
     g2 = (const char*)c->d_g2;
     uu = (const char*)c->d_u;
@@ -607,6 +601,14 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
   ka.grad = c->d_grad;
   ka.sumsq = c->d_sq;
   ka.wcache = c->d_wc;
+  ka.tstep = tstep;
+  ka.seed = seed;
+  ka.step = step;
+  if (rng_mode != AIQMC_RNG_HOST) {
+    ka.dg1 = c->d_g1;
+    ka.dg2 = c->d_g2;
+    ka.du = c->d_u;
+  }
   timed(c, 1, s, [&] { ops.walker(c->dtype, MODE_GRAD, ka, B, s); });
   // (2) limdrift factor over the device batch (:60)
   if (c->dtype == AIQMC_F32)

@@ -54,6 +54,11 @@ struct KArgs {
   int mper, mdiv;
   const void* xnew;
   int value_only;         // k_walker_rev: log|psi| and phase only (no backward pass)
+  // walker launch of a Metropolis sweep (k_walker_rev, PROP = false): dg1/dg2/du != nullptr:
+  // lanes e < N of wave b write the sweep's Philox draws of walker b exactly as k_draws would
+  // (one launch fewer per sweep).  (Fusing the limdrift reduction the same way, by the last wave
+  // to finish, was measured 3.5x slower: every wave's device-scope fence writes back its L2.)
+  void *dg1, *dg2, *du;
   // Metropolis caches (walker_rev.h WCache / ECache); nullptr outside aiqmc_mc_step
   void* wcache;
   void* ecache;

@@ -970,6 +970,21 @@ k_walker_rev(KArgs ka) {
     if (ka.phase) ((T*)ka.phase)[conf] = f_atan2(phi, phr);
     if (ka.sumsq) ((T*)ka.sumsq)[conf] = sumsq;
   }
+  if constexpr (!PREP) {
+    if (ka.dg1 && !ka.proposal && lane < N) {   // the sweep's draws of walker conf (k_draws)
+      const uint32_t t = (uint32_t)(conf * N + lane);
+      float a[3], b[3], c[4];
+      philox_normal3f(ka.seed, ka.step, t, 0u, a);
+      philox_normal3f(ka.seed, ka.step, t, 1u, b);
+      philox_u4(ka.seed, ka.step, t, 2u, c);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        ((T*)ka.dg1)[(size_t)t * 3 + k] = (T)a[k];
+        ((T*)ka.dg2)[(size_t)t * 3 + k] = (T)b[k];
+      }
+      ((T*)ka.du)[t] = (T)(c[0] - 5.9604644775390625e-08f);
+    }
+  }
   AQ_PH(9);
 }
 
