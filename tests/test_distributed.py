@@ -74,3 +74,46 @@ def test_single_process_collectives_are_identity():
     assert constants.all_gather(x).shape == (1, 2)
     m, v = constants.pmean_stats(torch.tensor([1.0, 3.0]))
     assert float(m) == 2.0 and float(v) == 1.0
+
+
+def _clip_worker(rank, world, port, q):
+    import sys
+    from conftest import PKG
+    sys.path.insert(0, PKG)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from aiqmc import constants
+    from aiqmc.Loss.loss import clip_local_values
+    e_all = np.random.default_rng(11).normal(-14.6, 0.5, size=64 * world)
+    e_all[5] = 3.0                                                      # outlier clipped by the 5-TV window
+    e = torch.tensor(e_all[64 * rank:64 * (rank + 1)])
+    loss = constants.pmean(torch.mean(e))
+    center, diff = clip_local_values(e, loss, 5.0, False, True)
+    g = constants.pmean(torch.tensor(np.full(7, float(rank))))          # the gradient pmean (adam.py:55)
+    q.put((rank, float(loss), float(center), diff.numpy(), g.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_clipping_and_gradient_pmean_match_global(world):
+    """loss.py:73-135 statistics over ranks (pmean'd mean, TV and clipped mean) equal the
+    single-device computation on the concatenated batch; the gradient pmean is the rank mean."""
+    from oracle import loss as oloss
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_clip_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+    e_all = np.random.default_rng(11).normal(-14.6, 0.5, size=64 * world)
+    e_all[5] = 3.0
+    center, diff = oloss.clip_local_values(e_all, e_all.mean(), 5.0)
+    for r in res:
+        assert abs(r[1] - e_all.mean()) < 1e-12 and abs(r[2] - center) < 1e-12
+        np.testing.assert_allclose(r[3], diff[64 * r[0]:64 * (r[0] + 1)], rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(r[4], np.full(7, (world - 1) / 2.0))
