@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
     ap.add_argument("--system", default="N2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-walkers", type=int, default=8)
+    ap.add_argument("--cpu-sample-walkers", type=int, default=64)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     ap.add_argument("--no-ecp", action="store_true", help="skip the C-atom ccECP local-energy side measurement")
     ap.add_argument("--no-adam", action="store_true", help="skip the Be-atom Adam training-step side measurement")
@@ -105,18 +105,27 @@ def cpu_baseline(name, params, atoms, charges, nsteps_unused, tstep, sample_walk
     g1 = torch.tensor(rng.standard_normal((B, 3 * N)))
     g2 = torch.tensor(rng.standard_normal((B, N, 3 * N)))
     u = torch.tensor(rng.uniform(size=(B, N)))
-    t0 = time.perf_counter()
-    mcstep.walkers_update(net, pt, x, g1, g2, u, tstep)
-    t_mc = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    hamiltonian.batch_local_energy(net, pt, x[:max(1, B // 2)])
-    t_el = time.perf_counter() - t0
+    # time-bounded sample (~10 s per leg): repeat until the leg has run for at least `target` s
+    target = 8.0
+    t_mc, n_mc = 0.0, 0
+    while t_mc < target:
+        t0 = time.perf_counter()
+        mcstep.walkers_update(net, pt, x, g1, g2, u, tstep)
+        t_mc += time.perf_counter() - t0
+        n_mc += B
+    be = 4
+    t_el, n_el = 0.0, 0
+    while t_el < target:
+        t0 = time.perf_counter()
+        hamiltonian.batch_local_energy(net, pt, x[:be])
+        t_el += time.perf_counter() - t0
+        n_el += be
     return {
-        "value": B / t_mc, "unit": "walker*steps/s", "cores": threads, "kind": "port",
-        "local_energy_evals_per_s": max(1, B // 2) / t_el,
+        "value": n_mc / t_mc, "unit": "walker*steps/s", "cores": threads, "kind": "port",
+        "local_energy_evals_per_s": n_el / t_el,
         "sample": f"float64 oracle (torch CPU, jvp-of-grad Laplacian, per-electron-config MH) on {name}: "
-                  f"1 Metropolis sweep of {B} walkers ({t_mc:.1f}s) + local energy of {max(1, B // 2)} "
-                  f"walkers ({t_el:.1f}s)",
+                  f"{n_mc // B} Metropolis sweeps of {B} walkers ({t_mc:.1f}s) + local energy of {n_el} "
+                  f"walkers in batches of {be} ({t_el:.1f}s)",
     }
 
 
