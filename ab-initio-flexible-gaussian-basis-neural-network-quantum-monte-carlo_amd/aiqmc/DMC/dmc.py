@@ -1,14 +1,15 @@
-"""One DMC propagation step (drop-in for AIQMCrelease3/DMC/dmc.py:13-93), T-moves excluded.
+"""One DMC propagation step (drop-in for AIQMCrelease3/DMC/dmc.py:13-93).
 
 ``dmc_propagate(signed_network, log_network, logabs_f, list_l, nelectrons, natoms, ndim,
 batch_size, tstep, nsteps, charges, spins, Rn_local, ...)`` returns
 ``dmc_propagate_run(params, key, data, weights, branchcut_start, e_trial, e_est) ->
-(eloc_new, weights, new_data)``: drift-diffusion (aiqmc_dmc_drift_diffusion), the complex
-pseudopotential local energies before and after (aiqmc_local_energy_ecp), and the weight
-update with the S factors (aiqmc_dmc_weights).  The reference first applies T-moves
-(DMC/Tmoves.py), whose amplitude bookkeeping hard-codes the slice layout of a 3-atom system
-(back_amplitudes[:, 1:19] ... [:, 79:151]) and compares complex amplitudes with `>`; they are
-not built here, so this step is the reference's propagation without the T-move proposal.
+(eloc_new, weights, new_data)``, in the reference's order (dmc.py:79-93): T-moves
+(aiqmc_dmc_tmoves, DMC/Tmoves.py with its quirks T1-T8), drift-diffusion of the T-moved
+walkers (aiqmc_dmc_drift_diffusion), the complex pseudopotential local energies of the
+walkers before the T-moves and after the drift-diffusion (aiqmc_local_energy_ecp), and the
+weight update with the S factors (aiqmc_dmc_weights).  Every stage is a batched GPU launch
+sequence; the draws come from one PhiloxKey per call (the reference reuses one device key for
+all stages and walkers; threefry bits are out of scope).
 """
 from __future__ import annotations
 
@@ -16,6 +17,8 @@ import torch
 
 from ..Energy import pphamiltonian
 from ..VMC.VMCmcstep import PhiloxKey
+from ..wavefunction_Ynlm.nn import AINetData
+from .Tmoves import compute_tmoves
 from .drift_diffusion import propose_drift_diffusion
 
 
@@ -30,11 +33,15 @@ def dmc_propagate(signed_network, log_network, logabs_f, list_l: int, nelectrons
                                     non_local_exps=Non_local_exps, natoms=natoms, nelectrons=nelectrons, ndim=ndim,
                                     list_l=list_l)
     net = signed_network._aiqmc_network
+    tm = compute_tmoves(list_l, tstep, nelectrons, natoms, ndim, signed_network, Rn_non_local, Non_local_coes,
+                        Non_local_exps)
 
     def dmc_propagate_run(params, key, data, weights: torch.Tensor, branchcut_start, e_trial, e_est):
         k = key if isinstance(key, PhiloxKey) else PhiloxKey(int(key), 0)
+        pos_t, _ = tm(data, params, PhiloxKey(k.seed + 3, k.offset))
+        t_move_data = AINetData(positions=pos_t, spins=data.spins, atoms=data.atoms, charges=data.charges)
         eloc_old, _ = le(params, PhiloxKey(k.seed + 1, k.offset), data)
-        new_data, _, tdamp_scalar, go, gn = dd(params, k, data)
+        new_data, _, tdamp_scalar, go, gn = dd(params, k, t_move_data)
         eloc_new, _ = le(params, PhiloxKey(k.seed + 2, k.offset), new_data)
         ctx = net.bind(params, data.atoms, go.dtype)
         td = torch.zeros(3, dtype=torch.float64, device=go.device)

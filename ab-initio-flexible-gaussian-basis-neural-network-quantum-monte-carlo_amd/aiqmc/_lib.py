@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_profile_enable", "aiqmc_profile_read", "aiqmc_debug_logpsi_grad_forward",
     "aiqmc_debug_set_proposal_reuse", "aiqmc_debug_phase_cycles", "aiqmc_debug_local_energy_forward",
     "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
-    "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch",
+    "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -114,6 +114,7 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_dmc_drift_diffusion.argtypes = [vp, vp, i32, dbl, i32, vp, vp, vp, u64, u64, vp, vp, vp, vp]
     lib.aiqmc_dmc_weights.argtypes = [vp, i32, vp, vp, vp, vp, vp, dbl, dbl, dbl, dbl, vp, vp]
     lib.aiqmc_dmc_branch.argtypes = [vp, i32, vp, dbl, vp, vp, vp]
+    lib.aiqmc_dmc_tmoves.argtypes = [vp, vp, i32, dbl, i32, vp, vp, vp, u64, u64, vp, vp]
     lib.aiqmc_set_ecp.argtypes = [vp, ctypes.POINTER(AiqmcEcp)]
     lib.aiqmc_local_energy_ecp.argtypes = [vp, vp, i32, i32, vp, ctypes.c_uint64, ctypes.c_uint64, vp, vp, vp,
                                            vp, vp]
@@ -366,6 +367,31 @@ class Context:
         check(self._lib.aiqmc_dmc_branch(self._h, B, _ptr(w), float(u), _ptr(idx), _ptr(wo), _stream(self.device)),
               "aiqmc_dmc_branch")
         return wo, idx
+
+    def dmc_tmoves(self, pos: torch.Tensor, tstep: float, rot=None, u_sel=None, u_acc=None, seed: int = 0,
+                   offset: int = 0):
+        """In-place T-moves (DMC/Tmoves.py:32-225) on `pos`; returns the acceptance [B, N].
+        rot [B,3,3], u_sel [B], u_acc [B,N]: injected draws (parity mode); all None: Philox."""
+        if not (pos.is_cuda and pos.dtype == self.dtype and pos.is_contiguous()):
+            raise ValueError("dmc_tmoves needs a contiguous device tensor of the context dtype (updated in place)")
+        B = pos.numel() // (3 * self.N)
+        host = rot is not None
+        if host != (u_sel is not None) or host != (u_acc is not None):
+            raise ValueError("rot, u_sel and u_acc are injected together or not at all")
+        dev = lambda t, n: None if t is None else self._dev(t, n)
+        r, us, ua = dev(rot, 9 * B), dev(u_sel, B), dev(u_acc, B * self.N)
+        acc = torch.empty(B, self.N, dtype=self.dtype, device=self.device)
+        check(self._lib.aiqmc_dmc_tmoves(self._h, _ptr(pos), B, float(tstep), AIQMC_RNG_HOST if host else
+                                         AIQMC_RNG_PHILOX, _ptr(r), _ptr(us), _ptr(ua), ctypes.c_uint64(seed),
+                                         ctypes.c_uint64(offset), _ptr(acc), _stream(self.device)),
+              "aiqmc_dmc_tmoves")
+        return acc
+
+    def _dev(self, t, n: int) -> torch.Tensor:
+        t = torch.as_tensor(t).to(self.device, self.dtype).contiguous()
+        if t.numel() != n:
+            raise ValueError(f"expected {n} values, got {t.numel()}")
+        return t
 
     def set_ecp(self, rn_local, local_coes, local_exps, rn_non_local, non_local_coes, non_local_exps,
                 list_l: int):

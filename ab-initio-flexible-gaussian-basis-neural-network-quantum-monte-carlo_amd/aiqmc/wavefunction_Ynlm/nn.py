@@ -207,3 +207,20 @@ def make_ai_net(nspins, charges, parallel_indices, antiparallel_indices, spin_up
     apply_fn = lambda *a, **k: apply(*a, **k)
     apply_fn._aiqmc_network = net
     return Network(init=net.init, apply=apply_fn, orbitals=net.orbitals)
+
+
+def make_log_network(signed_network):
+    """The complex log the pp drivers build from the signed network
+    (``log_network`` in DMC/main_dmc.py:91-93, main_pp_adam_muti_GPU.py:119-121):
+    log|psi| + i phase, tagged with the aiqmc network so that the pp / T-move drop-ins
+    can dispatch to the kernels."""
+    net = getattr(signed_network, "_aiqmc_network", None)
+    if net is None:
+        raise TypeError("make_log_network: signed_network must be an aiqmc make_ai_net apply")
+
+    def log_network(*args, **kwargs):
+        phase, mag = signed_network(*args, **kwargs)
+        return mag + 1j * phase
+
+    log_network._aiqmc_network = net
+    return log_network

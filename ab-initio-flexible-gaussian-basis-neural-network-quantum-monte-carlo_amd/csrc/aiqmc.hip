@@ -404,6 +404,7 @@ int aiqmc_destroy(aiqmc_ctx* c) {
   (void)hipSetDevice(c->device);
   free_ws(c);
   free_ecp_ws(c);
+  if (c->d_tm_scr) (void)hipFree(c->d_tm_scr);
   if (c->d_ecp_tab) (void)hipFree(c->d_ecp_tab);
   void* pgp[] = {c->d_gmap, c->d_wnorm, c->d_pg, c->d_pgr};
   for (void* p : pgp)
@@ -799,38 +800,27 @@ int aiqmc_set_ecp(aiqmc_ctx* c, const aiqmc_ecp* e) {
   return AIQMC_OK;
 }
 
-int aiqmc_local_energy_ecp(aiqmc_ctx* c, const void* pos, int32_t B, int32_t rng_mode, const void* rot,
-                           uint64_t seed, uint64_t offset, void* e_re, void* e_im, void* logabs_q, void* phase_q,
-                           void* stream) {
-  int rc = check_call(c, pos, B);
-  if (rc) return rc;
-  if (!c->ecp_set) return fail(AIQMC_ESTATE, "aiqmc_set_ecp has not been called");
-  if (!e_re || !e_im) return fail(AIQMC_EINVAL, "null e_re / e_im");
-  if (rng_mode == AIQMC_RNG_HOST && !rot) return fail(AIQMC_EINVAL, "AIQMC_RNG_HOST needs rot");
-  if (rng_mode != AIQMC_RNG_HOST && rng_mode != AIQMC_RNG_PHILOX) return fail(AIQMC_EINVAL, "rng_mode");
-  if (B == 0) return AIQMC_OK;
+}  // extern "C"
+
+// Steps shared by the pp local energy and the T-moves (pseudopotential.py:272-318): per-walker
+// rotations (Philox draws or the caller's), the N*A*50 moved-electron positions, log psi at the
+// walkers (walker launch, which also fills the walker cache) and at every quadrature
+// configuration (value-only proposal launch through the cache).
+static int ecp_quadrature(aiqmc_ctx* c, const void* pos, int B, int rng_mode, const void* rot, uint64_t seed,
+                          uint64_t offset, void* logabs_q, void* phase_q, EcpArgs& ea, hipStream_t s) {
   const int64_t M = (int64_t)c->N * c->A * ECP_NQ;
   if ((int64_t)B * M > INT32_MAX) return fail(AIQMC_EINVAL, "too many quadrature configurations for one call");
-  HIPCHK(hipSetDevice(c->device));
   ShapeOps ops;
   shape_ops(c->N, c->A, &ops);
-  rc = ensure_ws(c, B);
-  if (rc) return rc;
-  rc = ensure_ecp_ws(c, B, ops);
+  int rc = ensure_ws(c, B);
   if (rc) return rc;
   if (!c->reuse) {
     rc = ensure_wcp(c, (int64_t)B * M, ops);
     if (rc) return rc;
   }
-  hipStream_t s = (hipStream_t)stream;
   const int nq = (int)(B * M);
   void* lq = logabs_q ? logabs_q : c->d_ecp_lq;
   void* pq = phase_q ? phase_q : c->d_ecp_pq;
-  // (1) all-electron local energy V + KE (walker_lap.h)
-  rc = aiqmc_local_energy(c, pos, B, c->d_ecp_el, nullptr, nullptr, stream);
-  if (rc) return rc;
-  // (2) rotations, quadrature positions
-  EcpArgs ea;
   std::memset(&ea, 0, sizeof(ea));
   ea.B = B;
   ea.N = c->N;
@@ -845,9 +835,6 @@ int aiqmc_local_energy_ecp(aiqmc_ctx* c, const void* pos, int32_t B, int32_t rng
   ea.ph0 = c->d_ecp_ph0;
   ea.lpq = lq;
   ea.phq = pq;
-  ea.eall = c->d_ecp_el;
-  ea.e_re = e_re;
-  ea.e_im = e_im;
   ea.xnew = c->d_ecp_x;
   ea.seed = seed;
   ea.step = offset;
@@ -858,7 +845,7 @@ int aiqmc_local_energy_ecp(aiqmc_ctx* c, const void* pos, int32_t B, int32_t rng
   }
   if (f32) k_ecp_points<float><<<dim3((nq + 255) / 256), dim3(256), 0, s>>>(ea);
   else k_ecp_points<double><<<dim3((nq + 255) / 256), dim3(256), 0, s>>>(ea);
-  // (3) walker launch: log psi at the walkers + the walker cache
+  // walker launch: log psi at the walkers + the walker cache
   KArgs ka = base_args(c);
   ka.nconf = B;
   ka.pos = pos;
@@ -866,7 +853,7 @@ int aiqmc_local_energy_ecp(aiqmc_ctx* c, const void* pos, int32_t B, int32_t rng
   ka.phase = c->d_ecp_ph0;
   ka.wcache = c->d_wc;
   ops.walker(c->dtype, MODE_GRAD, ka, B, s);
-  // (4) quadrature configurations: one moved electron each, value only
+  // quadrature configurations: one moved electron each, value only
   KArgs kp = base_args(c);
   kp.nconf = nq;
   kp.pos = pos;
@@ -885,9 +872,84 @@ int aiqmc_local_energy_ecp(aiqmc_ctx* c, const void* pos, int32_t B, int32_t rng
     kp.wcache = c->d_wcp;
   }
   timed(c, 3, s, [&] { ops.walker(c->dtype, MODE_GRAD, kp, nq, s); });
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+extern "C" {
+
+int aiqmc_local_energy_ecp(aiqmc_ctx* c, const void* pos, int32_t B, int32_t rng_mode, const void* rot,
+                           uint64_t seed, uint64_t offset, void* e_re, void* e_im, void* logabs_q, void* phase_q,
+                           void* stream) {
+  int rc = check_call(c, pos, B);
+  if (rc) return rc;
+  if (!c->ecp_set) return fail(AIQMC_ESTATE, "aiqmc_set_ecp has not been called");
+  if (!e_re || !e_im) return fail(AIQMC_EINVAL, "null e_re / e_im");
+  if (rng_mode == AIQMC_RNG_HOST && !rot) return fail(AIQMC_EINVAL, "AIQMC_RNG_HOST needs rot");
+  if (rng_mode != AIQMC_RNG_HOST && rng_mode != AIQMC_RNG_PHILOX) return fail(AIQMC_EINVAL, "rng_mode");
+  if (B == 0) return AIQMC_OK;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  // (1) all-electron local energy V + KE (walker_lap.h)
+  {
+    ShapeOps ops0;
+    shape_ops(c->N, c->A, &ops0);
+    rc = ensure_ecp_ws(c, B, ops0);
+    if (rc) return rc;
+  }
+  rc = aiqmc_local_energy(c, pos, B, c->d_ecp_el, nullptr, nullptr, stream);
+  if (rc) return rc;
+  // (2)-(4) rotations, quadrature positions, log psi at the walkers and the quadrature points
+  EcpArgs ea;
+  rc = ecp_quadrature(c, pos, B, rng_mode, rot, seed, offset, logabs_q, phase_q, ea, s);
+  if (rc) return rc;
+  ea.eall = c->d_ecp_el;
+  ea.e_re = e_re;
+  ea.e_im = e_im;
   // (5) local pp part + nonlocal quadrature sum
-  if (f32) k_ecp_energy<float><<<dim3(B), dim3(64), 0, s>>>(ea);
+  if (c->dtype == AIQMC_F32) k_ecp_energy<float><<<dim3(B), dim3(64), 0, s>>>(ea);
   else k_ecp_energy<double><<<dim3(B), dim3(64), 0, s>>>(ea);
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_dmc_tmoves(aiqmc_ctx* c, void* pos, int32_t B, double tstep, int32_t rng_mode, const void* rot,
+                     const void* u_sel, const void* u_acc, uint64_t seed, uint64_t offset, void* acceptance,
+                     void* stream) {
+  int rc = check_call(c, pos, B);
+  if (rc) return rc;
+  if (!c->ecp_set) return fail(AIQMC_ESTATE, "aiqmc_set_ecp has not been called");
+  if (!(tstep > 0.0)) return fail(AIQMC_EINVAL, "tstep must be > 0");
+  if (rng_mode == AIQMC_RNG_HOST && (!rot || !u_sel || !u_acc))
+    return fail(AIQMC_EINVAL, "AIQMC_RNG_HOST needs rot, u_sel and u_acc");
+  if (rng_mode != AIQMC_RNG_HOST && rng_mode != AIQMC_RNG_PHILOX) return fail(AIQMC_EINVAL, "rng_mode");
+  if (B == 0) return AIQMC_OK;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  {
+    ShapeOps ops0;
+    shape_ops(c->N, c->A, &ops0);
+    rc = ensure_ecp_ws(c, B, ops0);
+    if (rc) return rc;
+  }
+  if (!c->d_tm_scr || c->tm_B < B) {
+    if (c->d_tm_scr) HIPCHK(hipFree(c->d_tm_scr));
+    c->d_tm_scr = nullptr;
+    c->tm_B = 0;
+    HIPCHK(hipMalloc(&c->d_tm_scr, (size_t)B * c->N * c->A * ECP_NQ * 4 * sizeof(double)));
+    c->tm_B = B;
+  }
+  EcpArgs ea;
+  rc = ecp_quadrature(c, pos, B, rng_mode, rot, seed, offset, nullptr, nullptr, ea, s);
+  if (rc) return rc;
+  ea.tstep = tstep;
+  ea.usel = rng_mode == AIQMC_RNG_HOST ? u_sel : nullptr;
+  ea.uacc = rng_mode == AIQMC_RNG_HOST ? u_acc : nullptr;
+  ea.acc = acceptance;
+  ea.pos_out = pos;
+  ea.scr = c->d_tm_scr;
+  if (c->dtype == AIQMC_F32) k_tmove<float><<<dim3(B), dim3(64), 0, s>>>(ea);
+  else k_tmove<double><<<dim3(B), dim3(64), 0, s>>>(ea);
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
 }

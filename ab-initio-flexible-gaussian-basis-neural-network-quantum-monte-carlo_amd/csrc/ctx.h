@@ -47,6 +47,8 @@ struct aiqmc_ctx {
   void *d_ecp_rot = nullptr, *d_ecp_x = nullptr, *d_ecp_lq = nullptr, *d_ecp_pq = nullptr, *d_ecp_ec = nullptr,
        *d_ecp_el = nullptr, *d_ecp_lp0 = nullptr, *d_ecp_ph0 = nullptr;
   int64_t ecp_bytes = 0;
+  double* d_tm_scr = nullptr;      // T-moves per-walker amplitudes [tm_B][N*A*50][4]
+  int tm_B = 0;
   // parameter gradients (aiqmc_logpsi_param_grad, walker_pgrad.h)
   int* d_gmap = nullptr;            // [ncanon]
   double* d_wnorm = nullptr;        // [6] |W_y row| of the current parameters

@@ -85,6 +85,13 @@ struct EcpArgs {
   void* e_im;
   void* xnew;           // k_ecp_points output [B*N*A*50][3]
   uint64_t seed, step;  // k_ecp_rot
+  // T-moves (k_tmove)
+  double tstep;
+  const void* usel;     // [B] selection uniform (NULL: Philox)
+  const void* uacc;     // [B][N] acceptance uniforms (NULL: Philox)
+  void* acc;            // [B][N] acceptance out (optional)
+  void* pos_out;        // [B][3N] positions, updated in place
+  double* scr;          // [B][N*A*50][4] forward amplitude (re, im), ratio (re, im)
 };
 
 // Uniform Haar O(3): a uniformly random unit quaternion (4 normals, normalised) gives SO(3);
@@ -234,6 +241,162 @@ __global__ __launch_bounds__(64) void k_ecp_energy(EcpArgs ea) {
       }
     ((T*)ea.e_re)[b] = (T)((double)((const T*)ea.eall)[b] - ven + er);
     ((T*)ea.e_im)[b] = (T)ei;
+  }
+}
+
+// T-moves (DMC/Tmoves.py:68-224; oracle/dmc.py tmoves, quirks T1-T8), one wave per walker.
+// Pass 1 (lanes over the N*A*50 quadrature entries): ratio (E4, times w_g), t_amp = ratio *
+// sum_l (exp(-tau v_l) - 1) P_l(cos), forward amplitude = lexicographic max(t_amp, 0), and the
+// walker's norm 1 + sum w_g fwd.  Pass 2 (lanes over electrons): the scan binary search of
+// jnp.searchsorted on the row cdf (prefix sums recomputed per probe: rows are <= A*50+1 long),
+// back norm over the hard-coded slices, acceptance, in-place move from the original position.
+__device__ __forceinline__ bool cplx_le(double qr, double qi, double ar, double ai) {
+  return qr < ar || (qr == ar && qi <= ai);
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void k_tmove(EcpArgs ea) {
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int N = ea.N, A = ea.A;
+  const int AQ = A * ECP_NQ, M = N * AQ, M1 = AQ + 1;
+  const double* atoms = ea.tab;
+  const int stride = 3 * (ea.KL + ea.L * ea.KN);
+  const double* tabs = ea.tab + 4 * A;
+  const T* x = (const T*)ea.pos + (size_t)b * 3 * N;
+  const T* R = (const T*)ea.rot + (size_t)b * 9;
+  const double la0 = (double)((const T*)ea.lp0)[b], ph0 = (double)((const T*)ea.ph0)[b];
+  const double dn = 1.0 / (la0 * la0 + ph0 * ph0);
+  double* scr = ea.scr + (size_t)b * M * 4;
+  double nr = 0.0, ni = 0.0;
+  for (int idx = lane; idx < M; idx += 64) {
+    const int i = idx / AQ;
+    const int a = (idx / ECP_NQ) % A;
+    const int q = idx % ECP_NQ;
+    double ae[3], r2 = 0.0;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      ae[d] = (double)x[3 * i + d] - atoms[a * 3 + d];
+      r2 += ae[d] * ae[d];
+    }
+    const double r = sqrt(r2);
+    double p[3], pr[3];
+    int grp;
+    ecp_point(q, p, grp);
+    ecp_rotate<T>(R, p, pr);
+    double fro2 = 0.0;   // E3
+    for (int qq = ecp_group_begin(grp); qq < ecp_group_end(grp); ++qq) {
+      double pp[3], ppr[3];
+      int gg;
+      ecp_point(qq, pp, gg);
+      ecp_rotate<T>(R, pp, ppr);
+#pragma unroll
+      for (int d = 0; d < 3; ++d) fro2 += (r * ppr[d]) * (r * ppr[d]);
+    }
+    const double dot = ae[0] * (r * pr[0]) + ae[1] * (r * pr[1]) + ae[2] * (r * pr[2]);
+    const double cs = dot / (r * sqrt(fro2));
+    const size_t conf = (size_t)b * M + idx;
+    const double la = (double)((const T*)ea.lpq)[conf], ph = (double)((const T*)ea.phq)[conf];
+    const double w = ecp_weight(grp);
+    const double rr = (la * la0 + ph * ph0) * dn * w, ri = (ph * la0 - la * ph0) * dn * w;   // T1
+    const double* tnl = tabs + a * stride + 3 * ea.KL;
+    double wt = 0.0;
+    for (int l = 0; l < ea.L; ++l)
+      wt += (exp(-ea.tstep * ecp_radial(tnl + 3 * ea.KN * l, ea.KN, r, 0.0)) - 1.0) * ecp_pl(l, cs);   // T2
+    const double tr = rr * wt, ti = ri * wt;
+    const bool pos = tr > 0.0 || (tr == 0.0 && ti > 0.0);   // T3
+    const double fr = pos ? tr : 0.0, fi = pos ? ti : 0.0;
+    scr[4 * idx + 0] = fr;
+    scr[4 * idx + 1] = fi;
+    scr[4 * idx + 2] = rr;
+    scr[4 * idx + 3] = ri;
+    nr += w * fr;   // T4
+    ni += w * fi;
+  }
+  nr = 1.0 + wave_sum(nr);
+  ni = wave_sum(ni);
+  __threadfence_block();
+  __syncthreads();
+  double us;
+  if (ea.usel) {
+    us = (double)((const T*)ea.usel)[b];
+  } else {
+    float u[4];
+    philox_u4(ea.seed, ea.step, (uint32_t)b, 19u, u);
+    us = (double)u[0] - 5.9604644775390625e-08;   // (0,1] -> [0,1)
+  }
+  const double qr = us + 1.0;
+  const double in2 = 1.0 / (nr * nr + ni * ni);
+  const double inr = nr * in2, ini = -ni * in2;   // 1 / norm
+  int levels = 0;
+  while ((1 << levels) < M1 + 1) ++levels;        // ceil(log2(M1 + 1))
+  const int lo_[5] = {0, 1, 19, 55, 79}, hi_[5] = {1, 19, 55, 79, 151};
+  for (int e = lane; e < N; e += 64) {
+    // T5: jnp.searchsorted(cdf_e, u + 1), cdf_e[k] = sum_{j<=k} row_e[j] / norm
+    const double* fe = scr + (size_t)e * AQ * 4;
+    int low = 0, high = M1;
+    for (int lv = 0; lv < levels; ++lv) {
+      const int mid = (low + high) >> 1;
+      double cr = inr, ci = ini;   // row_e[0] = 1
+      for (int j = 1; j <= mid; ++j) {
+        const double fr = fe[4 * (j - 1)], fi = fe[4 * (j - 1) + 1];
+        cr += fr * inr - fi * ini;
+        ci += fr * ini + fi * inr;
+      }
+      if (cplx_le(qr, 0.0, cr, ci)) high = mid;
+      else low = mid;
+    }
+    const int mv = high < M1 ? high : 0;
+    // T6: back amplitudes = row[min(mv, N-1)] / ratio_total[e, mv]
+    double cr = 1.0, ci = 0.0;
+    if (mv > 0) {
+      const double rr = fe[4 * (mv - 1) + 2], ri = fe[4 * (mv - 1) + 3];
+      const double d = 1.0 / (rr * rr + ri * ri);
+      cr = rr * d;
+      ci = -ri * d;
+    }
+    const int ri_ = mv < N - 1 ? mv : N - 1;
+    const double* fb = scr + (size_t)ri_ * AQ * 4;
+    double sr = 0.0, si = 0.0;   // T7: sum_k W_k sum row[slice_k], W_0 = 0
+    for (int k = 1; k < 5; ++k) {
+      const double wk = ecp_weight(k - 1);
+      const int hi = hi_[k] < M1 ? hi_[k] : M1;
+      double tr = 0.0, ti = 0.0;
+      for (int j = lo_[k]; j < hi; ++j) {
+        tr += fb[4 * (j - 1)];
+        ti += fb[4 * (j - 1) + 1];
+      }
+      sr += wk * tr;
+      si += wk * ti;
+    }
+    const double br = 1.0 + (sr * cr - si * ci), bi = sr * ci + si * cr;
+    const double acc = (nr * br + ni * bi) / (br * br + bi * bi);   // T8: Re(norm / back_norm)
+    double ua;
+    if (ea.uacc) {
+      ua = (double)((const T*)ea.uacc)[(size_t)b * N + e];
+    } else {
+      float u[4];
+      philox_u4(ea.seed, ea.step, (uint32_t)(b * N + e), 20u, u);
+      ua = (double)u[0] - 5.9604644775390625e-08;
+    }
+    if (ea.acc) ((T*)ea.acc)[(size_t)b * N + e] = (T)acc;
+    if (acc > ua && mv > 0) {
+      const int m = mv - 1, a = m / ECP_NQ, q = m % ECP_NQ;
+      double r2 = 0.0;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const double t = (double)x[3 * e + d] - atoms[a * 3 + d];
+        r2 += t * t;
+      }
+      const double r = sqrt(r2);
+      double p[3], pr[3];
+      int grp;
+      ecp_point(q, p, grp);
+      ecp_rotate<T>(R, p, pr);
+      T* xo = (T*)ea.pos_out + (size_t)b * 3 * N + 3 * e;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) xo[d] = (T)(r * pr[d]);   // E2
+    }
   }
 }
 

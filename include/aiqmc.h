@@ -175,6 +175,21 @@ int aiqmc_local_energy_ecp(aiqmc_ctx* ctx, const void* pos, int32_t B, int32_t r
                            uint64_t seed, uint64_t offset, void* e_re, void* e_im, void* logabs_q,
                            void* phase_q, void* stream);
 
+/* DMC T-moves (DMC/Tmoves.py:32-225, called per walker by dmc.py:79 before the
+ * drift-diffusion step), in place on pos_inout [B][3N]: for every electron the
+ * pp quadrature configurations of aiqmc_local_energy_ecp give the amplitudes
+ * ratio * sum_l (exp(-tstep v_l) - 1) P_l(cos); one configuration per electron
+ * is selected with the reference's cdf / searchsorted rule and accepted with
+ * Re(norm / back_norm) > u (quirks T1-T8, oracle/dmc.py).  Needs aiqmc_set_ecp.
+ * rng_mode AIQMC_RNG_HOST: rot [B][3][3] (get_rot's matrix), u_sel [B]
+ *   (select_walker's uniform, one per walker, shared by its electrons) and
+ *   u_acc [B][N] (the acceptance uniforms), device arrays of the ctx dtype;
+ * AIQMC_RNG_PHILOX: all three drawn from (seed, offset).
+ * acceptance (optional, [B][N], ctx dtype): Re(norm / back_norm). */
+int aiqmc_dmc_tmoves(aiqmc_ctx* ctx, void* pos_inout, int32_t B, double tstep, int32_t rng_mode, const void* rot,
+                     const void* u_sel, const void* u_acc, uint64_t seed, uint64_t offset, void* acceptance,
+                     void* stream);
+
 /* Optional HIP-event timing of the hot kernels, recorded on the caller's
  * stream around each launch while enabled.  Slots: 0 = proposal
  * value+gradient launches of aiqmc_mc_step, 1 = walker gradient launches of

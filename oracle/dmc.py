@@ -85,3 +85,107 @@ def branch(weights, u):
     base = u * wtot
     newinds = np.searchsorted(prob, (base + np.linspace(0, wtot, n, endpoint=False)) % wtot)
     return wtot / n, newinds
+
+
+# --------------------------------------------------------------------------------------------
+# T-moves (DMC/Tmoves.py:32-225), one walker, draws injected.
+#
+# Quirks kept, as written in the reference (all relative to Tmoves.py):
+# * T1 the quadrature is the pp one (get_P_l, pseudopotential.py:272-318): E2 rotated
+#      electron at r_ia p_q R (not offset by the atom), E3 Frobenius cos(theta), E4 ratio =
+#      quotient of COMPLEX logs times the group weight w_g;
+# * T2 t_amp = ratio * sum_l (exp(-tau v_l(r_ia)) - 1) P_l(cos)   (:54-55, :92-101), P_l with the
+#      extra 1/(4 pi) (E5) and v_l with r**n (E1);
+# * T3 forward amplitude = where(t_amp > 0, t_amp, 0) with JAX's LEXICOGRAPHIC complex order
+#      (real part first, then imaginary) (:102-104);
+# * T4 norm = 1 + sum_g w_g sum_{i,a,q} fwd  -- one norm per walker over ALL electrons, the
+#      group weight applied a second time (:113-115);
+# * T5 per electron row [1, fwd[i, a, q] (a-major, q in OA|OB|OC|OD order)], cdf = cumsum(row /
+#      norm) (:123-141); selected = searchsorted(cdf, u + 1) with the SAME u for every electron
+#      (:145-149; jnp.searchsorted's scan binary search over the complex lexicographic order,
+#      side='left'); index == len(row) means "no move" (:154);
+# * T6 back amplitudes index the forward table by ROW = the selected move (clamped to the
+#      last electron, JAX gather semantics) times 1 / ratio_total[i, move] (:183-189, :196-198);
+# * T7 back norm = 1 + sum_k W_k sum back[:, slice_k] with W = [0, w_OA, w_OB, w_OC, w_OD] and
+#      the hard-coded slices [0], [1:19], [19:55], [55:79], [79:151] clipped to the row length
+#      (:202-210);
+# * T8 acceptance = Re(norm / back_norm) per electron, accepted iff > u_acc[i]; all electrons
+#      move simultaneously, each from the ORIGINAL configuration (:212-224).
+# --------------------------------------------------------------------------------------------
+
+TMOVE_SLICES = ((0, 1), (1, 19), (19, 55), (55, 79), (79, 151))
+
+
+def _lex_le(q: complex, a: complex) -> bool:
+    """q <= a in JAX's complex sort order (real part, then imaginary part)."""
+    return q.real < a.real or (q.real == a.real and q.imag <= a.imag)
+
+
+def searchsorted_scan(arr, q) -> int:
+    """jnp.searchsorted(arr, q, side='left', method='scan'): a fixed-depth binary search
+    (ceil(log2(n + 1)) levels, low = 0, high = n, go_left = q <= arr[mid]) that is defined
+    for unsorted arrays too."""
+    n = len(arr)
+    low, high = 0, n
+    for _ in range(int(np.ceil(np.log2(n + 1)))):
+        mid = (low + high) // 2
+        if _lex_le(q, complex(arr[mid])):
+            high = mid
+        else:
+            low = mid
+    return high
+
+
+def tmoves(net, params, ecp, pos, rot, u_sel: float, u_acc, tstep: float):
+    """calculate_ratio_weight_tmoves (Tmoves.py:68-224) for ONE walker pos[3N].
+
+    rot [3,3] is get_rot's orthogonal matrix, u_sel the uniform of select_walker (:146),
+    u_acc [N] the acceptance uniforms (:216-217).  Returns (new positions [3N], acceptance [N])."""
+    from . import pphamiltonian as pp
+    atoms = net.atoms.to(pos.dtype)
+    N, A = net.N, net.A
+    ph0, la0 = net.apply(params, pos)
+    den = complex(la0.item(), ph0.item())
+    vnl = pp.non_local_coefficients(ecp, pos, atoms).numpy()                 # [N, A, L]
+    x2 = pos.reshape(N, 3).numpy()
+    r = np.linalg.norm(x2[:, None, :] - atoms.numpy()[None], axis=-1)      # [N, A]
+    groups, gw = pp.quadrature_grids()
+    fwd, rat, coords = [], [], []
+    norm = 1.0 + 0j
+    for g, w in zip(groups, gw):
+        pts = pp.rotate_points(rot, g)
+        cos, cfg = pp.rotated_configurations(pos, atoms, pts)
+        P = pts.shape[0]
+        flat = cfg.reshape(N * A * P, 3 * N)
+        vals = [net.apply(params, flat[k]) for k in range(flat.shape[0])]
+        num = np.array([complex(v[1].item(), v[0].item()) for v in vals]).reshape(N, A, P)
+        ratio = num / den * w                                                # T1
+        pl = [t.numpy() for t in pp.p_l(cos, ecp.list_l)]
+        wts = sum((np.exp(-tstep * vnl[:, :, l]) - 1.0)[..., None] * pl[l] for l in range(ecp.list_l + 1))
+        t_amp = ratio * wts                                                  # T2
+        pos_part = (t_amp.real > 0) | ((t_amp.real == 0) & (t_amp.imag > 0))
+        f = np.where(pos_part, t_amp, 0.0)                                   # T3
+        norm = norm + w * f.sum()                                            # T4
+        fwd.append(f)
+        rat.append(ratio)
+        coords.append(r[:, :, None, None] * pts[None, None])                 # [N, A, P, 3] (E2)
+    fwd = np.concatenate(fwd, axis=-1).reshape(N, A * 50)
+    rat = np.concatenate(rat, axis=-1).reshape(N, A * 50)
+    coords = np.concatenate(coords, axis=2).reshape(N, A * 50, 3)
+    M1 = 1 + A * 50
+    row = np.concatenate([np.ones((N, 1)), fwd], axis=1)                     # T5
+    rat_f = np.concatenate([np.ones((N, 1)), rat], axis=1)
+    cfg_f = np.concatenate([x2[:, None, :], coords], axis=1)
+    cdf = np.cumsum(row / norm, axis=-1)
+    W = np.concatenate([[0.0], gw])
+    new = x2.copy()
+    acc = np.zeros(N)
+    for i in range(N):
+        sel = searchsorted_scan(cdf[i], complex(u_sel + 1.0, 0.0))
+        mv = sel if sel < M1 else 0
+        back = row[min(mv, N - 1)] * (1.0 / rat_f[i, mv])                   # T6
+        bn = 1.0 + sum(W[k] * back[lo:min(hi, M1)].sum() for k, (lo, hi) in enumerate(TMOVE_SLICES))  # T7
+        acc[i] = (norm / bn).real                                            # T8
+        if acc[i] > u_acc[i]:
+            new[i] = cfg_f[i, mv]
+    return torch.tensor(new.reshape(-1)), acc

@@ -1,7 +1,7 @@
 """DMC pieces (AIQMCrelease3/DMC): drift-diffusion step, S / weight update, stochastic comb.
-CPU: the oracle against closed forms; GPU: the HIP path against the oracle (fp64; E_L,
-weights and positions to 1e-9, indices exact).  T-moves (DMC/Tmoves.py) are not built
-(see DESIGN.md)."""
+T-moves.  CPU: the oracle against closed forms and its golden fixture; GPU: the HIP path
+against the oracle (fp64; E_L, weights and positions to 1e-9, indices and T-move selections
+exact)."""
 import math
 
 import numpy as np
@@ -125,8 +125,169 @@ def test_dmc_propagate_step_c_atom():
     eloc, w, new = run(params, PhiloxKey(3, 0), data, w0, torch.full((B,), 10.0), -3.0, -3.1)
     torch.cuda.synchronize()
     assert torch.isfinite(eloc.real).all() and torch.isfinite(w).all() and bool((w > 0).all())
-    # same drift-diffusion step outside: identical positions (deterministic Philox draws)
+    # same T-moves + drift-diffusion outside: identical positions (deterministic Philox draws)
+    from aiqmc.DMC.Tmoves import compute_tmoves
+    tm = compute_tmoves(2, 0.01, 4, 1, 3, nn.make_log_network(network.apply), e.rn_non_local, e.non_local_coes,
+                        e.non_local_exps)
+    pos_t, _ = tm(data, params, PhiloxKey(3 + 3, 0))
+    data_t = nn.AINetData(positions=pos_t, spins=s.spins, atoms=s.atoms, charges=s.charges)
     dd = propose_drift_diffusion(network.apply, 0.01, 3, 4, B)
-    new2, _, td, go, gn = dd(params, PhiloxKey(3, 0), data)
+    new2, _, td, go, gn = dd(params, PhiloxKey(3, 0), data_t)
     torch.cuda.synchronize()
     assert torch.equal(new.positions, new2.positions)
+
+
+# ----------------------------------------------------------------------------- T-moves
+
+def test_searchsorted_scan_matches_numpy_on_sorted():
+    rng = np.random.default_rng(0)
+    for n in range(1, 40):
+        a = np.sort(rng.uniform(size=n))
+        for q in np.concatenate([rng.uniform(size=8), a[:3], [-1.0, 2.0]]):
+            assert odmc.searchsorted_scan(a, q) == np.searchsorted(a, q)
+    # complex lexicographic order: equal real parts compare the imaginary parts
+    assert odmc.searchsorted_scan(np.array([1 - 1j, 1 + 0j, 1 + 1j]), 1.0) == 1
+
+
+def _c_atom():
+    from oracle import network, system
+    s = system.make_system("C_ecp")
+    return s, network
+
+
+def test_tmoves_zero_nonlocal_never_moves():
+    """v_l = 0: every t_amp is 0, norm = back_norm = 1, acceptance 1, no electron moves."""
+    from oracle import pphamiltonian as opp, system
+    s, network = _c_atom()
+    rng = np.random.default_rng(5)
+    params = system.init_params(rng, s, randomize_aux=True)
+    ecp = opp.ECP([[1.0]], [[0.0]], [[1.0]], [[[2.0], [2.0]]], [[[0.0], [0.0]]], [[[1.0], [1.0]]], 1)
+    pos = torch.tensor(system.init_electrons(rng, s.atoms, s.charges, 1, 1.0)[0])
+    new, acc = odmc.tmoves(network.Network(s), network.to_torch(params), ecp, pos, opp.haar_rotations(rng, 1)[0],
+                           0.0, np.full(4, 0.999), 0.5)
+    np.testing.assert_array_equal(new.numpy(), pos.numpy())
+    np.testing.assert_allclose(acc, 1.0, rtol=0, atol=1e-15)
+
+
+def test_tmoves_golden_fixture(golden_dir):
+    """The committed fixture is what the oracle computes (first two walkers recomputed), and
+    every moved electron sits on its own shell |x| = r_i (atom at the origin, E2; to the
+    1e-8 of the reference's 8-digit grid literals)."""
+    import os
+    from oracle import pphamiltonian as opp
+    s, network = _c_atom()
+    g = dict(np.load(os.path.join(golden_dir, "C_tmoves.npz")))
+    net = network.Network(s)
+    from oracle import system
+    pt = network.to_torch(system.unflatten_params(system.init_params(np.random.default_rng(0), s), g["params_flat"]))
+    ecp = {"ccecp": opp.c_atom_ccecp(),
+           "attractive": opp.ECP([[1.0]], [[0.0]], [[1.0]], [[[2.0], [1.0]]], [[[-3.0], [-5.0]]], [[[0.7], [0.4]]], 1)}
+    for name in ("ccecp", "attractive"):
+        new, pos = g[f"new_{name}"].reshape(-1, 4, 3), g["pos"].reshape(-1, 4, 3)
+        np.testing.assert_allclose(np.linalg.norm(new, axis=-1), np.linalg.norm(pos, axis=-1), rtol=1e-7)  # 8-digit grid literals
+        for b in range(2):
+            nb, ab = odmc.tmoves(net, pt, ecp[name], torch.tensor(g["pos"][b]), g["rot"][b], g["u_sel"][b],
+                                 g["u_acc"][b], float(g[f"tstep_{name}"]))
+            np.testing.assert_allclose(nb.numpy(), g[f"new_{name}"][b], rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(ab, g[f"acc_{name}"][b], rtol=1e-10)
+    assert (np.abs(g["new_attractive"] - g["pos"]).sum() > 0)
+
+
+def _tm_ctx(dtype, ecp):
+    from oracle import system
+    from aiqmc import _lib
+    s = system.make_system("C_ecp")
+    t = s.tables()
+    ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
+                       t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"], dtype=dtype, device=0)
+    ctx.set_ecp(ecp.rn_local, ecp.local_coes, ecp.local_exps, ecp.rn_non_local, ecp.non_local_coes,
+                ecp.non_local_exps, ecp.list_l)
+    return s, ctx
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ccecp", "attractive"])
+def test_tmoves_match_golden(golden_dir, name):
+    """HIP T-moves (fp64, injected draws) reproduce the oracle fixture: selections exact,
+    positions to 1e-9, acceptance to 1e-8."""
+    import os
+    from oracle import pphamiltonian as opp
+    g = dict(np.load(os.path.join(golden_dir, "C_tmoves.npz")))
+    ecp = opp.c_atom_ccecp() if name == "ccecp" else opp.ECP([[1.0]], [[0.0]], [[1.0]], [[[2.0], [1.0]]],
+                                                            [[[-3.0], [-5.0]]], [[[0.7], [0.4]]], 1)
+    s, ctx = _tm_ctx(torch.float64, ecp)
+    ctx.set_params(g["params_flat"])
+    pos = torch.tensor(g["pos"], device="cuda").contiguous()
+    acc = ctx.dmc_tmoves(pos, float(g[f"tstep_{name}"]), rot=torch.tensor(g["rot"]), u_sel=torch.tensor(g["u_sel"]),
+                         u_acc=torch.tensor(g["u_acc"]))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(pos.cpu().numpy(), g[f"new_{name}"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(acc.cpu().numpy(), g[f"acc_{name}"], rtol=1e-8, atol=1e-10)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_tmoves_full_batch_properties(dtype):
+    """4096 walkers, Philox draws: finite acceptance, every electron stays on its shell
+    |x_i| (moves go to r_i p_q R, atom at the origin), the attractive table moves electrons,
+    and a walker's result does not depend on the batch it runs in (host draws)."""
+    from oracle import pphamiltonian as opp, system
+    ecp = opp.ECP([[1.0]], [[0.0]], [[1.0]], [[[2.0], [1.0]]], [[[-3.0], [-5.0]]], [[[0.7], [0.4]]], 1)
+    s, ctx = _tm_ctx(dtype, ecp)
+    rng = np.random.default_rng(12)
+    ctx.set_params(system.flatten_params(system.init_params(rng, s, randomize_aux=True)))
+    B = 4096
+    x0 = torch.tensor(system.init_electrons(rng, s.atoms, s.charges, B, 1.0), dtype=dtype, device="cuda")
+    pos = x0.clone()
+    acc = ctx.dmc_tmoves(pos, 0.3, seed=7, offset=1)
+    torch.cuda.synchronize()
+    assert torch.isfinite(acc).all()
+    tol = 1e-5 if dtype == torch.float32 else 1e-7   # the grid's 8-digit literals are not unit vectors
+    r0, r1 = x0.reshape(B, 4, 3).norm(dim=-1), pos.reshape(B, 4, 3).norm(dim=-1)
+    assert torch.allclose(r1, r0, rtol=tol, atol=tol)
+    assert bool(((pos - x0).abs().reshape(B, 4, 3).sum(-1) > 0).any())
+    # host draws: a sub-batch gives the same walkers' results
+    rot = torch.tensor(opp.haar_rotations(rng, B), dtype=dtype)
+    us = torch.tensor(np.where(rng.uniform(size=B) < 0.5, 0.0, rng.uniform(size=B) * 1e-3), dtype=dtype)
+    ua = torch.tensor(rng.uniform(size=(B, 4)), dtype=dtype)
+    pa = x0.clone()
+    ctx.dmc_tmoves(pa, 0.3, rot=rot, u_sel=us, u_acc=ua)
+    sub = torch.arange(100, 164)
+    pb = x0[sub].clone().contiguous()
+    ctx.dmc_tmoves(pb, 0.3, rot=rot[sub], u_sel=us[sub], u_acc=ua[sub])
+    torch.cuda.synchronize()
+    assert torch.equal(pa[sub], pb)
+
+
+@pytest.mark.gpu
+def test_compute_tmoves_dropin(golden_dir):
+    """aiqmc.DMC.Tmoves.compute_tmoves (reference signature) with injected draws equals the
+    fixture; the walker data are not modified in place."""
+    import os
+    from oracle import pphamiltonian as opp
+    from aiqmc import spin_indices
+    from aiqmc.DMC.Tmoves import HostTmoveDraws, compute_tmoves
+    from aiqmc.wavefunction_Ynlm import nn
+    s, _ = _c_atom()
+    g = dict(np.load(os.path.join(golden_dir, "C_tmoves.npz")))
+    par, anti, npar, nanti = spin_indices.jastrow_indices_ee(spins=s.spins, nelectrons=4)
+    up, dn = spin_indices.spin_indices_h(s.spins)
+    network = nn.make_ai_net(ndim=3, nelectrons=4, natoms=1, nspins=(2, 2), charges=s.charges,
+                             parallel_indices=par, antiparallel_indices=anti, n_parallel=npar,
+                             n_antiparallel=nanti, spin_up_indices=up, spin_down_indices=dn)
+    e = opp.c_atom_ccecp()
+    tm = compute_tmoves(2, float(g["tstep_ccecp"]), 4, 1, 3, nn.make_log_network(network.apply), e.rn_non_local,
+                        e.non_local_coes, e.non_local_exps)
+    pos = torch.tensor(g["pos"], device="cuda")
+    keep = pos.clone()
+    data = nn.AINetData(positions=pos, spins=s.spins, atoms=s.atoms, charges=s.charges)
+    from oracle import system
+    params = system.unflatten_params(system.init_params(np.random.default_rng(0), s), g["params_flat"])
+    new, acc = tm(data, params, HostTmoveDraws(torch.tensor(g["rot"]), torch.tensor(g["u_sel"]),
+                                                         torch.tensor(g["u_acc"])))
+    torch.cuda.synchronize()
+    assert torch.equal(pos, keep)
+    np.testing.assert_allclose(new.cpu().numpy(), g["new_ccecp"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(acc.cpu().numpy(), g["acc_ccecp"], rtol=1e-8, atol=1e-10)
+    with pytest.raises(TypeError):
+        compute_tmoves(2, 0.1, 4, 1, 3, lambda *a: None, e.rn_non_local, e.non_local_coes, e.non_local_exps)
