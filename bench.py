@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     ap.add_argument("--no-ecp", action="store_true", help="skip the C-atom ccECP local-energy side measurement")
     ap.add_argument("--no-adam", action="store_true", help="skip the Be-atom Adam training-step side measurement")
+    ap.add_argument("--no-dmc", action="store_true", help="skip the C-atom DMC side measurement")
     return ap.parse_args()
 
 
@@ -175,6 +176,66 @@ def ecp_side_bench(dtype, device, walkers, steps, cpu_baseline_on):
         res["cpu_baseline"] = {"value": 2 / tc, "unit": "local-energy evals/s", "cores": torch.get_num_threads(),
                                "kind": "port", "sample": f"float64 oracle, 2 walkers ({tc:.1f}s)"}
     return res
+
+
+def dmc_side_bench(dtype, device, walkers, steps):
+    """DMC propagation through the drop-in API (DMC/dmc.py:72-93 + branch.py, as main_dmc.py:160-210
+    drives it): T-moves, drift-diffusion, pp local energies before/after, weight update, stochastic
+    comb, on the C-atom ccECP system (the only pseudopotential tables the reference ships;
+    dmc_propagate always uses the pp Hamiltonian)."""
+    from aiqmc import spin_indices
+    from aiqmc.DMC import dmc
+    from aiqmc.DMC.Tmoves import compute_tmoves
+    from aiqmc.VMC.VMCmcstep import PhiloxKey
+    from aiqmc.wavefunction_Ynlm import nn
+    from aiqmc.initial_electrons_positions.init import init_electrons
+    from oracle import pphamiltonian as opp, system as osys
+    s = osys.make_system("C_ecp")
+    par, anti, npar, nanti = spin_indices.jastrow_indices_ee(s.spins, 4)
+    up, dn = spin_indices.spin_indices_h(s.spins)
+    network = nn.make_ai_net(nspins=(2, 2), charges=s.charges, parallel_indices=par, antiparallel_indices=anti,
+                             spin_up_indices=up, spin_down_indices=dn, n_parallel=npar, n_antiparallel=nanti,
+                             ndim=3, natoms=1, nelectrons=4)
+    params = network.init(3)
+    e = opp.c_atom_ccecp()
+    tstep = 0.01
+    run = dmc.dmc_propagate(network.apply, nn.make_log_network(network.apply), network.apply, e.list_l, 4, 1, 3,
+                            walkers, tstep, 1, s.charges, s.spins, e.rn_local, e.local_coes, e.local_exps,
+                            e.rn_non_local, e.non_local_coes, e.non_local_exps)
+    tm = compute_tmoves(e.list_l, tstep, 4, 1, 3, nn.make_log_network(network.apply), e.rn_non_local,
+                        e.non_local_coes, e.non_local_exps)
+    pos, sp = init_electrons(11, None, s.atoms, s.charges, s.spins, walkers, 1.0)
+    data = nn.AINetData(positions=pos.to(device, dtype).contiguous(), spins=sp, atoms=s.atoms, charges=s.charges)
+    ctx = network.apply._aiqmc_network.bind(params, s.atoms, dtype)
+    w = torch.ones(walkers, dtype=dtype, device=device)
+    bc = torch.full((walkers,), 10.0)
+
+    def one(k):
+        nonlocal data, w
+        eloc, w, data = run(params, PhiloxKey(21, k), data, w, bc, -5.4, -5.4)
+        wn, idx = ctx.dmc_branch(w, 0.37)
+        data = nn.AINetData(positions=data.positions[idx.long()].contiguous(), spins=data.spins, atoms=data.atoms,
+                            charges=data.charges)
+        w = wn.expand(walkers).contiguous()
+        return eloc
+
+    for k in range(2):
+        one(k)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        eloc = one(100 + k)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for k in range(steps):
+        tm(data, params, PhiloxKey(5, k))
+    torch.cuda.synchronize()
+    dtm = time.perf_counter() - t0
+    return {"config": "C atom ccECP DMC step: T-moves + drift-diffusion + 2x pp E_L + weights + comb, drop-in API",
+            "walkers": walkers, "tstep": tstep, "ms_per_dmc_step": 1e3 * dt / steps,
+            "walker_steps_per_s": walkers * steps / dt, "tmoves_ms": 1e3 * dtm / steps,
+            "mean_energy_re": float(eloc.real.mean()), "finite": bool(torch.isfinite(eloc.real).all())}
 
 
 def adam_side_bench(dtype, device, walkers, steps):
@@ -350,6 +411,11 @@ def main():
                 out["adam_be_atom"] = adam_side_bench(dtype, dev, 4096, 5)
             except Exception as e:  # a side measurement, never a failure of the headline bench
                 out["adam_be_atom"] = {"error": repr(e)}
+        if world == 1 and not args.no_dmc:
+            try:
+                out["dmc_c_atom"] = dmc_side_bench(dtype, dev, 4096, 5)
+            except Exception as e:  # a side measurement, never a failure of the headline bench
+                out["dmc_c_atom"] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(args.system, params, atoms, charges, args.nsteps, args.tstep,
