@@ -675,7 +675,7 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
   if (rc) return rc;
   if (nsteps < 0) return fail(AIQMC_EINVAL, "negative nsteps");
   if (!(tstep > 0.0)) return fail(AIQMC_EINVAL, "tstep must be > 0");
-  if (rng_mode == AIQMC_RNG_HOST && (!gauss1 || !gauss2 || !u))
+  if (rng_mode == AIQMC_RNG_HOST && B > 0 && (!gauss1 || !gauss2 || !u))
     return fail(AIQMC_EINVAL, "AIQMC_RNG_HOST needs gauss1, gauss2 and u");
   if (rng_mode != AIQMC_RNG_HOST && rng_mode != AIQMC_RNG_PHILOX) return fail(AIQMC_EINVAL, "rng_mode");
   if (B == 0 || nsteps == 0) return AIQMC_OK;
@@ -704,8 +704,8 @@ int aiqmc_logpsi_param_grad(aiqmc_ctx* c, const void* pos, int32_t B, const void
                             void* logabs, void* stream) {
   int rc = check_call(c, pos, B);
   if (rc) return rc;
-  if (!out) return fail(AIQMC_EINVAL, "null out");
   if (B == 0) return AIQMC_OK;
+  if (!out) return fail(AIQMC_EINVAL, "null out");
   HIPCHK(hipSetDevice(c->device));
   ShapeOps ops;
   shape_ops(c->N, c->A, &ops);
@@ -884,10 +884,10 @@ int aiqmc_local_energy_ecp(aiqmc_ctx* c, const void* pos, int32_t B, int32_t rng
   int rc = check_call(c, pos, B);
   if (rc) return rc;
   if (!c->ecp_set) return fail(AIQMC_ESTATE, "aiqmc_set_ecp has not been called");
-  if (!e_re || !e_im) return fail(AIQMC_EINVAL, "null e_re / e_im");
-  if (rng_mode == AIQMC_RNG_HOST && !rot) return fail(AIQMC_EINVAL, "AIQMC_RNG_HOST needs rot");
+  if (rng_mode == AIQMC_RNG_HOST && B > 0 && !rot) return fail(AIQMC_EINVAL, "AIQMC_RNG_HOST needs rot");
   if (rng_mode != AIQMC_RNG_HOST && rng_mode != AIQMC_RNG_PHILOX) return fail(AIQMC_EINVAL, "rng_mode");
   if (B == 0) return AIQMC_OK;
+  if (!e_re || !e_im) return fail(AIQMC_EINVAL, "null e_re / e_im");
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
   // (1) all-electron local energy V + KE (walker_lap.h)
@@ -920,7 +920,7 @@ int aiqmc_dmc_tmoves(aiqmc_ctx* c, void* pos, int32_t B, double tstep, int32_t r
   if (rc) return rc;
   if (!c->ecp_set) return fail(AIQMC_ESTATE, "aiqmc_set_ecp has not been called");
   if (!(tstep > 0.0)) return fail(AIQMC_EINVAL, "tstep must be > 0");
-  if (rng_mode == AIQMC_RNG_HOST && (!rot || !u_sel || !u_acc))
+  if (rng_mode == AIQMC_RNG_HOST && B > 0 && (!rot || !u_sel || !u_acc))
     return fail(AIQMC_EINVAL, "AIQMC_RNG_HOST needs rot, u_sel and u_acc");
   if (rng_mode != AIQMC_RNG_HOST && rng_mode != AIQMC_RNG_PHILOX) return fail(AIQMC_EINVAL, "rng_mode");
   if (B == 0) return AIQMC_OK;
@@ -960,11 +960,11 @@ int aiqmc_dmc_drift_diffusion(aiqmc_ctx* c, void* pos, int32_t B, double tstep, 
   int rc = check_call(c, pos, B);
   if (rc) return rc;
   if (!(tstep > 0.0)) return fail(AIQMC_EINVAL, "tstep must be > 0");
-  if (rng_mode == AIQMC_RNG_HOST && (!gauss1 || !gauss2 || !u))
+  if (rng_mode == AIQMC_RNG_HOST && B > 0 && (!gauss1 || !gauss2 || !u))
     return fail(AIQMC_EINVAL, "AIQMC_RNG_HOST needs gauss1, gauss2 and u");
   if (rng_mode != AIQMC_RNG_HOST && rng_mode != AIQMC_RNG_PHILOX) return fail(AIQMC_EINVAL, "rng_mode");
-  if (!grad_eff_old || !grad_new_eff || !tdamp) return fail(AIQMC_EINVAL, "null output");
   if (B == 0) return AIQMC_OK;
+  if (!grad_eff_old || !grad_new_eff || !tdamp) return fail(AIQMC_EINVAL, "null output");
   HIPCHK(hipSetDevice(c->device));
   rc = ensure_ws(c, B);
   if (rc) return rc;
