@@ -1,0 +1,39 @@
+"""Forward vs backward split of the N2 proposal kernel: per-configuration time of the
+value-only proposal path (ECP quadrature launch, F0-F5) vs the value+gradient proposal
+launch of the Metropolis sweep (F0-B4).  Diagnostics only."""
+import json, os, sys
+import numpy as np
+import torch
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "ab-initio-flexible-gaussian-basis-neural-network-quantum-monte-carlo_amd"))
+from oracle import system, pphamiltonian as opp
+from aiqmc import _lib
+s = system.make_system("N2")
+t = s.tables()
+ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"], t["spin_down_indices"],
+                   t["parallel_indices"], t["antiparallel_indices"], dtype=torch.float32, device=0)
+ctx.set_params(system.flatten_params(system.init_params(np.random.default_rng(1), s)))
+z = np.zeros((2, 1))
+ctx.set_ecp(z, z, z + 1, np.zeros((2, 1, 1)) + 2, np.zeros((2, 1, 1)), np.ones((2, 1, 1)), 0)
+from aiqmc.initial_electrons_positions.init import init_electrons
+pos, _ = init_electrons(3, None, s.atoms, s.charges, s.spins, 4096, 1.0)
+pos = pos.to("cuda", torch.float32).contiguous()
+ctx.mc_step(pos, 3, 0.05, seed=1)
+sub = pos[:512].contiguous()
+ctx.local_energy_ecp(sub, seed=1)
+torch.cuda.synchronize()
+ctx.profile(True)
+ctx.mc_step(pos, 10, 0.05, seed=2)
+for k in range(5):
+    ctx.local_energy_ecp(sub, seed=2 + k)
+torch.cuda.synchronize()
+ctx.profile(False)
+pm, pn = ctx.profile_read(_lib.PROF_MC_PROPOSAL)
+qm, qn = ctx.profile_read(_lib.PROF_ECP_QUAD)
+nprop = 4096 * 14
+nq = 512 * 14 * 2 * 50
+out = {"proposal_ms": pm / pn, "proposal_ns_per_config": 1e6 * pm / pn / nprop,
+       "value_only_ms": qm / qn, "value_only_ns_per_config": 1e6 * qm / qn / nq}
+out["forward_share"] = out["value_only_ns_per_config"] / out["proposal_ns_per_config"]
+print(json.dumps(out))
