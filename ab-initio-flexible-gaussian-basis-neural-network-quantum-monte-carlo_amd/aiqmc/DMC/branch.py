@@ -3,8 +3,8 @@
 ``branch(data, weights, key)`` -> (weights, newinds): newinds = searchsorted(cumsum(w),
 (u wtot + linspace(0, wtot, n, endpoint=False)) % wtot), weights -> wtot / n.  ``key`` is the
 uniform draw u in [0, 1) (parity mode) or an int seed for numpy's generator.  The driver's
-re-indexing of the positions (main_dmc.py:208-242: unique() plus ad-hoc extra walkers, marked
-"not a good solution" by its author) is not reproduced: ``apply_branch`` gathers x[newinds]."""
+re-indexing of the positions (main_dmc.py:208-242: unique() plus ad-hoc extra walkers) is
+``DMC.main_dmc.reindex_walkers``; ``apply_branch`` is the plain comb gather x[newinds]."""
 from __future__ import annotations
 
 import numpy as np

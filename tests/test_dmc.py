@@ -291,3 +291,64 @@ def test_compute_tmoves_dropin(golden_dir):
     np.testing.assert_allclose(acc.cpu().numpy(), g["acc_ccecp"], rtol=1e-8, atol=1e-10)
     with pytest.raises(TypeError):
         compute_tmoves(2, 0.1, 4, 1, 3, lambda *a: None, e.rn_non_local, e.non_local_coes, e.non_local_exps)
+
+
+# ----------------------------------------------------------------------------- DMC driver pieces
+
+def test_reindex_walkers_follows_driver():
+    """main_dmc.py:215-233: sorted unique comb indices, killed walkers replaced by the last
+    unique walker plus U[0,1) noise."""
+    from aiqmc.DMC.main_dmc import reindex_walkers
+    rng = np.random.default_rng(6)
+    x1 = torch.tensor(rng.standard_normal((6, 12)))
+    idx = torch.tensor([4, 1, 1, 4, 4, 0], dtype=torch.int32)
+    noise = torch.tensor(rng.uniform(size=(6, 12)))
+    got = reindex_walkers(x1, idx, noise)
+    unique = np.unique(idx.numpy())
+    temp = x1.numpy()[unique]
+    want = np.concatenate([temp, temp[-1] + noise.numpy()[:6 - len(unique)]])
+    np.testing.assert_array_equal(got.numpy(), want)
+    full = reindex_walkers(x1, torch.arange(6), noise)
+    assert torch.equal(full, x1)
+
+
+def test_estimate_and_total_energy_dropins():
+    from aiqmc.DMC.estimate_energy import estimate_energy
+    from aiqmc.DMC.total_energy import calculate_total_energy
+    e = torch.tensor([[1.0, 2.0], [3.0, 0.0]])
+    w = torch.tensor([[1.0, 1.0], [2.0, 0.0]])
+    assert abs(estimate_energy(e, w).item() - np.average(e.numpy(), weights=w.numpy())) < 1e-12
+    el = torch.tensor([1.0 + 1j, 3.0 - 1j, 2.0 + 0j], dtype=torch.complex128)
+    te = calculate_total_energy(lambda params, key, data: (el, None))
+    e_l, var = te(None, 0, None)
+    d = el.numpy() - el.numpy().mean()
+    assert torch.equal(e_l, el) and abs(var.item() - np.mean(d * np.conj(d))) < 1e-12
+
+
+@pytest.mark.gpu
+def test_main_dmc_driver_runs_from_vmc_checkpoint(tmp_path):
+    """aiqmc.DMC.main_dmc.main with the reference driver's arguments (single_atom_C tables),
+    restarted from a VMC checkpoint written by aiqmc.checkpoint: finite block estimates, a
+    DMC_states.csv row per block, walkers kept per device."""
+    from oracle import pphamiltonian as opp, system
+    from aiqmc import checkpoint
+    from aiqmc.DMC import main_dmc
+    from aiqmc.wavefunction_Ynlm import nn
+    s = system.make_system("C_ecp")
+    B = 128
+    params = system.init_params(np.random.default_rng(8), s, randomize_aux=True)
+    pos = torch.tensor(system.init_electrons(np.random.default_rng(9), s.atoms, s.charges, B, 1.0))
+    checkpoint.save(str(tmp_path), 5, nn.AINetData(positions=pos, spins=s.spins, atoms=s.atoms, charges=s.charges),
+                    params, np.zeros(1))
+    e = opp.c_atom_ccecp()
+    est, data, w = main_dmc.main(atoms=s.atoms, charges=s.charges, spins=s.spins, tstep=0.01, nelectrons=4,
+                                 nsteps=1, natoms=1, ndim=3, batch_size=B, iterations=2, nblocks=2, feedback=1.0,
+                                 nspins=(2, 2), save_path=str(tmp_path), restore_path=None, Rn_local=e.rn_local,
+                                 Local_coes=e.local_coes, Local_exps=e.local_exps, Rn_non_local=e.rn_non_local,
+                                 Non_local_coes=e.non_local_coes, Non_local_exps=e.non_local_exps,
+                                 save_frequency=1e9, structure=None, seed=3)
+    torch.cuda.synchronize()
+    assert len(est) == 2 and all(np.isfinite(est))
+    assert data.positions.shape == (B, 12) and torch.isfinite(data.positions).all()
+    rows = open(tmp_path / "DMC_states.csv").read().strip().split("\n")
+    assert rows[0] == "block,energy,positions" and len(rows) >= 3
