@@ -6,13 +6,15 @@ center_at_clipped_energy, complex_output)`` returns ``total_energy(params, key, 
 through a custom JVP (:220-270).  Here the derivative is explicit:
 ``total_energy.value_and_grad(params, key, data) -> ((loss, aux), grad_tree)``, with
 
-    grad = pmean( (2 / B) sum_b diff_b d log|psi_b| / d theta )
+    grad = (2 / B) sum_b [ Re(diff_b) d log|psi_b| / d theta + Im(cl_b) d phase_b / d theta ]
 
-(diff = clipped local energy minus its batch mean, :73-135; for real E_L the complex_output
-formula (term1 - 2 term2).real / B reduces to this), computed on the GPU by
-aiqmc_logpsi_param_grad with weights 2 diff_b / B (one launch + a device reduction).
-Complex local energies (the pseudopotential driver) need d phase / d theta as well, which is
-not built: they raise.
+the custom-JVP tangent (term1 - 2 term2).real / B of :256-265 with psi_tangent = d(log|psi| +
+i phase) (complex_output=True; diff = clipped local energy minus its centre, :73-135;
+cl = diff + aux.clipped_energy, which is the clip centre when clipping and E_L itself when
+not -- kept as written).  For real E_L the phase term vanishes.  complex_output=False uses the
+reference's dot(psi_tangent, diff) / B (factor 1/B, not 2/B).  Both terms are weighted
+device reductions of the per-walker parameter gradients (aiqmc_logpsi_param_grad,
+aiqmc_phase_param_grad).  The optimizer pmeans the result over ranks (adam.py:55).
 """
 from __future__ import annotations
 
@@ -94,22 +96,31 @@ def make_loss(network, local_energy, clip_local_energy: float = 0.0, clip_from_m
 
     def value_and_grad(params, key, data):
         e_l, e_mat, loss, variance = _energy(params, key, data)
-        if torch.is_complex(e_l) and bool(torch.any(e_l.imag != 0)):
-            raise NotImplementedError("complex local energies need d phase / d theta, which is not built")
-        e_r = e_l.real if torch.is_complex(e_l) else e_l
-        loss_r = loss.real if torch.is_complex(loss) else loss
+        cplx = torch.is_complex(e_l) and bool(torch.any(e_l.imag != 0))
+        if cplx and not complex_output:
+            raise NotImplementedError("complex local energies need complex_output=True (loss.py:256-265)")
+        e_c = e_l if cplx else (e_l.real if torch.is_complex(e_l) else e_l)
+        loss_c = loss if cplx else (loss.real if torch.is_complex(loss) else loss)
         if clip_local_energy > 0.0:
-            center, diff = clip_local_values(e_r, loss_r, clip_local_energy, clip_from_median,
+            center, diff = clip_local_values(e_c, loss_c, clip_local_energy, clip_from_median,
                                              center_at_clipped_energy)
+            aux_clipped = center                      # aux_data.clipped_energy (loss.py:240-246)
         else:
-            center, diff = loss_r, e_r - loss_r
+            center, diff = loss_c, e_c - loss_c
+            aux_clipped = e_c                         # total_energy's clipped_energy = e_l
         pos = data.positions if isinstance(data.positions, torch.Tensor) else torch.as_tensor(
             np.asarray(data.positions))
         dtype = pos.dtype if pos.dtype in (torch.float32, torch.float64) else torch.float32
         ctx = net.bind(params, data.atoms, dtype)
         B = diff.numel()
-        w = (2.0 / B) * diff.reshape(-1).to(ctx.device, dtype)
+        scale = (2.0 if complex_output else 1.0) / B
+        d_re = diff.real if torch.is_complex(diff) else diff
+        w = scale * d_re.reshape(-1).to(ctx.device, dtype)
         g = ctx.logpsi_param_grad(pos.reshape(B, -1), weights=w)     # loss.py:256-265
+        if cplx:
+            cl = diff + aux_clipped
+            wp = scale * cl.imag.reshape(-1).to(ctx.device, dtype)
+            g = g + ctx.phase_param_grad(pos.reshape(B, -1), weights=wp)
         aux = AuxiliaryLossData(variance=variance, local_energy=e_l, clipped_energy=center + diff,
                                 local_energy_mat=e_mat)
         return (loss, aux), g

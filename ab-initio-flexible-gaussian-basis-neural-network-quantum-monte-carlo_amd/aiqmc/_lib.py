@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_profile_enable", "aiqmc_profile_read", "aiqmc_debug_logpsi_grad_forward",
     "aiqmc_debug_set_proposal_reuse", "aiqmc_debug_phase_cycles", "aiqmc_debug_local_energy_forward",
     "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
-    "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves",
+    "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves", "aiqmc_phase_param_grad",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -110,6 +110,7 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_debug_phase_cycles.argtypes = [vp, vp]
     lib.aiqmc_debug_phase_cycles.restype = ctypes.c_int
     lib.aiqmc_logpsi_param_grad.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+    lib.aiqmc_phase_param_grad.argtypes = [vp, vp, i32, vp, vp, vp, vp]
     dbl, u64 = ctypes.c_double, ctypes.c_uint64
     lib.aiqmc_dmc_drift_diffusion.argtypes = [vp, vp, i32, dbl, i32, vp, vp, vp, u64, u64, vp, vp, vp, vp]
     lib.aiqmc_dmc_weights.argtypes = [vp, i32, vp, vp, vp, vp, vp, dbl, dbl, dbl, dbl, vp, vp]
@@ -325,6 +326,24 @@ class Context:
         check(self._lib.aiqmc_logpsi_param_grad(self._h, _ptr(p), B, _ptr(w), _ptr(out), _ptr(la),
                                                 _stream(self.device)), "aiqmc_logpsi_param_grad")
         return (out, la) if want_logabs else out
+
+    def phase_param_grad(self, pos: torch.Tensor, weights: Optional[torch.Tensor] = None,
+                         want_phase: bool = False):
+        """d phase / d theta (phase = arg det A), same conventions as logpsi_param_grad."""
+        p = self._pos(pos)
+        B = p.shape[0]
+        w = None
+        if weights is not None:
+            w = weights.to(self.device, self.dtype).contiguous()
+            if w.numel() != B:
+                raise ValueError("weights must have one entry per walker")
+            out = torch.empty(self.nparams, dtype=self.dtype, device=self.device)
+        else:
+            out = torch.empty(B, self.nparams, dtype=self.dtype, device=self.device)
+        ph = torch.empty(B, dtype=self.dtype, device=self.device) if want_phase else None
+        check(self._lib.aiqmc_phase_param_grad(self._h, _ptr(p), B, _ptr(w), _ptr(out), _ptr(ph),
+                                               _stream(self.device)), "aiqmc_phase_param_grad")
+        return (out, ph) if want_phase else out
 
     # -- DMC (DMC/drift_diffusion.py, S_matrix.py, dmc.py, branch.py) -------------
     def dmc_drift_diffusion(self, pos: torch.Tensor, tstep: float, gauss1=None, gauss2=None, u=None, seed: int = 0,

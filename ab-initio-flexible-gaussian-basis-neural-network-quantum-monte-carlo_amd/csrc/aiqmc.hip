@@ -700,8 +700,12 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
   return AIQMC_OK;
 }
 
-int aiqmc_logpsi_param_grad(aiqmc_ctx* c, const void* pos, int32_t B, const void* weights, void* out,
-                            void* logabs, void* stream) {
+}  // extern "C"
+
+// d log|psi| / d theta (phase = false) or d phase / d theta (phase = true), per walker or
+// weighted sum, in canonical order.  vals: log|psi| or phase at the walkers (optional).
+static int param_grad(aiqmc_ctx* c, const void* pos, int32_t B, const void* weights, void* out, void* vals,
+                      bool phase, void* stream) {
   int rc = check_call(c, pos, B);
   if (rc) return rc;
   if (B == 0) return AIQMC_OK;
@@ -731,7 +735,9 @@ int aiqmc_logpsi_param_grad(aiqmc_ctx* c, const void* pos, int32_t B, const void
   ka.nconf = B;
   ka.pos = pos;
   ka.grad = c->d_pg;
-  ka.logabs = logabs;
+  ka.logabs = phase ? nullptr : vals;
+  ka.phase = phase ? vals : nullptr;
+  ka.phase_grad = phase ? 1 : 0;
   rc = ops.pgrad(c->dtype, ka, B, s);
   if (rc) return rc;
   const int nk = (int)c->nkern, nc = (int)c->ncanon;
@@ -759,6 +765,18 @@ int aiqmc_logpsi_param_grad(aiqmc_ctx* c, const void* pos, int32_t B, const void
                                                          c->d_wnorm, c->N, rows, (double*)out);
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
+}
+
+extern "C" {
+
+int aiqmc_logpsi_param_grad(aiqmc_ctx* c, const void* pos, int32_t B, const void* weights, void* out,
+                            void* logabs, void* stream) {
+  return param_grad(c, pos, B, weights, out, logabs, false, stream);
+}
+
+int aiqmc_phase_param_grad(aiqmc_ctx* c, const void* pos, int32_t B, const void* weights, void* out, void* phase,
+                           void* stream) {
+  return param_grad(c, pos, B, weights, out, phase, true, stream);
 }
 
 int aiqmc_set_ecp(aiqmc_ctx* c, const aiqmc_ecp* e) {

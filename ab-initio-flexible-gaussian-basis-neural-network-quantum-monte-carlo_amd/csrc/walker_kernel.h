@@ -54,6 +54,7 @@ struct KArgs {
   int mper, mdiv;
   const void* xnew;
   int value_only;         // k_walker_rev: log|psi| and phase only (no backward pass)
+  int phase_grad;         // k_param_grad: d phase / d theta instead of d log|psi| / d theta
   // walker launch of a Metropolis sweep (k_walker_rev, PROP = false): dg1/dg2/du != nullptr:
   // lanes e < N of wave b write the sweep's Philox draws of walker b exactly as k_draws would
   // (one launch fewer per sweep).  (Fusing the limdrift reduction the same way, by the last wave

@@ -196,6 +196,7 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
   gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi);
   __syncthreads();
   // ---------------------------------------------------------------- reverse: orbitals (B1)
+  const bool phg = ka.phase_grad != 0;
   T* ybar = sm + SM::ybar;
   T* hb = sm + SM::hb;
   for (int idx = lane; idx < N * N; idx += 64) {
@@ -203,8 +204,10 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
     const int src = rowsrc[r], s = r < nup ? 0 : 1;
     const T br = Mx[(c * N + r) * 2], bi = Mx[(c * N + r) * 2 + 1];
     const T yt = Yv[idx];
-    const T pr_ = br * yt, pi_ = -bi * yt;          // dL/dPhi_re, dL/dPhi_im
-    ybar[idx] = br * Ph[idx * 2] - bi * Ph[idx * 2 + 1];
+    // log|det| = Re ln det: (Re B yt, -Im B yt), dYt = Re(B Phi); phase = Im ln det:
+    // (Im B yt, Re B yt), dYt = Im(B Phi)
+    const T pr_ = phg ? bi * yt : br * yt, pi_ = phg ? br * yt : -bi * yt;   // dL/dPhi_re, dL/dPhi_im
+    ybar[idx] = phg ? br * Ph[idx * 2 + 1] + bi * Ph[idx * 2] : br * Ph[idx * 2] - bi * Ph[idx * 2 + 1];
     lds_add(&pg[Ly::orb_b + (s * N + c) * 2], pr_);
     lds_add(&pg[Ly::orb_b + (s * N + c) * 2 + 1], pi_);
 #pragma unroll
@@ -220,7 +223,8 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
     for (int c = 0; c < N; ++c) {
       const T br = Mx[(c * N + r) * 2], bi = Mx[(c * N + r) * 2 + 1];
       const T yt = Yv[r * N + c];
-      a += P[Ly::orb_w + ((s * NH + f) * N + c) * 2] * br * yt - P[Ly::orb_w + ((s * NH + f) * N + c) * 2 + 1] * bi * yt;
+      const T wr = P[Ly::orb_w + ((s * NH + f) * N + c) * 2], wi = P[Ly::orb_w + ((s * NH + f) * N + c) * 2 + 1];
+      a += phg ? wr * bi * yt + wi * br * yt : wr * br * yt - wi * bi * yt;
     }
     hb[rowsrc[r] * NH + f] = a;
   }
@@ -275,7 +279,8 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
       const T bj = P[Ly::jae_b + i * A + a];
       const T c34 = P[Ly::c34 + a], c14 = P[Ly::c14 + a];
       const T ex = f_exp(-c14 * bj * ra[a]);
-      pg[Ly::jae_b + i * A + a] += c34 / (T(2) * bj * bj) * (T(1) - ex) - c34 / (T(2) * bj) * (c14 * ra[a] * ex);
+      if (!phg)   // the Jastrows are real: no phase
+        pg[Ly::jae_b + i * A + a] += c34 / (T(2) * bj * bj) * (T(1) - ex) - c34 / (T(2) * bj) * (c14 * ra[a] * ex);
     }
     pg[Ly::env_alpha + i] += envb * da;
     pg[Ly::env_xi + i] += envb * dxi;
@@ -510,7 +515,7 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
     for (int m = 0; m < 4; ++m)
 #pragma unroll
       for (int o = 0; o < 4; ++o) lds_add(&pg[Ly::dbl_w0 + m * 4 + o], p0[m] * z1[o]);
-    if (k < i) {   // Jastrow.py:23-52: cusp r / (1 + alpha r), alpha per unordered pair
+    if (k < i && !phg) {   // Jastrow.py:23-52: cusp r / (1 + alpha r), alpha per unordered pair
       const T cusp = P[Ly::jee_c + k * N + i], al = P[Ly::jee_a + k * N + i];
       const T den = al * r + T(1);
       pg[Ly::jee_a + k * N + i] += -cusp * r * r / (den * den);
@@ -522,6 +527,7 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
   for (int idx = lane; idx < Ly::total; idx += 64) out[idx] = pg[idx];
   const T lpsi = logdet + wave_sum(jae_v + jee_v);
   if (lane == 0 && ka.logabs) ((T*)ka.logabs)[conf] = lpsi;
+  if (lane == 0 && ka.phase) ((T*)ka.phase)[conf] = f_atan2(phi, phr);
 }
 
 // out[j] = sum_b w[b] O[b][j] over the kernel layout (deterministic order): one block of 256

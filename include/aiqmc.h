@@ -114,6 +114,14 @@ int aiqmc_mc_step(aiqmc_ctx* ctx, void* pos_inout, int32_t B, int32_t nsteps, do
 int aiqmc_logpsi_param_grad(aiqmc_ctx* ctx, const void* pos, int32_t B, const void* weights, void* out,
                             void* logabs, void* stream);
 
+/* Parameter gradient of the phase of psi (arg det A; the Jastrows are real), the imaginary
+ * part of psi_tangent when the driver differentiates the complex log
+ * log|psi| + i phase (Loss/loss.py:256-265 with complex_output=True, network = log_network
+ * of main_pp_adam_muti_GPU.py:119-121).  Same layout and weights convention as
+ * aiqmc_logpsi_param_grad; phase[B] (optional) receives the phase at the walkers. */
+int aiqmc_phase_param_grad(aiqmc_ctx* ctx, const void* pos, int32_t B, const void* weights, void* out,
+                           void* phase, void* stream);
+
 /* DMC drift-diffusion step (DMC/drift_diffusion.py:25-107): one Metropolis sweep
  * exactly as aiqmc_mc_step with nsteps = 1 (same draws, in place), plus
  *   grad_eff_old[B*3N]  limdrift(grad log|psi|) at the walkers before the move (:60-61),

@@ -88,3 +88,56 @@ class Adam:
         u = u * self.schedule(self.count)
         self.count += 1
         return params - u
+
+
+def phase_param_grad(net, params_np, pos: torch.Tensor) -> np.ndarray:
+    """[B, P] d phase(x_b) / d theta (phase = arg det, the imaginary part of the complex log
+    the pp drivers differentiate, main_pp_adam_muti_GPU.py:119-121), canonical order."""
+    pt = network.to_torch(params_np)
+    g = grad(lambda p, x: net.apply(p, x)[0])
+    rows = []
+    for b in range(pos.shape[0]):
+        gt = g(pt, pos[b])
+        rows.append(system.flatten_params(system.map_tree(lambda t: t.detach().numpy(), gt)))
+    return np.stack(rows)
+
+
+def phase_param_grad_fd(net, params_np, pos: torch.Tensor, h: float = 1e-6) -> np.ndarray:
+    """Central finite differences of the phase wrt every canonical parameter (pins the above)."""
+    flat = system.flatten_params(params_np)
+    rows = np.zeros((pos.shape[0], flat.size))
+    for k in range(flat.size):
+        for sgn in (1.0, -1.0):
+            f = flat.copy()
+            f[k] += sgn * h
+            pt = network.to_torch(system.unflatten_params(params_np, f))
+            ph = np.array([net.apply(pt, pos[b])[0].item() for b in range(pos.shape[0])])
+            rows[:, k] += sgn * ph / (2 * h)
+    return rows
+
+
+def energy_gradient_complex(e_l: np.ndarray, O_abs: np.ndarray, O_phase: np.ndarray, clip_scale: float = 5.0,
+                            clip_from_median: bool = False, center_at_clipped_energy: bool = True,
+                            complex_output: bool = True):
+    """loss.py:220-270 literally, for complex E_L and psi_tangent = O_abs + i O_phase
+    (network = the complex log of the pp drivers): returns (loss, grad [P])."""
+    e_l = np.asarray(e_l, dtype=np.complex128)
+    loss = np.mean(e_l)
+    if clip_scale > 0:
+        center = np.median(e_l.real) if clip_from_median else loss
+        tv_r = np.mean(np.abs(e_l.real - center.real))
+        tv_i = np.mean(np.abs(e_l.imag - np.imag(center)))
+        clipped = (np.clip(e_l.real, center.real - clip_scale * tv_r, center.real + clip_scale * tv_r)
+                   + 1j * np.clip(e_l.imag, np.imag(center) - clip_scale * tv_i, np.imag(center) + clip_scale * tv_i))
+        diff_center = np.mean(clipped) if center_at_clipped_energy else loss
+        aux_clipped, diff = diff_center, clipped - diff_center
+    else:
+        aux_clipped, diff = e_l, e_l - loss
+    B = e_l.shape[0]
+    psi_t = O_abs + 1j * O_phase                                   # [B, P]
+    if complex_output:
+        clipped_el = diff + aux_clipped
+        term1 = clipped_el @ np.conj(psi_t) + np.conj(clipped_el) @ psi_t
+        term2 = (aux_clipped * np.ones(B)) @ psi_t.real
+        return loss.real, (term1 - 2 * term2).real / B
+    return loss, (diff @ psi_t) / B

@@ -66,3 +66,67 @@ def test_param_grad_full_batch_finite():
     O = ctx.logpsi_param_grad(x[:64])
     torch.cuda.synchronize()
     assert torch.isfinite(g).all() and torch.isfinite(O).all()
+
+
+@pytest.mark.parametrize("name", ["H2", "Be", "N2"])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_phase_param_grad_matches_oracle(name, dtype):
+    """d phase / d theta (aiqmc_phase_param_grad) vs torch.func.grad of the oracle's phase
+    (itself pinned by finite differences in tests/test_oracle_loss.py)."""
+    from oracle import loss, network
+    s, ctx, params, pos = _setup(name, dtype, seed=43)
+    g, ph = ctx.phase_param_grad(torch.tensor(pos, dtype=dtype, device="cuda"), want_phase=True)
+    torch.cuda.synchronize()
+    ref = loss.phase_param_grad(network.Network(s), params, torch.tensor(pos))
+    got = g.double().cpu().numpy()
+    tol = 1e-8 if dtype == torch.float64 else 2e-3
+    scale = np.abs(ref).max(axis=1, keepdims=True) + 1e-3
+    err = np.abs(got - ref) / scale
+    assert err.max() < tol, (err.max(), np.unravel_index(err.argmax(), err.shape))
+    _, ph_ref = ctx.logpsi(torch.tensor(pos, dtype=dtype, device="cuda"))
+    ptol = 1e-9 if dtype == torch.float64 else 1e-3   # two different fp32 kernels (pgrad vs walker)
+    np.testing.assert_allclose(ph.double().cpu().numpy(), ph_ref.double().cpu().numpy(), rtol=ptol, atol=ptol)
+    # the Jastrow parameters carry no phase
+    assert np.abs(got[:, np.abs(ref).max(axis=0) == 0]).max(initial=0.0) < 1e-12
+
+
+def test_complex_energy_gradient_pp_loss():
+    """make_loss(complex_output=True) on complex pp local energies (C-atom ccECP, the
+    main_pp_adam_muti_GPU.py:150-156 configuration): the gradient equals the literal
+    custom-JVP tangent of the oracle built from the per-walker d log|psi| and d phase rows."""
+    from oracle import loss as oloss, pphamiltonian as opp, system
+    from aiqmc import spin_indices
+    from aiqmc.Energy import pphamiltonian
+    from aiqmc.Loss import loss as L
+    from aiqmc.VMC.VMCmcstep import PhiloxKey
+    from aiqmc.wavefunction_Ynlm import nn
+    s = system.make_system("C_ecp")
+    par, anti, npar, nanti = spin_indices.jastrow_indices_ee(spins=s.spins, nelectrons=4)
+    up, dn = spin_indices.spin_indices_h(s.spins)
+    network = nn.make_ai_net(ndim=3, nelectrons=4, natoms=1, nspins=(2, 2), charges=s.charges,
+                             parallel_indices=par, antiparallel_indices=anti, n_parallel=npar,
+                             n_antiparallel=nanti, spin_up_indices=up, spin_down_indices=dn)
+    params = system.init_params(np.random.default_rng(12), s, randomize_aux=True)
+    e = opp.c_atom_ccecp()
+    le = pphamiltonian.local_energy(f=network.apply, lognetwork=nn.make_log_network(network.apply),
+                                    charges=s.charges, nspins=s.spins, rn_local=e.rn_local,
+                                    local_coes=e.local_coes, local_exps=e.local_exps,
+                                    rn_non_local=e.rn_non_local, non_local_coes=e.non_local_coes,
+                                    non_local_exps=e.non_local_exps, natoms=1, nelectrons=4, ndim=3, list_l=2)
+    B = 256
+    pos = torch.tensor(system.init_electrons(np.random.default_rng(13), s.atoms, s.charges, B, 1.0), device="cuda")
+    data = nn.AINetData(positions=pos, spins=s.spins, atoms=s.atoms, charges=s.charges)
+    key = PhiloxKey(4, 0)
+    e_l, _ = le(params, key, data)
+    assert bool((e_l.imag != 0).any())
+    ctx = network.apply._aiqmc_network.bind(params, s.atoms, torch.float64)
+    Oa = ctx.logpsi_param_grad(pos).cpu().numpy()
+    Op = ctx.phase_param_grad(pos).cpu().numpy()
+    for clip in (5.0, 0.0):
+        ev = L.make_loss(network=nn.make_log_network(network.apply), local_energy=le, clip_local_energy=clip,
+                         clip_from_median=False, center_at_clipped_energy=True, complex_output=True)
+        (lv, aux), g = ev.value_and_grad(params, key, data)
+        torch.cuda.synchronize()
+        l_ref, g_ref = oloss.energy_gradient_complex(e_l.cpu().numpy(), Oa, Op, clip_scale=clip)
+        assert abs(lv.real.item() - l_ref) < 1e-10
+        np.testing.assert_allclose(g.cpu().numpy(), g_ref, rtol=1e-9, atol=1e-11 * np.abs(g_ref).max())

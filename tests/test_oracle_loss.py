@@ -49,3 +49,29 @@ def test_adam_restatement():
     p2 = opt.update(g, p1)
     assert loss.lr_schedule(1) == 0.05 * 2.0 ** -10000   # the reference schedule collapses after step 0
     np.testing.assert_allclose(p2, p1, atol=1e-300)
+
+
+def test_complex_energy_gradient_reduces_to_weights():
+    """The literal custom-JVP tangent (term1 - 2 term2).real / B for complex E_L equals
+    (2/B) sum_b [Re(diff_b) O_abs_b + Im(cl_b) O_phase_b], cl = diff + aux.clipped_energy
+    (the clip centre when clipping, E_L itself when not) -- the form the GPU path uses."""
+    from oracle import loss
+    rng = np.random.default_rng(3)
+    B, P = 40, 7
+    e = rng.normal(-5, 1, B) + 1j * rng.normal(0, 0.3, B)
+    e[3] += 9.0 + 4.0j                       # outlier: exercises both clip windows
+    Oa, Op = rng.standard_normal((B, P)), rng.standard_normal((B, P))
+    for clip in (5.0, 0.0):
+        _, g = loss.energy_gradient_complex(e, Oa, Op, clip_scale=clip)
+        if clip > 0:
+            m = e.mean()
+            tr, ti = np.mean(np.abs(e.real - m.real)), np.mean(np.abs(e.imag - m.imag))
+            c = np.clip(e.real, m.real - clip * tr, m.real + clip * tr) + 1j * np.clip(
+                e.imag, m.imag - clip * ti, m.imag + clip * ti)
+            center = c.mean()
+            diff, cl = c - center, c
+        else:
+            diff = e - e.mean()
+            cl = diff + e
+        want = (2.0 / B) * (diff.real @ Oa + cl.imag @ Op)
+        np.testing.assert_allclose(g, want, rtol=1e-12, atol=1e-12)
