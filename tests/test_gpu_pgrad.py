@@ -130,3 +130,48 @@ def test_complex_energy_gradient_pp_loss():
         l_ref, g_ref = oloss.energy_gradient_complex(e_l.cpu().numpy(), Oa, Op, clip_scale=clip)
         assert abs(lv.real.item() - l_ref) < 1e-10
         np.testing.assert_allclose(g.cpu().numpy(), g_ref, rtol=1e-9, atol=1e-11 * np.abs(g_ref).max())
+
+
+def test_pp_adam_training_step():
+    """One Adam step driven like main_pp_adam_muti_GPU.py:150-190 (complex pp E_L, clip 5.0,
+    complex_output=True): parameters == the oracle Adam update of the literal custom-JVP
+    gradient built from the same E_L and per-walker gradient rows."""
+    from oracle import loss as oloss, pphamiltonian as opp, system
+    from aiqmc import spin_indices
+    from aiqmc.Energy import pphamiltonian
+    from aiqmc.Loss import loss as L
+    from aiqmc.Optimizer import adam, optax_like as optax
+    from aiqmc.VMC.VMCmcstep import PhiloxKey
+    from aiqmc.wavefunction_Ynlm import nn
+    s = system.make_system("C_ecp")
+    par, anti, npar, nanti = spin_indices.jastrow_indices_ee(spins=s.spins, nelectrons=4)
+    up, dn = spin_indices.spin_indices_h(s.spins)
+    network = nn.make_ai_net(ndim=3, nelectrons=4, natoms=1, nspins=(2, 2), charges=s.charges,
+                             parallel_indices=par, antiparallel_indices=anti, n_parallel=npar,
+                             n_antiparallel=nanti, spin_up_indices=up, spin_down_indices=dn)
+    params = system.init_params(np.random.default_rng(14), s, randomize_aux=True)
+    e = opp.c_atom_ccecp()
+    log_network = nn.make_log_network(network.apply)
+    le = pphamiltonian.local_energy(f=network.apply, lognetwork=log_network, charges=s.charges, nspins=s.spins,
+                                    rn_local=e.rn_local, local_coes=e.local_coes, local_exps=e.local_exps,
+                                    rn_non_local=e.rn_non_local, non_local_coes=e.non_local_coes,
+                                    non_local_exps=e.non_local_exps, natoms=1, nelectrons=4, ndim=3, list_l=2)
+    ev = L.make_loss(network=log_network, local_energy=le, clip_local_energy=5.0, clip_from_median=False,
+                     center_at_clipped_energy=True, complex_output=True)
+    opt = optax.chain(optax.scale_by_adam(b1=0.9, b2=0.999, eps=1e-8, eps_root=0.0),
+                      optax.scale_by_schedule(lambda t: 0.05 * (1.0 / (1.0 + t)) ** 10000), optax.scale(-1.))
+    step = adam.make_training_step(adam.make_opt_update_step(ev, opt))
+    B = 128
+    pos = torch.tensor(system.init_electrons(np.random.default_rng(15), s.atoms, s.charges, B, 1.0), device="cuda")
+    data = nn.AINetData(positions=pos, spins=s.spins, atoms=s.atoms, charges=s.charges)
+    key = PhiloxKey(6, 0)
+    _, new_params, state, loss_v, aux = step(data, params, None, key)
+    torch.cuda.synchronize()
+    e_l, _ = le(params, key, data)
+    ctx = network.apply._aiqmc_network.bind(params, s.atoms, torch.float64)
+    Oa, Op = ctx.logpsi_param_grad(pos).cpu().numpy(), ctx.phase_param_grad(pos).cpu().numpy()
+    l_ref, g_ref = oloss.energy_gradient_complex(e_l.cpu().numpy(), Oa, Op, clip_scale=5.0)
+    flat = system.flatten_params(params)
+    p_ref = oloss.Adam(flat.size).update(g_ref, flat)
+    assert abs(float(loss_v.real) - l_ref) < 1e-9
+    np.testing.assert_allclose(system.flatten_params(new_params), p_ref, rtol=1e-9, atol=1e-9)
