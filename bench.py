@@ -178,6 +178,57 @@ def ecp_side_bench(dtype, device, walkers, steps, cpu_baseline_on):
     return res
 
 
+def pp_adam_side_bench(dtype, device, walkers, steps):
+    """main_pp_adam_muti_GPU.py:150-190 on the C-atom ccECP config: one training iteration =
+    mc_step (10 sweeps) + complex pp local energy + complex-E_L energy gradient (d log|psi| and
+    d phase parameter gradients) + Adam update, through the drop-in API."""
+    from aiqmc import spin_indices
+    from aiqmc.Energy import pphamiltonian
+    from aiqmc.Loss import loss as L
+    from aiqmc.Optimizer import adam, optax_like as optax
+    from aiqmc.VMC import VMCmcstep
+    from aiqmc.wavefunction_Ynlm import nn
+    from aiqmc.initial_electrons_positions.init import init_electrons
+    from oracle import pphamiltonian as opp, system as osys
+    s = osys.make_system("C_ecp")
+    par, anti, npar, nanti = spin_indices.jastrow_indices_ee(s.spins, 4)
+    up, dn = spin_indices.spin_indices_h(s.spins)
+    network = nn.make_ai_net(nspins=(2, 2), charges=s.charges, parallel_indices=par, antiparallel_indices=anti,
+                             spin_up_indices=up, spin_down_indices=dn, n_parallel=npar, n_antiparallel=nanti,
+                             ndim=3, natoms=1, nelectrons=4)
+    params = network.init(4)
+    e = opp.c_atom_ccecp()
+    log_network = nn.make_log_network(network.apply)
+    le = pphamiltonian.local_energy(f=network.apply, lognetwork=log_network, charges=s.charges, nspins=s.spins,
+                                    rn_local=e.rn_local, local_coes=e.local_coes, local_exps=e.local_exps,
+                                    rn_non_local=e.rn_non_local, non_local_coes=e.non_local_coes,
+                                    non_local_exps=e.non_local_exps, natoms=1, nelectrons=4, ndim=3, list_l=2)
+    ev = L.make_loss(network=log_network, local_energy=le, clip_local_energy=5.0, clip_from_median=False,
+                     center_at_clipped_energy=True, complex_output=True)
+    opt = optax.chain(optax.scale_by_adam(b1=0.9, b2=0.999, eps=1e-8, eps_root=0.0),
+                      optax.scale_by_schedule(lambda t: 0.05 * (1.0 / (1.0 + t)) ** 10000), optax.scale(-1.))
+    step = adam.make_training_step(adam.make_opt_update_step(ev, opt))
+    mc_step = VMCmcstep.main_monte_carlo(f=network.apply, tstep=0.05, ndim=3, nelectrons=4, nsteps=10,
+                                         batch_size=walkers)
+    pos, sp = init_electrons(17, None, s.atoms, s.charges, s.spins, walkers, 1.0)
+    data = nn.AINetData(positions=pos.to(device, dtype).contiguous(), spins=sp, atoms=s.atoms, charges=s.charges)
+    state = None
+    for t in range(2):
+        data = mc_step(params, data, VMCmcstep.PhiloxKey(19, 10 * t))
+        data, params, state, loss_v, aux = step(data, params, state, VMCmcstep.PhiloxKey(23, t))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(steps):
+        data = mc_step(params, data, VMCmcstep.PhiloxKey(19, 100 + 10 * t))
+        data, params, state, loss_v, aux = step(data, params, state, VMCmcstep.PhiloxKey(23, 100 + t))
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    lv = float(loss_v.real) if torch.is_tensor(loss_v) else float(loss_v)
+    return {"config": "C atom ccECP, Adam: mc_step (10 sweeps) + complex pp E_L + complex energy gradient + Adam",
+            "walkers": walkers, "ms_per_iteration": 1e3 * dt, "iterations_per_s": 1.0 / dt,
+            "energy": lv, "finite": bool(math.isfinite(lv))}
+
+
 def dmc_side_bench(dtype, device, walkers, steps):
     """DMC propagation through the drop-in API (DMC/dmc.py:72-93 + branch.py, as main_dmc.py:160-210
     drives it): T-moves, drift-diffusion, pp local energies before/after, weight update, stochastic
@@ -289,12 +340,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; if fewer GPUs than ranks are visible (a rehearsal), ranks share devices.
+    # The device is bound before the process group so RCCL's communicator uses it.
+    local_dev = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group(args.dist_backend if torch.cuda.is_available() else "gloo")
-    # one process per GPU; if fewer GPUs than ranks are visible (a rehearsal), ranks share devices
-    local_dev = local_rank % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
     dtype = torch.float32 if args.dtype == "f32" else torch.float64
     from aiqmc import constants, _lib
@@ -411,6 +463,11 @@ def main():
                 out["adam_be_atom"] = adam_side_bench(dtype, dev, 4096, 5)
             except Exception as e:  # a side measurement, never a failure of the headline bench
                 out["adam_be_atom"] = {"error": repr(e)}
+        if world == 1 and not args.no_adam:
+            try:
+                out["pp_adam_c_atom"] = pp_adam_side_bench(dtype, dev, 4096, 5)
+            except Exception as e:  # a side measurement, never a failure of the headline bench
+                out["pp_adam_c_atom"] = {"error": repr(e)}
         if world == 1 and not args.no_dmc:
             try:
                 out["dmc_c_atom"] = dmc_side_bench(dtype, dev, 4096, 5)
