@@ -530,7 +530,7 @@ k_walker_rev(KArgs ka) {
         gown[1][t] = class4_sum(inG1 ? x : T(0)) * ginv1;
       }
     }
-    T cq[SM::QM];
+    T zc[SM::QM];
 #pragma unroll
     for (int q = 0; q < SM::QM; ++q) {
       if (q < Q) {
@@ -541,7 +541,31 @@ k_walker_rev(KArgs ka) {
         T z = F * convw[4 * q + ff];
         z += dpp<0xB1>(z);
         z += dpp<0x4E>(z);
-        cq[q] = f_tanh(z * T(0.25) + convb[q]);
+        zc[q] = z;
+      }
+    }
+    // the tanh's of a full quad of outputs 4s..4s+3 are spread over the quad (lane f
+    // evaluates output 4s + f, one transcendental pair instead of four) and broadcast
+    // back by DPP; the Q mod 4 remaining outputs are evaluated by every lane
+    const int QF = Q / 4;
+    T cq[SM::QM];
+#pragma unroll
+    for (int s4 = 0; s4 < SM::QM / 4; ++s4) {
+      if (s4 < QF) {
+        const int q0 = 4 * s4;
+        const T zs = ff == 0 ? zc[q0] : (ff == 1 ? zc[q0 + 1] : (ff == 2 ? zc[q0 + 2] : zc[q0 + 3]));
+        const T c = f_tanh(zs * T(0.25) + convb[q0 + ff]);
+        if (ilive) cqv[(l * N + ic) * SM::QM + q0 + ff] = c;
+        cq[q0 + 0] = quad_bcast<0>(c);
+        cq[q0 + 1] = quad_bcast<1>(c);
+        cq[q0 + 2] = quad_bcast<2>(c);
+        cq[q0 + 3] = quad_bcast<3>(c);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < SM::QM; ++q) {
+      if (q >= 4 * QF && q < Q) {
+        cq[q] = f_tanh(zc[q] * T(0.25) + convb[q]);
         if (ilive && (q & 3) == ff) cqv[(l * N + ic) * SM::QM + q] = cq[q];
       }
     }
@@ -685,26 +709,44 @@ k_walker_rev(KArgs ka) {
       }
       const T zq[4] = {quad_bcast<0>(zs), quad_bcast<1>(zs), quad_bcast<2>(zs), quad_bcast<3>(zs)};
       // conv: c = tanh(0.25 sum F w + b); fb[q] = adjoint of input 4q + f
-      T fb[SM::QM];
+      // cg[q] = tanh'(conv q) * 0.25 * (adjoint of conv output q) is the same on the four
+      // lanes of an electron: for a full quad of outputs 4s..4s+3 lane f forms output 4s + f
+      // and DPP broadcasts it (as the forward tanh's); the Q mod 4 rest on every lane
+      const int QF = Q / 4;
+      T cg[SM::QM];
 #pragma unroll
       for (int q = 0; q < SM::QM; ++q) {
-        if (q < Q) {
+        const bool full = q < 4 * QF;
+        if (q < Q && (!full || (q & 3) == 0)) {
+          const int qq = full ? q + ff : q;     // output this lane forms
           T cb = T(0);
 #pragma unroll
-          for (int m = 0; m < 4; ++m) cb += zq[m] * sngw[q * 4 + m];
-          const T c = cqv[(l * N + ic) * SM::QM + q];
-          fb[q] = cb * (T(1) - c * c) * T(0.25) * convw[4 * q + ff];
+          for (int m = 0; m < 4; ++m) cb += zq[m] * sngw[qq * 4 + m];
+          const T c = cqv[(l * N + ic) * SM::QM + qq];
+          const T g = cb * (T(1) - c * c) * T(0.25);
           if constexpr (PREP) {
             // conv node (stored once, by the lane of its quad position): tanh', abar * tanh''
-            if (ilive && (q & 3) == ff) {
+            if (ilive && (qq & 3) == ff) {
               const T c1 = T(1) - c * c;
-              T* cn = Lw + l * LCc::layer_n + LCc::cn + (ic * LCc::QM + q) * 2;
+              T* cn = Lw + l * LCc::layer_n + LCc::cn + (ic * LCc::QM + qq) * 2;
               cn[0] = c1;
               cn[1] = T(-2) * c * c1 * cb;
             }
           }
+          if (full) {
+            cg[q + 0] = quad_bcast<0>(g);
+            cg[q + 1] = quad_bcast<1>(g);
+            cg[q + 2] = quad_bcast<2>(g);
+            cg[q + 3] = quad_bcast<3>(g);
+          } else {
+            cg[q] = g;
+          }
         }
       }
+      T fb[SM::QM];
+#pragma unroll
+      for (int q = 0; q < SM::QM; ++q)
+        if (q < Q) fb[q] = cg[q] * convw[4 * q + ff];
       // g2 adjoints (inputs 3 d1 + 4G + f), consumed by B3
       if (ilive) {   // pre-scaled by the group-mean weights 1/|G| of the pair sums
         g2b[((l * 2 + 0) * N + ic) * 4 + ff] = fb[3 * T4 + 0] * ginv0;
