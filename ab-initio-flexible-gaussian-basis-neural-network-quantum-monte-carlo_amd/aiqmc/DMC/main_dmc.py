@@ -11,15 +11,24 @@ the driver's walker re-indexing (:204-233, ``reindex_walkers``), e_trial feedbac
 ``DMC_states`` CSV row (:239-244).
 
 One process per GPU (torchrun); ``batch_size`` is the global walker count, each rank owns
-batch_size / world walkers.  Kept from the reference: esigma = std over the per-device copies
-of the (already pmean'd) e_est, which is 0, so the branch cut passed to the weight update is 0
-(:118, :137); weights are per device.  Deviations (documented in DESIGN.md): the Philox key
-offset advances every step (the reference passes the same ``subkeys`` to every step, :162);
-the re-indexing pads each device block to its own walker count (the reference compares the
-unique count with the GLOBAL batch_size, which only reshapes back on one device, :219-229).
+batch_size / world walkers.  Kept from the reference:
+* ``total_e`` returns the PER-WALKER pp energies (DMC/total_energy.py:32), so the first
+  block runs with per-walker e_trial = e_est = those energies (:115-116), and
+  esigma = jnp.std(e_est) over every walker of every device (:118) = sqrt of total_e's
+  pmean'd variance; the branch cut passed to the weight update is 10 esigma (:137, :162);
+* the energy cut of comput_S is one minimum over all devices (aiqmc.DMC.dmc: MIN all-reduce);
+* the block estimate is the weighted average over all blocks so far and all devices (:190);
+* e_trial feedback uses jnp.mean over the per-device comb weights (:237): all-reduced here.
+Multi-rank housekeeping: rank 0 alone writes the checkpoint and the CSV, with the positions
+of all ranks gathered (the reference's arrays are global).  Deviations (documented in
+DESIGN.md): the Philox key offset advances every step (the reference passes the same
+``subkeys`` to every step, :162); the re-indexing pads each device block to its own walker
+count (the reference compares the unique count with the GLOBAL batch_size, which only
+reshapes back on one device, :219-229).
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import time
 from typing import Optional, Tuple
@@ -51,6 +60,78 @@ def reindex_walkers(x1: torch.Tensor, newindices: torch.Tensor, extra_uniform: t
         extra = temp[-1] + extra_uniform[:n].to(x1.device, x1.dtype)
         temp = torch.cat([temp, extra], dim=0)
     return temp.contiguous()
+
+
+def _gather_walkers(x: torch.Tensor, world: int) -> torch.Tensor:
+    """The global walker array (rank-major, the reference's [ndev, B] reshape) on every rank."""
+    if world == 1:
+        return x
+    parts = [torch.empty_like(x) for _ in range(world)]
+    dist.all_gather(parts, x.contiguous())
+    return torch.cat(parts, dim=0)
+
+
+def dmc_blocks(run, ctx, params, data, e_l0, variance0, nblocks: int, iterations: int, feedback: float,
+               step_key, block_draws, t_init: int = 0, on_block=None, writer=None):
+    """The block loop of main_dmc.py:113-244 over this rank's walkers.
+
+    run: dmc_propagate_run; ctx: the bound HIP context (comb); e_l0 [B] / variance0: total_e of
+    the starting walkers (per-walker e_trial = e_est = e_l0 in the first block, esigma =
+    sqrt(variance0) = jnp.std(e_est), :113-118); step_key(step) -> the key of one
+    dmc_propagate_run call (PhiloxKey or HostDmcDraws); block_draws(block) -> (u, extra) with
+    u the comb's uniform (branch.py:17) and extra [B,3N] the re-indexing noise (:222).
+    Returns (block estimates, data, weights, trace) -- trace holds per-step energies / weights
+    and per-block comb indices for the parity tests."""
+    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    B = data.positions.shape[0]
+    dev = data.positions.device
+    dtype = data.positions.dtype
+    e_trial = e_l0
+    e_est = e_l0
+    esigma = float(torch.sqrt(torch.as_tensor(variance0).real.clamp(min=0)).item())   # :118 jnp.std(e_est)
+    weights = torch.ones(B, dtype=dtype, device=dev)
+    branchcut_start = torch.full((B,), 10.0, dtype=torch.float64)
+    energy_data = torch.zeros(nblocks, iterations, B, dtype=torch.float64, device=dev)
+    weights_data = torch.zeros_like(energy_data)
+    estimates = []
+    trace = {"energy": [], "weights": [], "positions": [], "newinds": [], "comb_weight": [], "e_trial": []}
+    step = 0
+    for block in range(nblocks):
+        for t in range(t_init, t_init + iterations):
+            energy, weights, data = run(params, step_key(step), data, weights, branchcut_start * esigma, e_trial,
+                                        e_est)
+            step += 1
+            energy_data[block, t - t_init] = energy.real.to(torch.float64)
+            weights_data[block, t - t_init] = weights.to(torch.float64)
+            trace["energy"].append(energy.detach().clone())
+            trace["weights"].append(weights.detach().clone())
+            trace["positions"].append(data.positions.detach().clone())
+        # :190 jnp.average over the global [nblocks, iterations, batch] arrays
+        v = torch.stack([(energy_data * weights_data).sum(), weights_data.sum()])
+        if world > 1:
+            dist.all_reduce(v)
+        e_est = complex((v[0] / v[1]).item())
+        logging.info('Block %05d: %03.4f E_h', block, e_est.real)
+        if on_block is not None:
+            on_block(block, e_est, data)
+        u, extra = block_draws(block)
+        wn, newinds = ctx.dmc_branch(weights, float(u))                 # :202
+        weights = wn.expand(B).contiguous()
+        x2 = reindex_walkers(data.positions, newinds, extra)           # :204-233
+        data = nn.AINetData(positions=x2, spins=data.spins, atoms=data.atoms, charges=data.charges)
+        wmean = wn.to(torch.float64).reshape(1).clone()               # :237 jnp.mean over the devices' weights
+        if world > 1:
+            dist.all_reduce(wmean)
+            wmean /= world
+        e_trial = complex(e_est.real - feedback * float(torch.log(wmean).item()), 0.0)
+        estimates.append(e_est.real)
+        trace["newinds"].append(newinds.detach().clone())
+        trace["comb_weight"].append(float(wn.item()))
+        trace["e_trial"].append(e_trial.real)
+        all_x2 = _gather_walkers(x2, world)
+        if writer is not None:
+            writer.write(block, block=block, energy=e_est.real, positions=np.asarray(all_x2.cpu()))
+    return estimates, data, weights, trace
 
 
 def main(atoms, charges, spins, tstep: float, nelectrons: int, nsteps: int, natoms: int, ndim: int,
@@ -94,49 +175,32 @@ def main(atoms, charges, spins, tstep: float, nelectrons: int, nsteps: int, nato
     data = nn.AINetData(positions=pos.to(dev, dtype).contiguous(), spins=data.spins, atoms=data.atoms,
                         charges=data.charges)
     key0 = PhiloxKey(seed + 7919 * rank, 0)
-    e_l, _ = total_e(params, key0, data)
-    from .. import constants
-    e_trial = complex(constants.pmean(e_l.mean()))                 # :115 (pmean'd inside total_e)
-    e_est = e_trial
-    esigma = float(np.std(np.full(world, e_est.real)))            # :118 -- 0 by construction
-    weights = torch.ones(device_batch_size, dtype=dtype, device=dev)
-    branchcut_start = torch.full((device_batch_size,), 10.0, dtype=torch.float64)
+    e_l0, variance0 = total_e(params, key0, data)                  # :113-116 (e_trial, e_est per walker)
     run = dmc_propagate(signed_network, log_network, signed_network, 2, nelectrons, natoms, ndim,
                         device_batch_size, tstep, nsteps, charges, spins, Rn_local, Local_coes, Local_exps,
                         Rn_non_local, Non_local_coes, Non_local_exps)
     ctx = network.apply._aiqmc_network.bind(params, data.atoms, dtype)
     rng = np.random.default_rng(seed + rank)
-    energy_data = torch.zeros(nblocks, iterations, device_batch_size, dtype=torch.float64, device=dev)
-    weights_data = torch.zeros_like(energy_data)
-    time_of_last_ckpt = time.time()
-    estimates = []
-    step = 0
-    with writers.Writer(name='DMC_states', schema=['block', 'energy', 'positions'],
-                        directory=ckpt_restore_path or ckpt_save_path, iteration_key=None, log=False) as writer:
-        for block in range(nblocks):
-            for t in range(t_init, t_init + iterations):
-                energy, weights, data = run(params, PhiloxKey(key0.seed, step), data, weights,
-                                            branchcut_start * esigma, e_trial.real, e_est.real)
-                step += 1
-                energy_data[block, t - t_init] = energy.real.to(torch.float64)
-                weights_data[block, t - t_init] = weights.to(torch.float64)
-            e_est = complex(estimate_energy(energy_data, weights_data).item())
-            if world > 1:   # the reference's estimate is over the global arrays
-                v = torch.tensor([(energy_data * weights_data).sum().item(), weights_data.sum().item()],
-                                 dtype=torch.float64, device=dev)
-                dist.all_reduce(v)
-                e_est = complex((v[0] / v[1]).item())
-            logging.info('Block %05d: %03.4f E_h', block, e_est.real)
-            if time.time() - time_of_last_ckpt > save_frequency * 60:
-                checkpoint.save(ckpt_restore_path or ckpt_save_path, block, data, params, opt_state)
-                time_of_last_ckpt = time.time()
-            wn, newinds = ctx.dmc_branch(weights, float(rng.uniform()))
-            weights = wn.expand(device_batch_size).contiguous()
-            x2 = reindex_walkers(data.positions, newinds,
-                                 torch.tensor(rng.uniform(size=(device_batch_size, nelectrons * ndim))))
-            data = nn.AINetData(positions=x2, spins=data.spins, atoms=data.atoms, charges=data.charges)
-            e_trial = complex(e_est.real - feedback * float(torch.log(weights.mean()).real), 0.0)
-            estimates.append(e_est.real)
+    out_dir = ckpt_restore_path or ckpt_save_path
+    last_ckpt = [time.time()]
+
+    def on_block(block, e_est, data):
+        if time.time() - last_ckpt[0] > save_frequency * 60:
+            all_pos = _gather_walkers(data.positions, world)
             if rank == 0:
-                writer.write(block, block=block, energy=e_est.real, positions=np.asarray(x2.cpu()))
+                checkpoint.save(out_dir, block, nn.AINetData(positions=all_pos, spins=data.spins, atoms=data.atoms,
+                                                             charges=data.charges), params, opt_state)
+            if world > 1:
+                dist.barrier()
+            last_ckpt[0] = time.time()
+
+    writer = writers.Writer(name='DMC_states', schema=['block', 'energy', 'positions'], directory=out_dir,
+                            iteration_key=None, log=False) if rank == 0 else contextlib.nullcontext()
+    with writer:
+        estimates, data, weights, _ = dmc_blocks(
+            run, ctx, params, data, e_l0, variance0, nblocks, iterations, feedback, t_init=t_init,
+            step_key=lambda step: PhiloxKey(key0.seed, step),
+            block_draws=lambda block: (float(rng.uniform()),
+                                       torch.tensor(rng.uniform(size=(device_batch_size, nelectrons * ndim)))),
+            on_block=on_block, writer=writer if rank == 0 else None)
     return estimates, data, weights

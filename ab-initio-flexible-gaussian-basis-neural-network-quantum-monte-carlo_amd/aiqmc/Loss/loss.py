@@ -47,12 +47,17 @@ def clip_local_values(local_values: torch.Tensor, mean_local_values: torch.Tenso
         return torch.clamp(values, center - scale * tv, center + scale * tv)
 
     if clip_from_median:
-        center = torch.median(constants.all_gather(local_values).real.reshape(-1))
+        # jnp.median: the mean of the two middle values for an even count (torch.median would
+        # return the lower one)
+        center = torch.quantile(constants.all_gather(local_values).real.reshape(-1), 0.5)
     else:
         center = mean_local_values
     if torch.is_complex(local_values):
-        clipped = torch.complex(clip_at_total_variation(local_values.real, center.real, clip_scale),
-                                clip_at_total_variation(local_values.imag, center.imag, clip_scale))
+        # the median centre is real (.real before the median); JAX's .imag of a real array is 0
+        c_re = center.real if torch.is_complex(center) else center
+        c_im = center.imag if torch.is_complex(center) else torch.zeros_like(center)
+        clipped = torch.complex(clip_at_total_variation(local_values.real, c_re, clip_scale),
+                                clip_at_total_variation(local_values.imag, c_im, clip_scale))
     else:
         clipped = clip_at_total_variation(local_values, center, clip_scale)
     diff_center = batch_mean(clipped) if center_at_clipped_value else mean_local_values

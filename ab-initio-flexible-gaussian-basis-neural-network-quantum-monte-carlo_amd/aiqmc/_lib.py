@@ -32,6 +32,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_debug_set_proposal_reuse", "aiqmc_debug_phase_cycles", "aiqmc_debug_local_energy_forward",
     "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
     "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves", "aiqmc_phase_param_grad",
+    "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -98,6 +99,7 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_set_params.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i64, vp]
     lib.aiqmc_logpsi.argtypes = [vp, vp, i32, vp, vp, vp]
     lib.aiqmc_logpsi_grad.argtypes = [vp, vp, i32, vp, vp, vp]
+    lib.aiqmc_orbitals.argtypes = [vp, vp, i32, vp, vp, vp, vp]
     lib.aiqmc_local_energy.argtypes = [vp, vp, i32, vp, vp, vp, vp]
     lib.aiqmc_mc_step.argtypes = [vp, vp, i32, i32, ctypes.c_double, i32, vp, vp, vp,
                                   ctypes.c_uint64, ctypes.c_uint64, vp, vp]
@@ -114,6 +116,8 @@ def load() -> ctypes.CDLL:
     dbl, u64 = ctypes.c_double, ctypes.c_uint64
     lib.aiqmc_dmc_drift_diffusion.argtypes = [vp, vp, i32, dbl, i32, vp, vp, vp, u64, u64, vp, vp, vp, vp]
     lib.aiqmc_dmc_weights.argtypes = [vp, i32, vp, vp, vp, vp, vp, dbl, dbl, dbl, dbl, vp, vp]
+    lib.aiqmc_dmc_weights_ex.argtypes = [vp, i32, vp, vp, vp, vp, vp, dbl, vp, vp, dbl, dbl, dbl, vp, vp, vp]
+    lib.aiqmc_dmc_cut_minima.argtypes = [vp, i32, vp, vp, vp, dbl, dbl, vp, vp]
     lib.aiqmc_dmc_branch.argtypes = [vp, i32, vp, dbl, vp, vp, vp]
     lib.aiqmc_dmc_tmoves.argtypes = [vp, vp, i32, dbl, i32, vp, vp, vp, u64, u64, vp, vp]
     lib.aiqmc_set_ecp.argtypes = [vp, ctypes.POINTER(AiqmcEcp)]
@@ -126,7 +130,8 @@ def load() -> ctypes.CDLL:
     for name in ("aiqmc_create", "aiqmc_destroy", "aiqmc_set_params", "aiqmc_logpsi",
                  "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_mc_step", "aiqmc_profile_enable",
                  "aiqmc_profile_read", "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
-                 "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch"):
+                 "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves",
+                 "aiqmc_phase_param_grad", "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib
@@ -256,6 +261,15 @@ class Context:
               "aiqmc_logpsi")
         return logabs, phase
 
+    def orbitals(self, pos: torch.Tensor):
+        """The complex orbital matrix [B, N, N] (make_orbitals.apply, nn.py:409-506)."""
+        p = self._pos(pos)
+        B = p.shape[0]
+        out = torch.empty(B, self.N, self.N, 2, dtype=self.dtype, device=self.device)
+        check(self._lib.aiqmc_orbitals(self._h, _ptr(p), B, _ptr(out), None, None, _stream(self.device)),
+              "aiqmc_orbitals")
+        return torch.view_as_complex(out)
+
     def logpsi_grad(self, pos: torch.Tensor):
         p = self._pos(pos)
         B = p.shape[0]
@@ -352,10 +366,14 @@ class Context:
         if not (pos.is_cuda and pos.dtype == self.dtype and pos.is_contiguous()):
             raise ValueError("dmc_drift_diffusion needs a contiguous device tensor of the context dtype")
         B = pos.numel() // (3 * self.N)
+        if B * 3 * self.N != pos.numel():
+            raise ValueError(f"positions must hold whole walkers of 3N={3 * self.N} coordinates")
         host = gauss1 is not None
-        g1 = gauss1.to(self.device, self.dtype).contiguous() if host else None
-        g2 = gauss2.to(self.device, self.dtype).contiguous() if host else None
-        uu = u.to(self.device, self.dtype).contiguous() if host else None
+        if host != (gauss2 is not None) or host != (u is not None):
+            raise ValueError("gauss1, gauss2 and u are injected together or not at all")
+        g1 = self._dev(gauss1, B * 3 * self.N) if host else None      # [1, B, 3N]
+        g2 = self._dev(gauss2, B * self.N * 3) if host else None      # [1, B, N, 3] (diagonal blocks)
+        uu = self._dev(u, B * self.N) if host else None               # [1, B, N]
         go = torch.empty(B, 3 * self.N, dtype=self.dtype, device=self.device)
         gn = torch.empty_like(go)
         td = torch.zeros(3, dtype=torch.float64, device=self.device)
@@ -365,17 +383,71 @@ class Context:
                                                   _ptr(gn), _ptr(td), _stream(self.device)), "aiqmc_dmc_drift_diffusion")
         return go, gn, td
 
+    def _real_dev(self, t, n: int, what: str) -> torch.Tensor:
+        t = torch.as_tensor(t)
+        t = t.real if torch.is_complex(t) else t
+        t = t.to(self.device, self.dtype).contiguous()
+        if t.numel() != n:
+            raise ValueError(f"{what}: expected {n} values, got {t.numel()}")
+        return t
+
+    def _grad_arg(self, g: torch.Tensor, B: int, what: str) -> torch.Tensor:
+        if not (isinstance(g, torch.Tensor) and g.is_cuda and g.dtype == self.dtype):
+            raise ValueError(f"{what} must be a device tensor of the context dtype {self.dtype}")
+        if g.numel() != B * 3 * self.N:
+            raise ValueError(f"{what}: expected {B * 3 * self.N} values, got {g.numel()}")
+        return g.contiguous()
+
     def dmc_weights(self, weights: torch.Tensor, eloc_old, eloc_new, grad_eff_old, grad_new_eff, tdamp, tstep: float,
-                    e_trial: float, e_est: float, branchcut: float):
-        """weights *= exp(tau tdamp (S_new + S_old) / 2), in place (S_matrix.py:4-24, dmc.py:88-92)."""
+                    e_trial, e_est, branchcut: float, cut_minima: Optional[torch.Tensor] = None):
+        """weights *= exp(tau tdamp (S_new + S_old) / 2), in place (S_matrix.py:4-24, dmc.py:88-92).
+        e_trial / e_est: scalars, or per-walker [B] values (the driver's first block);
+        cut_minima: optional device float64[2] global e_cut minima (multi-GPU, dmc_cut_minima)."""
         B = weights.numel()
-        eo = eloc_old.real.to(self.device, self.dtype).contiguous()
-        en = eloc_new.real.to(self.device, self.dtype).contiguous()
-        check(self._lib.aiqmc_dmc_weights(self._h, B, _ptr(eo), _ptr(en), _ptr(grad_eff_old.contiguous()),
-                                          _ptr(grad_new_eff.contiguous()), _ptr(tdamp), float(tstep), float(e_trial),
-                                          float(e_est), float(branchcut), _ptr(weights), _stream(self.device)),
-              "aiqmc_dmc_weights")
+        if not (weights.is_cuda and weights.dtype == self.dtype and weights.is_contiguous()):
+            raise ValueError("weights must be a contiguous device tensor of the context dtype (updated in place)")
+        eo = self._real_dev(eloc_old, B, "eloc_old")
+        en = self._real_dev(eloc_new, B, "eloc_new")
+        go = self._grad_arg(grad_eff_old, B, "grad_eff_old")
+        gn = self._grad_arg(grad_new_eff, B, "grad_new_eff")
+        if not (isinstance(tdamp, torch.Tensor) and tdamp.is_cuda and tdamp.dtype == torch.float64 and tdamp.numel() == 3):
+            raise ValueError("tdamp must be the device float64[3] of dmc_drift_diffusion")
+        et_b = ee_b = None
+        if torch.is_tensor(e_trial) and e_trial.numel() > 1:
+            et_b = self._real_dev(e_trial, B, "e_trial")
+            e_trial = 0.0
+        if torch.is_tensor(e_est) and e_est.numel() > 1:
+            ee_b = self._real_dev(e_est, B, "e_est")
+            e_est = 0.0
+        e_trial = complex(e_trial).real if not torch.is_tensor(e_trial) else complex(e_trial.item()).real
+        e_est = complex(e_est).real if not torch.is_tensor(e_est) else complex(e_est.item()).real
+        cm = None
+        if cut_minima is not None:
+            if not (cut_minima.is_cuda and cut_minima.dtype == torch.float64 and cut_minima.numel() == 2):
+                raise ValueError("cut_minima must be a device float64[2]")
+            cm = cut_minima.contiguous()
+        check(self._lib.aiqmc_dmc_weights_ex(self._h, B, _ptr(eo), _ptr(en), _ptr(go), _ptr(gn), _ptr(tdamp),
+                                             float(tstep), _ptr(et_b), _ptr(ee_b), float(e_trial), float(e_est),
+                                             float(branchcut), _ptr(cm), _ptr(weights), _stream(self.device)),
+              "aiqmc_dmc_weights_ex")
         return weights
+
+    def dmc_cut_minima(self, eloc_old, eloc_new, e_est, branchcut: float) -> torch.Tensor:
+        """This batch's e_cut minima [2] (float64, device) for eloc_old / eloc_new (S_matrix.py:21-22);
+        a multi-GPU driver all-reduces them with MIN (the reference's jnp.min spans all devices)."""
+        eo = torch.as_tensor(eloc_old)
+        B = eo.numel()
+        eo = self._real_dev(eo, B, "eloc_old")
+        en = self._real_dev(eloc_new, B, "eloc_new")
+        ee_b = None
+        if torch.is_tensor(e_est) and e_est.numel() > 1:
+            ee_b = self._real_dev(e_est, B, "e_est")
+            e_est = 0.0
+        e_est = complex(e_est).real if not torch.is_tensor(e_est) else complex(e_est.item()).real
+        out = torch.empty(2, dtype=torch.float64, device=self.device)
+        check(self._lib.aiqmc_dmc_cut_minima(self._h, B, _ptr(eo), _ptr(en), _ptr(ee_b), float(e_est),
+                                             float(branchcut), _ptr(out), _stream(self.device)), "aiqmc_dmc_cut_minima")
+        return out
 
     def dmc_branch(self, weights: torch.Tensor, u: float):
         """Stochastic comb (branch.py:10-33): (new uniform weight [1], newinds [B] int32)."""

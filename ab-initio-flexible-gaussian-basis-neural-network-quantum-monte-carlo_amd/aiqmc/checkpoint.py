@@ -3,9 +3,11 @@
 ``save`` writes ``qmcjax_ckpt_{t:06d}.npz`` with the reference's keys (t, data as a
 dict, params, opt_state) via ``np.savez``; device tensors are copied to host numpy
 first, so a file written here holds plain numpy leaves.  ``restore`` returns
-``(t + 1, AINetData, params, opt_state)`` as the reference does (:63-70).  Like the
-reference, ``restore``/``find_last_checkpoint`` read object arrays, i.e. pickles:
-only load files this package (or a trusted run of the reference) wrote.
+``(t + 1, AINetData, params, opt_state)`` as the reference does (:63-70).  Reading never
+unpickles: ``restore``/``find_last_checkpoint`` go through the weights-only interpreter of
+``utils.safe_npz`` (numpy/JAX arrays, numpy scalars, containers and optax state records;
+anything else in the file is refused), so the reference's own pickled-pytree checkpoints
+load without JAX and without executing anything from the file.
 """
 from __future__ import annotations
 
@@ -19,6 +21,7 @@ from typing import Any, Optional
 import numpy as np
 import torch
 
+from .utils.safe_npz import UnsafeCheckpointError, load_npz
 from .wavefunction_Ynlm.nn import AINetData
 
 
@@ -39,12 +42,12 @@ def find_last_checkpoint(ckpt_path: Optional[str] = None) -> Optional[str]:
         files = [f for f in os.listdir(ckpt_path) if "qmcjax_ckpt" in f]
         for file in sorted(files, reverse=True):
             fname = os.path.join(ckpt_path, file)
-            with open(fname, "rb") as f:
-                try:
-                    np.load(f, allow_pickle=True)
-                    return fname
-                except (OSError, EOFError, zipfile.BadZipFile, ValueError):
-                    logging.info("Error loading checkpoint %s. Trying next checkpoint...", fname)
+            try:
+                with open(fname, "rb") as f:
+                    load_npz(f)
+                return fname
+            except (OSError, EOFError, zipfile.BadZipFile, ValueError, KeyError, UnsafeCheckpointError):
+                logging.info("Error loading checkpoint %s. Trying next checkpoint...", fname)
     return None
 
 
@@ -62,14 +65,25 @@ def get_restore_path(restore_path: Optional[str] = None) -> Optional[str]:
     return restore_path if restore_path else None
 
 
+def _object0(tree) -> np.ndarray:
+    """A 0-d object array holding `tree` (what np.savez makes of a pytree argument)."""
+    if isinstance(tree, np.ndarray):
+        return tree
+    a = np.empty((), dtype=object)
+    a[()] = tree
+    return a
+
+
 def save(save_path: str, t: int, data: AINetData, params, opt_state) -> str:
-    """checkpoint.py:44-60."""
+    """checkpoint.py:44-60.  Written to a temporary name and renamed, so a reader never sees
+    a partial file (multi-rank drivers: rank 0 alone writes, see DMC.main_dmc)."""
     fname = os.path.join(save_path, f"qmcjax_ckpt_{t:06d}.npz")
     logging.info("Saving checkpoint %s", fname)
     d = {f.name: _host(getattr(data, f.name)) for f in dataclasses.fields(data)}
-    with open(fname, "wb") as f:
-        np.savez(f, t=t, data=d, params=np.asarray(_host(params), dtype=object)
-                 if not isinstance(params, np.ndarray) else params, opt_state=np.asarray(_host(opt_state), dtype=object))
+    tmp = os.path.join(save_path, f".partial_{t:06d}_{os.getpid()}.npz")   # no 'qmcjax_ckpt' in the name
+    with open(tmp, "wb") as f:
+        np.savez(f, t=t, data=_object0(d), params=_object0(_host(params)), opt_state=_object0(_host(opt_state)))
+    os.replace(tmp, fname)
     return fname
 
 
@@ -78,9 +92,9 @@ def restore(restore_filename: str, batch_size: Optional[int] = None):
     del batch_size
     logging.info("Loading checkpoint %s", restore_filename)
     with open(restore_filename, "rb") as f:
-        ck = np.load(f, allow_pickle=True)
-        t = ck["t"].tolist() + 1
-        data = AINetData(**ck["data"].item())
-        params = ck["params"].tolist()
-        opt_state = ck["opt_state"].tolist()
+        ck = load_npz(f)
+    t = ck["t"].tolist() + 1
+    data = AINetData(**ck["data"].item())
+    params = ck["params"].tolist()
+    opt_state = ck["opt_state"].tolist()
     return t, data, params, opt_state

@@ -44,13 +44,21 @@ def all_gather(x: torch.Tensor) -> torch.Tensor:
 def pmean_stats(e_l: torch.Tensor):
     """(mean E, variance) over all walkers of all ranks with ONE all-reduce.
 
-    Same quantities as loss.py:206-208 (pmean(mean(e)), pmean(mean(|e-E|^2)))
-    for equal per-device batches; accumulated in float64.
+    The reference takes two dependent pmeans (loss.py:206-208): E = pmean(mean(e)), then
+    var = pmean(mean(|e - E|^2)).  One all-reduce of [sum_r M2_r, sum_r n_r m_r, sum_r n_r m_r^2, n]
+    (rank mean m_r, centred sum of squares M2_r = sum |e - m_r|^2) gives the same quantity by
+    the pairwise combination of Chan et al.:
+        var = (sum_r M2_r + sum_r n_r (m_r - E)^2) / n,   sum_r n_r (m_r - E)^2 = sum_r n_r m_r^2 - n E^2,
+    in float64; the within-rank spread never meets the E^2 cancellation.  Equal to the
+    reference's two-pass value (for the equal per-device batches the drivers require).
     """
     e = e_l.to(torch.float64)
-    v = torch.stack([e.sum(), (e * e).sum(), torch.tensor(float(e.numel()), dtype=torch.float64,
-                                                          device=e.device)])
+    n = float(e.numel())
+    m = e.mean()
+    m2 = ((e - m) * (e - m)).sum()
+    v = torch.stack([m2, n * m, n * m * m, torch.tensor(n, dtype=torch.float64, device=e.device)])
     v = psum(v)
-    mean = v[0] / v[2]
-    var = v[1] / v[2] - mean * mean
+    mean = v[1] / v[3]
+    between = torch.clamp(v[2] - v[3] * mean * mean, min=0.0)
+    var = (v[0] + between) / v[3]
     return mean, var

@@ -1,0 +1,131 @@
+"""Systems and pseudopotential tables of the reference's example configurations.
+
+The reference has no config system: each example script builds ``atoms``, ``charges``,
+``spins`` and, for ccECP runs, the ``Rn_local / Local_coes / ...`` tables inline and calls a
+driver ``main(...)`` ("Config / flags").  This module holds those values as data
+so that drivers, benchmarks and tests build the same systems:
+
+* ``C_ecp``  example/single_atom_C/single_atom_C.py:9-23 (C atom, ccECP, Z_eff = 4, spins +-);
+* ``C2_ecp`` example/C2/C2.py:8-27 (C2 at z = +-1 bohr, ccECP on both atoms, BLOCK spins
+  [+1]*4 + [-1]*4, nspins (4, 4));
+* ``C2``     example/C2_muti_GPU_all_electrons/C2test.py (all-electron C2, alternating spins);
+* ``N2``     the benchmark molecule of BASELINE.json (R = 2.0744 bohr);
+* ``H2``, ``Be``, ``C``, ``Ne``: the remaining BASELINE.json systems (all-electron atoms /
+  molecule, alternating spins as every reference example uses);
+* ``O2``     16 electrons (the largest shape built), alternating spins.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Any, Dict, Tuple
+
+import numpy as np
+
+from .spin_indices import jastrow_indices_ee, spin_indices_h
+
+__all__ = ["System", "EcpTables", "make_system", "ccecp_tables", "SYSTEM_NAMES"]
+
+
+@dataclasses.dataclass
+class System:
+    """One molecule as a reference driver sets it up."""
+    name: str
+    atoms: np.ndarray        # [A, 3] bohr
+    charges: np.ndarray      # [A]   (Z, or Z_eff for ccECP systems)
+    spins: np.ndarray        # [N]   +-1
+    nspins: Tuple[int, int]
+
+    @property
+    def nelectrons(self) -> int:
+        return int(self.spins.shape[0])
+
+    @property
+    def natoms(self) -> int:
+        return int(self.atoms.shape[0])
+
+    def tables(self) -> Dict[str, Any]:
+        """The closure tables of make_ai_net (spin_indices.py:5-45)."""
+        par, anti, npar, nanti = jastrow_indices_ee(self.spins, self.nelectrons)
+        (up,), (dn,) = spin_indices_h(self.spins)
+        return dict(parallel_indices=np.asarray(par), antiparallel_indices=np.asarray(anti), n_parallel=int(npar),
+                    n_antiparallel=int(nanti), spin_up_indices=np.asarray(up), spin_down_indices=np.asarray(dn))
+
+    def context(self, dtype=None, device: int = 0):
+        """A HIP context (libaiqmc_hip.so) for this system."""
+        import torch
+        from . import _lib
+        t = self.tables()
+        return _lib.Context(self.nelectrons, self.natoms, self.nspins, self.atoms, self.charges,
+                            t["spin_up_indices"], t["spin_down_indices"], t["parallel_indices"],
+                            t["antiparallel_indices"], dtype=dtype or torch.float32, device=device)
+
+    def make_network(self):
+        """nn.make_ai_net with this system's closure tables (the drivers' call, e.g.
+        main_all_electrons_adam_muti_GPU.py:108-120)."""
+        from .wavefunction_Ynlm import nn
+        t = self.tables()
+        return nn.make_ai_net(nspins=self.nspins, charges=self.charges, parallel_indices=t["parallel_indices"],
+                              antiparallel_indices=t["antiparallel_indices"], spin_up_indices=t["spin_up_indices"],
+                              spin_down_indices=t["spin_down_indices"], n_parallel=t["n_parallel"],
+                              n_antiparallel=t["n_antiparallel"], ndim=3, natoms=self.natoms,
+                              nelectrons=self.nelectrons)
+
+
+def _alternating(n: int) -> np.ndarray:
+    return np.array([1.0 if i % 2 == 0 else -1.0 for i in range(n)])
+
+
+_GEOMETRY = {
+    "H2": ([[0.0, 0.0, -0.7], [0.0, 0.0, 0.7]], [1.0, 1.0]),
+    "Be": ([[0.0, 0.0, 0.0]], [4.0]),
+    "C": ([[0.0, 0.0, 0.0]], [6.0]),
+    "C_ecp": ([[0.0, 0.0, 0.0]], [4.0]),
+    "Ne": ([[0.0, 0.0, 0.0]], [10.0]),
+    "C2": ([[0.0, 0.0, -1.0], [0.0, 0.0, 1.0]], [6.0, 6.0]),
+    "C2_ecp": ([[0.0, 0.0, -1.0], [0.0, 0.0, 1.0]], [4.0, 4.0]),
+    "N2": ([[0.0, 0.0, -1.0372], [0.0, 0.0, 1.0372]], [7.0, 7.0]),
+    "O2": ([[0.0, 0.0, -1.1408], [0.0, 0.0, 1.1408]], [8.0, 8.0]),
+}
+SYSTEM_NAMES = tuple(_GEOMETRY)
+
+
+def make_system(name: str) -> System:
+    atoms, charges = _GEOMETRY[name]
+    atoms = np.asarray(atoms, np.float64)
+    charges = np.asarray(charges, np.float64)
+    n = int(round(charges.sum()))
+    if name == "C2_ecp":   # example/C2/C2.py:10 -- block spins
+        spins = np.array([1.0] * (n // 2) + [-1.0] * (n - n // 2))
+    else:
+        spins = _alternating(n)
+    nup = int((spins > 0).sum())
+    return System(name, atoms, charges, spins, (nup, n - nup))
+
+
+@dataclasses.dataclass
+class EcpTables:
+    """Pseudopotential tables in the drivers' shapes (single_atom_C.py:13-23):
+    rn_local / local_coes / local_exps [A, KL]; rn_non_local / ... [A, list_l + 1, KN]."""
+    rn_local: np.ndarray
+    local_coes: np.ndarray
+    local_exps: np.ndarray
+    rn_non_local: np.ndarray
+    non_local_coes: np.ndarray
+    non_local_exps: np.ndarray
+    list_l: int
+
+
+# carbon ccECP as the examples write it (single_atom_C.py:13-23, C2.py:12-27)
+_C_LOCAL = ([1.0, 3.0, 2.0], [4.00000, 57.74008, -25.81955], [14.43502, 8.39889, 7.38188])
+_C_NONLOCAL = ([[2.0, 2.0], [2.0, 2.0], [2.0, 2.0]], [[52.13345, 0], [0, 0], [0, 0]],
+               [[7.76079, 0], [0, 0], [0, 0]])
+
+
+def ccecp_tables(name: str) -> EcpTables:
+    """The ccECP tables of a pseudopotential example system (one carbon block per atom)."""
+    if name not in ("C_ecp", "C2_ecp"):
+        raise KeyError(f"{name} has no pseudopotential tables")
+    A = make_system(name).natoms
+    rep = lambda rows: np.asarray([rows] * A, np.float64)
+    return EcpTables(rep(_C_LOCAL[0]), rep(_C_LOCAL[1]), rep(_C_LOCAL[2]), rep(_C_NONLOCAL[0]), rep(_C_NONLOCAL[1]),
+                     rep(_C_NONLOCAL[2]), 2)

@@ -3,8 +3,9 @@
 ``make_ai_net`` has the reference signature (nn.py:511-526) and returns a
 ``Network(init, apply, orbitals)``.  ``apply(params, pos, spins, atoms,
 charges) -> (phase, log|psi|)`` evaluates on the GPU through the HIP kernel
-``k_walker`` (libaiqmc_hip.so); unlike the reference it accepts a batch
-``pos[..., 3N]`` directly (the reference callers vmap it).
+``k_walker_rev`` (libaiqmc_hip.so); unlike the reference it accepts a batch
+``pos[..., 3N]`` directly (the reference callers vmap it).  ``orbitals(params, pos, ...)``
+returns the reference's ``[M]`` with the complex orbital matrix M (aiqmc_orbitals).
 
 Parameters are the reference pytree (nested dict/list of arrays, nn.py:203-278,
 370-407); they are flattened in JAX ``tree_flatten`` order for the C-ABI.
@@ -185,7 +186,15 @@ class AINet:
         return phase.reshape(shape), logabs.reshape(shape)
 
     def orbitals(self, params, pos, spins=None, atoms=None, charges=None):
-        raise NotImplementedError("the orbital matrix is internal to the HIP kernel; use apply()")
+        """make_orbitals.apply (nn.py:409-506): ``[M]`` with M the complex [..., N, N] matrix
+        Phi * Yt * exp(J_ee/N) exp(J_ae/N) whose slogdet apply() returns (a one-element list, as
+        the reference's ``total_orbitals_jastrow``; ``determinants`` is ignored, Q10)."""
+        del spins, charges
+        pos_t = pos if isinstance(pos, torch.Tensor) else torch.as_tensor(np.asarray(pos))
+        dtype = pos_t.dtype if pos_t.dtype in (torch.float32, torch.float64) else torch.float32
+        ctx = self.bind(params, atoms, dtype)
+        m = ctx.orbitals(pos_t)
+        return [m.reshape(*pos_t.shape[:-1], self.nelectrons, self.nelectrons)]
 
 
 def make_ai_net(nspins, charges, parallel_indices, antiparallel_indices, spin_up_indices, spin_down_indices,

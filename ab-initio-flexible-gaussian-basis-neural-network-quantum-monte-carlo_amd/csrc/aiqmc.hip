@@ -116,20 +116,19 @@ __global__ __launch_bounds__(256) void k_scale_grad(const T* __restrict__ g, con
   if (i < n) out[i] = g[i] * (T)taueff[0];
 }
 
-// DMC weights (DMC/S_matrix.py:4-24, dmc.py:80-92), one block:
-//   S = e_trial - e_est + e_cut / (1 + (v2 tau / N)^2), v2 = |grad_eff|^2 per walker,
-//   e_cut = min(min_b |e_est - eloc_b|, branchcut) * sign(e_est - eloc_b)  (ONE minimum over the
-//   batch: jnp.min of the stacked array), w *= exp(tau tdamp (S_new + S_old) / 2).
+// DMC energy cut minima (S_matrix.py:21-22): jnp.min over the stacked [|e_est - eloc|, branchcut]
+// array is ONE minimum over every walker (of every device: the reference stacks the pmapped
+// [ndev, B] arrays) and the cut.  out[0] / out[1] = that minimum for eloc_old / eloc_new.
+// eest_b (nullable): per-walker e_est (the first block, main_dmc.py:115-116), else e_est.
 template <typename T>
-__global__ __launch_bounds__(1024) void k_dmc_weights(int B, int N, const T* __restrict__ eold, const T* __restrict__ enew,
-                                                      const T* __restrict__ gold, const T* __restrict__ gnew,
-                                                      const double* __restrict__ tdamp, double tau, double e_trial,
-                                                      double e_est, double branchcut, T* __restrict__ w) {
-  __shared__ double mo[1024], mn[1024];
+__device__ __forceinline__ void dmc_cut_minima(int B, const T* __restrict__ eold, const T* __restrict__ enew,
+                                               const T* __restrict__ eest_b, double e_est, double branchcut,
+                                               double* mo, double* mn, double& cut_o, double& cut_n) {
   double a = branchcut, b = branchcut;
   for (int i = threadIdx.x; i < B; i += 1024) {
-    a = fmin(a, fabs(e_est - (double)eold[i]));
-    b = fmin(b, fabs(e_est - (double)enew[i]));
+    const double ee = eest_b ? (double)eest_b[i] : e_est;
+    a = fmin(a, fabs(ee - (double)eold[i]));
+    b = fmin(b, fabs(ee - (double)enew[i]));
   }
   mo[threadIdx.x] = a;
   mn[threadIdx.x] = b;
@@ -141,7 +140,44 @@ __global__ __launch_bounds__(1024) void k_dmc_weights(int B, int N, const T* __r
     }
     __syncthreads();
   }
-  const double cut_o = mo[0], cut_n = mn[0];
+  cut_o = mo[0];
+  cut_n = mn[0];
+}
+
+template <typename T>
+__global__ __launch_bounds__(1024) void k_dmc_cut_minima(int B, const T* __restrict__ eold, const T* __restrict__ enew,
+                                                         const T* __restrict__ eest_b, double e_est, double branchcut,
+                                                         double* __restrict__ out) {
+  __shared__ double mo[1024], mn[1024];
+  double co, cn;
+  dmc_cut_minima<T>(B, eold, enew, eest_b, e_est, branchcut, mo, mn, co, cn);
+  if (threadIdx.x == 0) {
+    out[0] = co;
+    out[1] = cn;
+  }
+}
+
+// DMC weights (DMC/S_matrix.py:4-24, dmc.py:80-92), one block:
+//   S = e_trial - e_est + e_cut / (1 + (v2 tau / N)^2), v2 = |grad_eff|^2 per walker,
+//   e_cut = cut * sign(e_est - eloc_b), cut = the global minimum above (computed here from this
+//   batch, or the caller's all-reduced cuts[2] for a multi-device run),
+//   w *= exp(tau tdamp (S_new + S_old) / 2).
+// etr_b / eest_b (nullable): per-walker e_trial / e_est of the first DMC block.
+template <typename T>
+__global__ __launch_bounds__(1024) void k_dmc_weights(int B, int N, const T* __restrict__ eold, const T* __restrict__ enew,
+                                                      const T* __restrict__ gold, const T* __restrict__ gnew,
+                                                      const double* __restrict__ tdamp, double tau,
+                                                      const T* __restrict__ etr_b, const T* __restrict__ eest_b,
+                                                      double e_trial, double e_est, double branchcut,
+                                                      const double* __restrict__ cuts, T* __restrict__ w) {
+  __shared__ double mo[1024], mn[1024];
+  double cut_o, cut_n;
+  if (cuts) {
+    cut_o = cuts[0];
+    cut_n = cuts[1];
+  } else {
+    dmc_cut_minima<T>(B, eold, enew, eest_b, e_est, branchcut, mo, mn, cut_o, cut_n);
+  }
   const double td = tdamp[2];   // [sum proposed, sum new, tdamp] of aiqmc_dmc_drift_diffusion
   for (int i = threadIdx.x; i < B; i += 1024) {
     double vo = 0.0, vn = 0.0;
@@ -150,9 +186,11 @@ __global__ __launch_bounds__(1024) void k_dmc_weights(int B, int N, const T* __r
       vo += x * x;
       vn += y * y;
     }
-    const double co = e_est - (double)eold[i], cn = e_est - (double)enew[i];
-    const double so = e_trial - e_est + cut_o * (double)((co > 0) - (co < 0)) / (1.0 + (vo * tau / N) * (vo * tau / N));
-    const double sn = e_trial - e_est + cut_n * (double)((cn > 0) - (cn < 0)) / (1.0 + (vn * tau / N) * (vn * tau / N));
+    const double ee = eest_b ? (double)eest_b[i] : e_est;
+    const double et = etr_b ? (double)etr_b[i] : e_trial;
+    const double co = ee - (double)eold[i], cn = ee - (double)enew[i];
+    const double so = et - ee + cut_o * (double)((co > 0) - (co < 0)) / (1.0 + (vo * tau / N) * (vo * tau / N));
+    const double sn = et - ee + cut_n * (double)((cn > 0) - (cn < 0)) / (1.0 + (vn * tau / N) * (vn * tau / N));
     w[i] = (T)(exp(tau * td * (0.5 * sn + 0.5 * so)) * (double)w[i]);
   }
 }
@@ -495,6 +533,30 @@ int aiqmc_logpsi(aiqmc_ctx* c, const void* pos, int32_t B, void* logabs, void* p
   rc = ensure_ws(c, B);
   if (rc) return rc;
   ka.wcache = c->d_wc;   // the kernel keeps its electron-local Jacobians there
+  ops.walker(c->dtype, MODE_GRAD, ka, B, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_orbitals(aiqmc_ctx* c, const void* pos, int32_t B, void* orbitals, void* logabs, void* phase,
+                   void* stream) {
+  int rc = check_call(c, pos, B);
+  if (rc) return rc;
+  if (B == 0) return AIQMC_OK;
+  if (!orbitals) return fail(AIQMC_EINVAL, "null orbitals");
+  HIPCHK(hipSetDevice(c->device));
+  ShapeOps ops;
+  shape_ops(c->N, c->A, &ops);
+  rc = ensure_ws(c, B);
+  if (rc) return rc;
+  KArgs ka = base_args(c);
+  ka.nconf = B;
+  ka.pos = pos;
+  ka.logabs = logabs;
+  ka.phase = phase;
+  ka.value_only = 1;
+  ka.orb = orbitals;
+  ka.wcache = c->d_wc;
   ops.walker(c->dtype, MODE_GRAD, ka, B, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
@@ -1024,9 +1086,10 @@ int aiqmc_dmc_drift_diffusion(aiqmc_ctx* c, void* pos, int32_t B, double tstep, 
   return AIQMC_OK;
 }
 
-int aiqmc_dmc_weights(aiqmc_ctx* c, int32_t B, const void* eloc_old, const void* eloc_new, const void* grad_eff_old,
-                      const void* grad_new_eff, const double* tdamp, double tstep, double e_trial, double e_est,
-                      double branchcut, void* weights_inout, void* stream) {
+int aiqmc_dmc_weights_ex(aiqmc_ctx* c, int32_t B, const void* eloc_old, const void* eloc_new,
+                         const void* grad_eff_old, const void* grad_new_eff, const double* tdamp, double tstep,
+                         const void* e_trial_b, const void* e_est_b, double e_trial, double e_est, double branchcut,
+                         const double* cut_minima, void* weights_inout, void* stream) {
   if (!c) return fail(AIQMC_EINVAL, "null context");
   if (B < 0) return fail(AIQMC_EINVAL, "negative batch");
   if (B == 0) return AIQMC_OK;
@@ -1037,12 +1100,38 @@ int aiqmc_dmc_weights(aiqmc_ctx* c, int32_t B, const void* eloc_old, const void*
   if (c->dtype == AIQMC_F32)
     k_dmc_weights<float><<<dim3(1), dim3(1024), 0, s>>>(B, c->N, (const float*)eloc_old, (const float*)eloc_new,
                                                          (const float*)grad_eff_old, (const float*)grad_new_eff, tdamp,
-                                                         tstep, e_trial, e_est, branchcut, (float*)weights_inout);
+                                                         tstep, (const float*)e_trial_b, (const float*)e_est_b, e_trial,
+                                                         e_est, branchcut, cut_minima, (float*)weights_inout);
   else
     k_dmc_weights<double><<<dim3(1), dim3(1024), 0, s>>>(B, c->N, (const double*)eloc_old, (const double*)eloc_new,
                                                           (const double*)grad_eff_old, (const double*)grad_new_eff,
-                                                          tdamp, tstep, e_trial, e_est, branchcut,
+                                                          tdamp, tstep, (const double*)e_trial_b, (const double*)e_est_b,
+                                                          e_trial, e_est, branchcut, cut_minima,
                                                           (double*)weights_inout);
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_dmc_weights(aiqmc_ctx* c, int32_t B, const void* eloc_old, const void* eloc_new, const void* grad_eff_old,
+                      const void* grad_new_eff, const double* tdamp, double tstep, double e_trial, double e_est,
+                      double branchcut, void* weights_inout, void* stream) {
+  return aiqmc_dmc_weights_ex(c, B, eloc_old, eloc_new, grad_eff_old, grad_new_eff, tdamp, tstep, nullptr, nullptr,
+                              e_trial, e_est, branchcut, nullptr, weights_inout, stream);
+}
+
+int aiqmc_dmc_cut_minima(aiqmc_ctx* c, int32_t B, const void* eloc_old, const void* eloc_new, const void* e_est_b,
+                         double e_est, double branchcut, double* out, void* stream) {
+  if (!c) return fail(AIQMC_EINVAL, "null context");
+  if (B < 0) return fail(AIQMC_EINVAL, "negative batch");
+  if (!out || (B > 0 && (!eloc_old || !eloc_new))) return fail(AIQMC_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (c->dtype == AIQMC_F32)
+    k_dmc_cut_minima<float><<<dim3(1), dim3(1024), 0, s>>>(B, (const float*)eloc_old, (const float*)eloc_new,
+                                                            (const float*)e_est_b, e_est, branchcut, out);
+  else
+    k_dmc_cut_minima<double><<<dim3(1), dim3(1024), 0, s>>>(B, (const double*)eloc_old, (const double*)eloc_new,
+                                                             (const double*)e_est_b, e_est, branchcut, out);
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
 }

@@ -11,7 +11,7 @@
 #include "walker_kernel.h"
 
 // (N, A) instantiations; the Makefile compiles shape.hip once per entry.
-#define AIQMC_SHAPE_LIST(X) X(2, 2) X(4, 1) X(6, 1) X(8, 1) X(10, 1) X(12, 2) X(14, 2)
+#define AIQMC_SHAPE_LIST(X) X(2, 2) X(4, 1) X(6, 1) X(8, 1) X(8, 2) X(10, 1) X(12, 2) X(14, 2) X(16, 2)
 
 int aiqmc_fail(int code, const std::string& msg);
 using aq::KArgs;

@@ -90,7 +90,12 @@ __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, in
   int myp = 0;
   unsigned used = 0;   // rows chosen so far (uniform bitmask)
   int inv = 0;         // inversions of the pivot sequence, for sgn(p)
-  T ld = T(0), pr_ = T(1), pi_ = T(0);
+  // log|det A| = 0.5 log prod_k |pivot_k|^2, the product carried as mantissa (in [2^-N, 1),
+  // no under/overflow for N <= 16) and binary exponent: one log per matrix instead of N
+  // log roundings (fp32: half the log|psi| error of summing per-pivot logs)
+  T pm = T(1);
+  int pe = 0;
+  T pr_ = T(1), pi_ = T(0);
 #pragma unroll
   for (int k = 0; k < N; ++k) {
     // ---- pivot: first maximal |re|+|im| among the unused rows of column k
@@ -119,7 +124,11 @@ __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, in
       rec[N + k] = f_sqrt(f_rcp(den));
     }
     const T rden = f_rcp(den);
-    ld += T(0.5) * f_log(den);                 // log|pivot|
+    {
+      int e;
+      pm *= f_frexp(den, e);
+      pe += e;
+    }
     {
       const T rm = f_sqrt(rden);
       const T ur = pr * rm, ui = pim * rm;
@@ -166,6 +175,7 @@ __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, in
       Bout[(myk[t] * N + myp) * 2 + 1] = ai[t];
     }
   }
+  const T ld = T(0.5) * (f_log(pm) + T(pe) * T(0.69314718055994531));
   if (rec && lane == 0) {
     rec[2 * N] = T(inv & 1);
     rec[2 * N + 1] = ld;

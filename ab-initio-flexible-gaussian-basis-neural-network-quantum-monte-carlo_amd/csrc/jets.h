@@ -58,6 +58,9 @@ template <> __device__ __forceinline__ float f_tanh(float x) {
   return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + e);
 }
 template <> __device__ __forceinline__ double f_tanh(double x) { return tanh(x); }
+// mantissa in [0.5, 1) and binary exponent (v_frexp_mant / v_frexp_exp)
+__device__ __forceinline__ float f_frexp(float x, int& e) { return frexpf(x, &e); }
+__device__ __forceinline__ double f_frexp(double x, int& e) { return frexp(x, &e); }
 template <typename T> __device__ __forceinline__ T f_abs(T x);
 template <> __device__ __forceinline__ float f_abs(float x) { return fabsf(x); }
 template <> __device__ __forceinline__ double f_abs(double x) { return fabs(x); }

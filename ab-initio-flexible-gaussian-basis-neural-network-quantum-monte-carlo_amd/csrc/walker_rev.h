@@ -620,10 +620,23 @@ k_walker_rev(KArgs ka) {
   }
   if constexpr (!PREP) {
     if (ka.value_only) {   // ECP quadrature configurations: log|psi| and phase only
-      const T lpsi = logdet + wave_sum(jv + jve);
+      const T jsum = wave_sum(jv + jve);
+      const T lpsi = logdet + jsum;
       if (lane == 0) {
         if (ka.logabs) ((T*)ka.logabs)[conf] = lpsi;
         if (ka.phase) ((T*)ka.phase)[conf] = f_atan2(phi, phr);
+      }
+      if (ka.orb) {
+        // make_orbitals.apply's output (nn.py:485-506): Phi (rows = up electrons then down
+        // electrons) * Yt (row r: electron r's envelope and y row, Q1) * exp(J_ee/N) exp(J_ae/N)
+        const T je = wave_sum(jve), ja = wave_sum(jv);
+        const T sc = f_exp(je / T(N)) * f_exp(ja / T(N));
+        T* O = (T*)ka.orb + (size_t)conf * N * N * 2;
+        for (int idx = lane; idx < N * N; idx += 64) {
+          const T y = Yv[idx] * sc;
+          O[2 * idx] = Ph[2 * idx] * y;
+          O[2 * idx + 1] = Ph[2 * idx + 1] * y;
+        }
       }
       return;
     }

@@ -46,7 +46,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--walkers", type=int, default=4096, help="walkers per GPU")
+    ap.add_argument("--walkers", type=int, default=4096, help="walkers per GPU (weak scaling, the default)")
+    ap.add_argument("--global-walkers", type=int, default=0,
+                    help="strong scaling: this many walkers in total, split over the ranks (SURVEY 8(d): 4096)")
     ap.add_argument("--nsteps", type=int, default=10, help="Metropolis sweeps per iteration")
     ap.add_argument("--tstep", type=float, default=0.05)
     ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
@@ -60,34 +62,14 @@ def parse():
     return ap.parse_args()
 
 
-def system_def(name):
-    if name == "N2":
-        return np.array([[0.0, 0.0, -1.0372], [0.0, 0.0, 1.0372]]), np.array([7.0, 7.0])
-    if name == "Be":
-        return np.zeros((1, 3)), np.array([4.0])
-    if name == "Ne":
-        return np.zeros((1, 3)), np.array([10.0])
-    if name == "H2":
-        return np.array([[0.0, 0.0, -0.7], [0.0, 0.0, 0.7]]), np.array([1.0, 1.0])
-    raise KeyError(name)
-
-
 def build(name, dtype, device):
-    from aiqmc import spin_indices
-    from aiqmc.wavefunction_Ynlm import nn
-    atoms, charges = system_def(name)
-    n = int(charges.sum())
-    spins = np.array([1.0 if i % 2 == 0 else -1.0 for i in range(n)])
-    par, anti, npar, nanti = spin_indices.jastrow_indices_ee(spins, n)
-    up, dn = spin_indices.spin_indices_h(spins)
-    nup = int((spins > 0).sum())
-    network = nn.make_ai_net(nspins=(nup, n - nup), charges=charges, parallel_indices=par,
-                             antiparallel_indices=anti, spin_up_indices=up, spin_down_indices=dn,
-                             n_parallel=npar, n_antiparallel=nanti, ndim=3, natoms=len(atoms), nelectrons=n)
+    from aiqmc import systems
+    s = systems.make_system(name)
+    network = s.make_network()
     params = network.init(1)
     net = network.apply._aiqmc_network
-    ctx = net.bind(params, atoms, dtype, device)
-    return atoms, charges, spins, network, params, ctx
+    ctx = net.bind(params, s.atoms, dtype, device)
+    return s.atoms, s.charges, s.spins, network, params, ctx
 
 
 def cpu_baseline(name, params, atoms, charges, nsteps_unused, tstep, sample_walkers):
@@ -133,18 +115,14 @@ def cpu_baseline(name, params, atoms, charges, nsteps_unused, tstep, sample_walk
 def ecp_side_bench(dtype, device, walkers, steps, cpu_baseline_on):
     """BASELINE.json config 'C atom with ccECP pseudopotential, 4096 walkers, 1xMI355X': complex
     pp local energy (pphamiltonian.py:177-188) of the whole batch, Philox grid rotations."""
-    sys.path.insert(0, ROOT)
-    from aiqmc import _lib
+    from aiqmc import _lib, systems
     from aiqmc.initial_electrons_positions.init import init_electrons
-    from oracle import pphamiltonian as opp, system as osys
-    s = osys.make_system("C_ecp")
-    t = s.tables()
-    ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
-                       t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"], dtype=dtype,
-                       device=device.index)
-    params = osys.init_params(np.random.default_rng(1), s)
-    ctx.set_params(osys.flatten_params(params))
-    e = opp.c_atom_ccecp()
+    from aiqmc.wavefunction_Ynlm.nn import flatten_params
+    s = systems.make_system("C_ecp")
+    ctx = s.context(dtype=dtype, device=device.index)
+    params = s.make_network().init(1)
+    ctx.set_params(flatten_params(params))
+    e = systems.ccecp_tables("C_ecp")
     ctx.set_ecp(e.rn_local, e.local_coes, e.local_exps, e.rn_non_local, e.non_local_coes, e.non_local_exps, e.list_l)
     pos, _ = init_electrons(77, None, s.atoms, s.charges, s.spins, walkers, 1.0)
     pos = pos.to(device, dtype).contiguous()
@@ -165,13 +143,15 @@ def ecp_side_bench(dtype, device, walkers, steps, cpu_baseline_on):
            "quadrature_configs_per_launch": nq, "quadrature_launch_avg_ms": q_ms / max(q_n, 1),
            "mean_energy_re": float(out.real.mean()), "finite": bool(torch.isfinite(out.real).all())}
     if cpu_baseline_on:
-        net = __import__("oracle.network", fromlist=["Network"]).Network(s)
-        pt = __import__("oracle.network", fromlist=["to_torch"]).to_torch(params)
+        sys.path.insert(0, ROOT)
+        from oracle import network as onet, pphamiltonian as opp, system as osys
+        net = onet.Network(osys.make_system("C_ecp"))
+        pt = onet.to_torch(params)
         rng = np.random.default_rng(9)
         x = torch.tensor(osys.init_electrons(rng, s.atoms, s.charges, 2, 1.0))
         rots = opp.haar_rotations(rng, 2)
         t0 = time.perf_counter()
-        opp.batch_local_energy_pp(net, pt, e, x, rots)
+        opp.batch_local_energy_pp(net, pt, opp.c_atom_ccecp(), x, rots)
         tc = time.perf_counter() - t0
         res["cpu_baseline"] = {"value": 2 / tc, "unit": "local-energy evals/s", "cores": torch.get_num_threads(),
                                "kind": "port", "sample": f"float64 oracle, 2 walkers ({tc:.1f}s)"}
@@ -189,15 +169,11 @@ def pp_adam_side_bench(dtype, device, walkers, steps):
     from aiqmc.VMC import VMCmcstep
     from aiqmc.wavefunction_Ynlm import nn
     from aiqmc.initial_electrons_positions.init import init_electrons
-    from oracle import pphamiltonian as opp, system as osys
-    s = osys.make_system("C_ecp")
-    par, anti, npar, nanti = spin_indices.jastrow_indices_ee(s.spins, 4)
-    up, dn = spin_indices.spin_indices_h(s.spins)
-    network = nn.make_ai_net(nspins=(2, 2), charges=s.charges, parallel_indices=par, antiparallel_indices=anti,
-                             spin_up_indices=up, spin_down_indices=dn, n_parallel=npar, n_antiparallel=nanti,
-                             ndim=3, natoms=1, nelectrons=4)
+    from aiqmc import systems
+    s = systems.make_system("C_ecp")
+    network = s.make_network()
     params = network.init(4)
-    e = opp.c_atom_ccecp()
+    e = systems.ccecp_tables("C_ecp")
     log_network = nn.make_log_network(network.apply)
     le = pphamiltonian.local_energy(f=network.apply, lognetwork=log_network, charges=s.charges, nspins=s.spins,
                                     rn_local=e.rn_local, local_coes=e.local_coes, local_exps=e.local_exps,
@@ -240,15 +216,11 @@ def dmc_side_bench(dtype, device, walkers, steps):
     from aiqmc.VMC.VMCmcstep import PhiloxKey
     from aiqmc.wavefunction_Ynlm import nn
     from aiqmc.initial_electrons_positions.init import init_electrons
-    from oracle import pphamiltonian as opp, system as osys
-    s = osys.make_system("C_ecp")
-    par, anti, npar, nanti = spin_indices.jastrow_indices_ee(s.spins, 4)
-    up, dn = spin_indices.spin_indices_h(s.spins)
-    network = nn.make_ai_net(nspins=(2, 2), charges=s.charges, parallel_indices=par, antiparallel_indices=anti,
-                             spin_up_indices=up, spin_down_indices=dn, n_parallel=npar, n_antiparallel=nanti,
-                             ndim=3, natoms=1, nelectrons=4)
+    from aiqmc import systems
+    s = systems.make_system("C_ecp")
+    network = s.make_network()
     params = network.init(3)
-    e = opp.c_atom_ccecp()
+    e = systems.ccecp_tables("C_ecp")
     tstep = 0.01
     run = dmc.dmc_propagate(network.apply, nn.make_log_network(network.apply), network.apply, e.list_l, 4, 1, 3,
                             walkers, tstep, 1, s.charges, s.spins, e.rn_local, e.local_coes, e.local_exps,
@@ -300,14 +272,10 @@ def adam_side_bench(dtype, device, walkers, steps):
     from aiqmc.VMC import VMCmcstep
     from aiqmc.wavefunction_Ynlm import nn
     from aiqmc.initial_electrons_positions.init import init_electrons
-    atoms, charges = system_def("Be")
-    n = 4
-    spins = np.array([1.0, -1.0, 1.0, -1.0])
-    par, anti, npar, nanti = spin_indices.jastrow_indices_ee(spins, n)
-    up, dn = spin_indices.spin_indices_h(spins)
-    network = nn.make_ai_net(nspins=(2, 2), charges=charges, parallel_indices=par, antiparallel_indices=anti,
-                             spin_up_indices=up, spin_down_indices=dn, n_parallel=npar, n_antiparallel=nanti,
-                             ndim=3, natoms=1, nelectrons=n)
+    from aiqmc import systems
+    sb = systems.make_system("Be")
+    atoms, charges, spins, n = sb.atoms, sb.charges, sb.spins, sb.nelectrons
+    network = sb.make_network()
     params = network.init(2)
     pos, sp = init_electrons(5, None, atoms, charges, spins, walkers, 1.0)
     data = nn.AINetData(positions=pos.to(device, dtype).contiguous(), spins=sp, atoms=atoms, charges=charges)
@@ -354,8 +322,15 @@ def main():
 
     atoms, charges, spins, network, params, ctx = build(args.system, dtype, local_dev)
     N = int(charges.sum())
-    B = args.walkers
-    pos0, _ = init_electrons(1000 + rank, None, atoms, charges, spins, B, 1.0)
+    strong = args.global_walkers > 0
+    if strong and args.global_walkers % world:
+        raise SystemExit("--global-walkers must be divisible by the number of ranks")
+    B = args.global_walkers // world if strong else args.walkers
+    if strong:   # contiguous blocks of one global batch (main_all_electrons_adam_muti_GPU.py:86-97)
+        pos0, _ = init_electrons(1000, None, atoms, charges, spins, args.global_walkers, 1.0)
+        pos0 = pos0[rank * B:(rank + 1) * B]
+    else:
+        pos0, _ = init_electrons(1000 + rank, None, atoms, charges, spins, B, 1.0)
     pos = pos0.to(dev, dtype).contiguous()
     el = torch.empty(B, dtype=dtype, device=dev)
     seed = 12345 + rank
@@ -413,13 +388,19 @@ def main():
         achieved = (flop_prop / (prop_avg_ms * 1e-3) / 1e12) if flop_prop else None
         lap_avg_ms = lap_ms / max(lap_n, 1)
         achieved_el = (B * F_EL_N2 / (lap_avg_ms * 1e-3) / 1e12) if args.system == "N2" else None
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            try:
-                traffic = json.load(open(pmc)).get("k_walker_grad_proposal_bytes_per_launch")
-            except Exception:
-                traffic = None
+        # PMC-derived per-launch figures of the proposal kernel, collected by profiles/pmc_passes.sh
+        # in separate rocprofv3 --pmc passes over this bench (corrected per MI355X_MICROARCH.md) and
+        # committed under profiles/; null when no pass has been committed for this build
+        pmc = {}
+        for fn in ("pmc_r02.json", "pmc_traffic.json"):
+            f = os.path.join(ROOT, "profiles", fn)
+            if os.path.exists(f):
+                try:
+                    pmc = json.load(open(f))
+                    break
+                except Exception:
+                    pmc = {}
+        traffic = pmc.get("proposal_hbm_bytes_per_launch", pmc.get("k_walker_grad_proposal_bytes_per_launch"))
         out = {
             "metric": METRIC,
             "value": value,
@@ -429,7 +410,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * t_job / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32" if dtype == torch.float32 else "f64",
             "data": "synthetic (init_electrons walkers, random-init network of the reference architecture)",
@@ -440,9 +421,16 @@ def main():
             "local_energy_evals_per_s": total_walkers * args.steps / (el_ms_max * 1e-3),
             "mc_walker_steps_per_s": total_walkers * args.nsteps * args.steps / (mc_ms_max * 1e-3),
             "roofline": {
-                "kernel": "k_walker_rev<float,14,2> proposal launch (B*N value+gradient configs)",
-                "bound": "mfma", "compute_unit": "VALU (fp32 dense peak = VALU peak)", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                "kernel": "k_walker_rev<float,14,2,PROP> proposal launch (B*N value+gradient configs)",
+                # no MFMA on this path (SQ_INSTS_MFMA = 0 per the committed PMC pass): the bound is the
+                # fp32 vector ALU (157.3 TF = 64 FLOP/clk/SIMD, MI355X_MICROARCH.md), not HBM
+                "bound": "valu", "compute_unit": "VALU fp32 (no MFMA on this path)",
+                "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                 "frac": (achieved / peak) if achieved else None, "traffic": traffic,
+                "hbm_gbs": (traffic / (prop_avg_ms * 1e-3) / 1e9) if traffic else None,
+                "hbm_frac": (traffic / (prop_avg_ms * 1e-3) / 1e9 / PEAK_HBM_GBS) if traffic else None,
+                "mfma_util": pmc.get("proposal_mfma_util"),
+                "valu_insts_per_wave": pmc.get("proposal_valu_insts_per_wave"),
                 "avg_launch_ms": prop_avg_ms, "launches": prop_n,
                 "flop_per_launch": flop_prop,
                 "flop_model": "B*N*3*F_fwd, F_fwd=4.9e4 (SURVEY 8d)"},

@@ -122,6 +122,13 @@ int aiqmc_logpsi_param_grad(aiqmc_ctx* ctx, const void* pos, int32_t B, const vo
 int aiqmc_phase_param_grad(aiqmc_ctx* ctx, const void* pos, int32_t B, const void* weights, void* out,
                            void* phase, void* stream);
 
+/* The orbital matrix of B walkers (Network.orbitals = make_orbitals.apply, nn.py:409-506,553):
+ * orbitals[B][N][N][2] (re, im; ctx dtype) = Phi * Yt * exp(J_ee/N) exp(J_ae/N), rows = up
+ * electrons then down electrons (spin_up_indices / spin_down_indices order), row r's envelope
+ * and y row those of electron r (quirk Q1).  logabs / phase (optional, [B]) as aiqmc_logpsi. */
+int aiqmc_orbitals(aiqmc_ctx* ctx, const void* pos, int32_t B, void* orbitals, void* logabs, void* phase,
+                   void* stream);
+
 /* DMC drift-diffusion step (DMC/drift_diffusion.py:25-107): one Metropolis sweep
  * exactly as aiqmc_mc_step with nsteps = 1 (same draws, in place), plus
  *   grad_eff_old[B*3N]  limdrift(grad log|psi|) at the walkers before the move (:60-61),
@@ -139,6 +146,24 @@ int aiqmc_dmc_drift_diffusion(aiqmc_ctx* ctx, void* pos_inout, int32_t B, double
 int aiqmc_dmc_weights(aiqmc_ctx* ctx, int32_t B, const void* eloc_old, const void* eloc_new, const void* grad_eff_old,
                       const void* grad_new_eff, const double* tdamp, double tstep, double e_trial, double e_est,
                       double branchcut, void* weights_inout, void* stream);
+
+/* aiqmc_dmc_weights with the general arguments of comput_S as main_dmc.py drives it:
+ *   e_trial_b / e_est_b (optional, device [B], ctx dtype): per-walker e_trial / e_est -- the
+ *     driver's first block passes the per-walker pp energies of total_e (main_dmc.py:115-116);
+ *     NULL: the scalars e_trial / e_est;
+ *   cut_minima (optional, device double[2]): the e_cut minima for eloc_old / eloc_new
+ *     (S_matrix.py:21-22: ONE jnp.min over the stacked arrays of ALL devices and the branch
+ *     cut) -- a multi-GPU run all-reduces aiqmc_dmc_cut_minima with MIN and passes the result;
+ *     NULL: computed from this batch. */
+int aiqmc_dmc_weights_ex(aiqmc_ctx* ctx, int32_t B, const void* eloc_old, const void* eloc_new,
+                         const void* grad_eff_old, const void* grad_new_eff, const double* tdamp, double tstep,
+                         const void* e_trial_b, const void* e_est_b, double e_trial, double e_est, double branchcut,
+                         const double* cut_minima, void* weights_inout, void* stream);
+
+/* This batch's e_cut minima (S_matrix.py:21-22) for eloc_old / eloc_new: out (device
+ * double[2]) = min(branchcut, min_b |e_est_b - eloc_b|) (e_est_b optional as above). */
+int aiqmc_dmc_cut_minima(aiqmc_ctx* ctx, int32_t B, const void* eloc_old, const void* eloc_new, const void* e_est_b,
+                         double e_est, double branchcut, double* out, void* stream);
 
 /* Stochastic comb (DMC/branch.py:10-33) with the uniform draw u in [0,1):
  * newinds[B] (int32, device) = searchsorted(cumsum(w), (u wtot + j wtot/B) mod wtot),

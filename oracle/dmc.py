@@ -189,3 +189,76 @@ def tmoves(net, params, ecp, pos, rot, u_sel: float, u_acc, tstep: float):
         if acc[i] > u_acc[i]:
             new[i] = cfg_f[i, mv]
     return torch.tensor(new.reshape(-1)), acc
+
+
+# --------------------------------------------------------------------------------------------
+# One dmc_propagate_run step (DMC/dmc.py:72-93) and the driver's block loop (main_dmc.py:113-244),
+# draws injected.  e_trial / e_est are per-walker arrays in the first block (total_e returns the
+# per-walker energies, total_energy.py:32; main_dmc.py:115-116) and scalars afterwards.
+# --------------------------------------------------------------------------------------------
+
+def dmc_step(net, params, ecp, x, weights, e_trial, e_est, branchcut, draws, tstep: float):
+    """Returns (eloc_new [B] complex, weights [B], x_new [B,3N], parts dict)."""
+    from . import pphamiltonian as pp
+    B, n3 = x.shape
+    N = n3 // 3
+    pos_t = torch.stack([tmoves(net, params, ecp, x[b], draws["rot_tm"][b], float(draws["u_sel"][b]),
+                                draws["u_acc"][b], tstep)[0] for b in range(B)])            # dmc.py:79
+    x_new, tdamp, go, gn = drift_diffusion(net, params, pos_t, torch.as_tensor(draws["gauss1"]),
+                                           torch.as_tensor(draws["gauss2"]), torch.as_tensor(draws["u"]), tstep)
+    eloc_old = pp.batch_local_energy_pp(net, params, ecp, x, draws["rot_old"])[0].detach().numpy()
+    eloc_new = pp.batch_local_energy_pp(net, params, ecp, x_new, draws["rot_new"])[0].detach().numpy()
+    s_old = comput_S(e_trial, e_est, branchcut, go.numpy() ** 2, tstep, eloc_old, N)
+    s_new = comput_S(e_trial, e_est, branchcut, gn.numpy() ** 2, tstep, eloc_new, N)
+    w = update_weights(np.asarray(weights), tstep, float(tdamp), s_new, s_old)
+    return eloc_new, w, x_new, dict(pos_t=pos_t.numpy(), tdamp=float(tdamp), eloc_old=eloc_old)
+
+
+def reindex(x, newinds, extra):
+    """main_dmc.py:215-233 for one device: sorted unique comb indices, killed walkers replaced by the
+    last unique walker plus U[0,1) noise."""
+    unique = np.unique(newinds)
+    temp = x[unique]
+    n = x.shape[0] - unique.size
+    if n > 0:
+        temp = np.concatenate([temp, temp[-1] + extra[:n]], axis=0)
+    return temp
+
+
+def dmc_blocks(net, params, ecp, x0, e_l0, nblocks: int, iterations: int, tstep: float, feedback: float,
+               step_draws, block_draws):
+    """main_dmc.py:113-244 on one device.  e_l0: the pp energies of x0 (total_e); step_draws(k) ->
+    the draws of step k; block_draws(block) -> (u_comb, extra [B,3N])."""
+    B = x0.shape[0]
+    x = np.asarray(x0, np.float64)
+    e_trial = e_est = np.asarray(e_l0)
+    esigma = float(np.std(np.asarray(e_l0)))                       # :118 (complex std)
+    weights = np.ones(B)
+    branchcut = 10.0 * esigma                                       # :137 branchcut_start * esigma
+    energy_data = np.zeros((nblocks, iterations, B))
+    weights_data = np.zeros((nblocks, iterations, B))
+    trace = {"energy": [], "weights": [], "positions": [], "newinds": [], "comb_weight": [], "e_est": [],
+             "e_trial": []}
+    k = 0
+    for block in range(nblocks):
+        for t in range(iterations):
+            eloc, weights, xt, _ = dmc_step(net, params, ecp, torch.tensor(x), weights, e_trial, e_est, branchcut,
+                                            step_draws(k), tstep)
+            k += 1
+            x = xt.numpy()
+            energy_data[block, t] = eloc.real
+            weights_data[block, t] = weights
+            trace["energy"].append(eloc)
+            trace["weights"].append(weights)
+            trace["positions"].append(x)
+        e_est = np.average(energy_data, weights=weights_data)          # :190
+        u, extra = block_draws(block)
+        wn, newinds = branch(weights, u)                               # :202
+        weights = np.full(B, wn)
+        x = reindex(x, newinds, extra)
+        e_trial = e_est - feedback * np.log(np.mean([wn])).real        # :237
+        trace["newinds"].append(newinds)
+        trace["comb_weight"].append(wn)
+        trace["e_est"].append(e_est)
+        trace["e_trial"].append(e_trial)
+    return trace, x, weights

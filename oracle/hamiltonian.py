@@ -96,9 +96,10 @@ def local_energy(logabs: Callable[[torch.Tensor], torch.Tensor], atoms, charges,
 
 
 def batch_local_energy(net, params, pos: torch.Tensor, method: str = "jvp", chunk: int = 64):
-    """E_L, log|psi|, grad log|psi| for a batch pos[B,3N] (float64)."""
-    atoms = net.atoms
-    charges = net.charges
+    """E_L, log|psi|, grad log|psi| for a batch pos[B,3N], in the dtype of pos (float64, or
+    float32/complex64 -- the reference's own arithmetic)."""
+    atoms = net.atoms.to(pos.dtype)
+    charges = net.charges.to(pos.dtype)
     f = lambda x: net.logabs(params, x)
     if method == "jvp":
         el_fn = vmap(local_energy(f, atoms, charges, method))

@@ -95,6 +95,14 @@ def c_atom_ccecp() -> ECP:
                [[[7.76079, 0], [0, 0], [0, 0]]], 2)
 
 
+def c2_ccecp() -> ECP:
+    """example/C2/C2.py:12-27: the carbon ccECP block on each of the two atoms (list_l = 2)."""
+    c = c_atom_ccecp()
+    two = lambda a: np.concatenate([a, a], axis=0)
+    return ECP(two(c.rn_local), two(c.local_coes), two(c.local_exps), two(c.rn_non_local), two(c.non_local_coes),
+               two(c.non_local_exps), 2)
+
+
 def local_pp_energy(ecp: ECP, pos: torch.Tensor, atoms: torch.Tensor, charges: torch.Tensor):
     """local_pp_energy (pseudopotential.py:86-117) summed over electrons and atoms."""
     N = pos.shape[0] // 3

@@ -102,13 +102,20 @@ def make_system(name: str) -> System:
     elif name == "C2":
         atoms = np.array([[0.0, 0.0, -1.0], [0.0, 0.0, 1.0]])   # C2test.py:9
         charges = np.array([6.0, 6.0])
+    elif name == "C2_ecp":
+        # example/C2/C2.py:8-10: ccECP carbons at z = -+1, Z_eff 4, BLOCK spins [+1]*4 + [-1]*4
+        atoms = np.array([[0.0, 0.0, -1.0], [0.0, 0.0, 1.0]])
+        charges = np.array([4.0, 4.0])
     elif name == "N2":
         atoms = np.array([[0.0, 0.0, -1.0372], [0.0, 0.0, 1.0372]])
         charges = np.array([7.0, 7.0])
+    elif name == "O2":
+        atoms = np.array([[0.0, 0.0, -1.1408], [0.0, 0.0, 1.1408]])
+        charges = np.array([8.0, 8.0])
     else:
         raise KeyError(name)
     n = int(charges.sum())
-    spins = alternating_spins(n)
+    spins = alternating_spins(n) if name != "C2_ecp" else np.array([1.0] * (n // 2) + [-1.0] * (n - n // 2))
     nup = int((spins > 0).sum())
     return System(name, atoms.astype(np.float64), charges.astype(np.float64), spins, (nup, n - nup))
 

@@ -1,6 +1,6 @@
 """Generate the golden parity fixtures in tests/golden/ from the float64 oracle.
 
-Run from the repo root:  python tests/golden/make_golden.py
+Run from the repo root:  python tests/golden/make_golden.py [names...]  (default: all)
 Each <system>.npz holds (all float64):
   params_flat   canonical tree_flatten parameter vector (aiqmc_set_params input)
   pos           [B,3N] walker positions (init_electrons semantics, width 1.0)
@@ -25,12 +25,13 @@ from oracle import hamiltonian, mcstep, network, system  # noqa: E402
 
 torch.set_default_dtype(torch.float64)
 
-SYSTEMS = {"H2": 8, "Be": 8, "N2": 8}
+SYSTEMS = {"H2": 8, "Be": 8, "N2": 8, "Ne": 8, "C2": 4, "O2": 4}
+SEEDS = {"H2": 11, "Be": 12, "N2": 13, "Ne": 14, "C2": 16, "O2": 15}
 
 
 def make(name: str, B: int, out_dir: str):
     s = system.make_system(name)
-    rng = np.random.default_rng({"H2": 11, "Be": 12, "N2": 13}[name])
+    rng = np.random.default_rng(SEEDS[name])
     params = system.init_params(rng, s, randomize_aux=True)
     flat = system.flatten_params(params)
     pos = system.init_electrons(rng, s.atoms, s.charges, B, 1.0)
@@ -56,5 +57,5 @@ def make(name: str, B: int, out_dir: str):
 
 if __name__ == "__main__":
     out = os.path.dirname(os.path.abspath(__file__))
-    for n, b in SYSTEMS.items():
-        make(n, b, out)
+    for n in sys.argv[1:] or list(SYSTEMS):
+        make(n, SYSTEMS[n], out)

@@ -40,7 +40,7 @@ def _ctx(name, dtype=torch.float64):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["Be", "N2"])
+@pytest.mark.parametrize("name", ["Be", "N2", "Ne"])
 def test_drift_diffusion_matches_oracle(name):
     from oracle import network, system
     s, ctx = _ctx(name)
@@ -193,10 +193,10 @@ def test_tmoves_golden_fixture(golden_dir):
     assert (np.abs(g["new_attractive"] - g["pos"]).sum() > 0)
 
 
-def _tm_ctx(dtype, ecp):
+def _tm_ctx(dtype, ecp, sysname="C_ecp"):
     from oracle import system
     from aiqmc import _lib
-    s = system.make_system("C_ecp")
+    s = system.make_system(sysname)
     t = s.tables()
     ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
                        t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"], dtype=dtype, device=0)
@@ -216,6 +216,51 @@ def test_tmoves_match_golden(golden_dir, name):
     ecp = opp.c_atom_ccecp() if name == "ccecp" else opp.ECP([[1.0]], [[0.0]], [[1.0]], [[[2.0], [1.0]]],
                                                             [[[-3.0], [-5.0]]], [[[0.7], [0.4]]], 1)
     s, ctx = _tm_ctx(torch.float64, ecp)
+    ctx.set_params(g["params_flat"])
+    pos = torch.tensor(g["pos"], device="cuda").contiguous()
+    acc = ctx.dmc_tmoves(pos, float(g[f"tstep_{name}"]), rot=torch.tensor(g["rot"]), u_sel=torch.tensor(g["u_sel"]),
+                         u_acc=torch.tensor(g["u_acc"]))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(pos.cpu().numpy(), g[f"new_{name}"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(acc.cpu().numpy(), g[f"acc_{name}"], rtol=1e-8, atol=1e-10)
+
+
+def _c2_tables(name):
+    from oracle import pphamiltonian as opp
+    if name == "ccecp":
+        return opp.c2_ccecp()
+    return opp.ECP([[1.0], [1.0]], [[0.0], [0.0]], [[1.0], [1.0]], [[[2.0], [1.0]]] * 2, [[[-3.0], [-5.0]]] * 2,
+                   [[[0.7], [0.4]]] * 2, 1)
+
+
+def test_c2_tmoves_golden_fixture(golden_dir):
+    """C2 example (atoms at z = -+1): the fixture is what the oracle computes (one walker
+    recomputed), moved electrons sit at |x_i| = r_ia about the ORIGIN (E2) and some move."""
+    import os
+    from oracle import network, system
+    g = dict(np.load(os.path.join(golden_dir, "C2_tmoves.npz")))
+    s = system.make_system("C2_ecp")
+    net = network.Network(s)
+    pt = network.to_torch(system.unflatten_params(system.init_params(np.random.default_rng(0), s), g["params_flat"]))
+    nb, ab = odmc.tmoves(net, pt, _c2_tables("attractive"), torch.tensor(g["pos"][0]), g["rot"][0], g["u_sel"][0],
+                         g["u_acc"][0], float(g["tstep_attractive"]))
+    np.testing.assert_allclose(nb.numpy(), g["new_attractive"][0], rtol=1e-12, atol=1e-12)
+    new, pos = g["new_attractive"].reshape(-1, 8, 3), g["pos"].reshape(-1, 8, 3)
+    moved = np.abs(new - pos).sum(-1) > 0
+    assert moved.any()
+    r_new = np.linalg.norm(new, axis=-1)
+    r_ia = np.linalg.norm(pos[:, :, None, :] - s.atoms[None, None], axis=-1)      # [B, N, A]
+    ok = np.min(np.abs(r_new[..., None] - r_ia), axis=-1) < 1e-6
+    assert ok[moved].all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ccecp", "attractive"])
+def test_c2_tmoves_match_golden(golden_dir, name):
+    """HIP T-moves on the C2 example (fp64, injected draws) reproduce the oracle fixture."""
+    import os
+    g = dict(np.load(os.path.join(golden_dir, "C2_tmoves.npz")))
+    s, ctx = _tm_ctx(torch.float64, _c2_tables(name), "C2_ecp")
     ctx.set_params(g["params_flat"])
     pos = torch.tensor(g["pos"], device="cuda").contiguous()
     acc = ctx.dmc_tmoves(pos, float(g[f"tstep_{name}"]), rot=torch.tensor(g["rot"]), u_sel=torch.tensor(g["u_sel"]),
@@ -352,3 +397,69 @@ def test_main_dmc_driver_runs_from_vmc_checkpoint(tmp_path):
     assert data.positions.shape == (B, 12) and torch.isfinite(data.positions).all()
     rows = open(tmp_path / "DMC_states.csv").read().strip().split("\n")
     assert rows[0] == "block,energy,positions" and len(rows) >= 3
+
+
+# ----------------------------------------------------------------------------- multi-step DMC trajectories
+
+_TRAJ_TABLES = {
+    "ccecp": lambda opp: opp.c_atom_ccecp(),
+    "attractive": lambda opp: opp.ECP([[1.0]], [[0.0]], [[1.0]], [[[2.0], [1.0]]], [[[-3.0], [-5.0]]],
+                                      [[[0.7], [0.4]]], 1),
+    "ne_allelectron": lambda opp: opp.ECP([[1.0]], [[0.0]], [[1.0]], [[[2.0], [2.0], [2.0]]], [[[0.0], [0.0], [0.0]]],
+                                          [[[1.0], [1.0], [1.0]]], 2),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ccecp", "attractive", "ne_allelectron"])
+def test_dmc_trajectory_matches_oracle(golden_dir, name):
+    """The driver's block loop (aiqmc.DMC.main_dmc.dmc_blocks: dmc_propagate_run steps = T-moves,
+    drift-diffusion, pp energies, weights; then comb, re-indexing, e_est / e_trial feedback) with
+    every draw injected reproduces the oracle's chain (oracle.dmc.dmc_blocks, main_dmc.py:113-244):
+    first block with per-walker e_trial = e_est, branch cut 10 std(E_L); positions to 1e-9,
+    weights to 1e-12 relative, comb indices exact.  ne_allelectron: all-electron Ne (10 e-)
+    through the pp-only DMC step with zero ECP coefficients (BASELINE's "Ne + DMC")."""
+    import os
+    from oracle import pphamiltonian as opp, system
+    from aiqmc import systems
+    from aiqmc.DMC import dmc, main_dmc
+    from aiqmc.DMC.Tmoves import HostTmoveDraws
+    from aiqmc.VMC.VMCmcstep import HostDraws
+    from aiqmc.wavefunction_Ynlm import nn
+    sysname = "Ne" if name == "ne_allelectron" else "C_ecp"
+    g = dict(np.load(os.path.join(golden_dir, f"{'Ne' if sysname == 'Ne' else 'C'}_dmc_{name}.npz")))
+    s = systems.make_system(sysname)
+    N, A = s.nelectrons, s.natoms
+    network = s.make_network()
+    params = system.unflatten_params(system.init_params(np.random.default_rng(0), system.make_system(sysname)),
+                                     g["params_flat"])
+    e = _TRAJ_TABLES[name](opp)
+    B = g["x0"].shape[0]
+    nblocks, iters = g["newinds"].shape[0], g["weights"].shape[0] // g["newinds"].shape[0]
+    tstep = float(g["tstep"])
+    run = dmc.dmc_propagate(network.apply, nn.make_log_network(network.apply), network.apply, e.list_l, N, A, 3, B,
+                            tstep, 1, s.charges, s.spins, e.rn_local, e.local_coes, e.local_exps, e.rn_non_local,
+                            e.non_local_coes, e.non_local_exps)
+    ctx = network.apply._aiqmc_network.bind(params, s.atoms, torch.float64)
+    data = nn.AINetData(positions=torch.tensor(g["x0"], device="cuda").contiguous(), spins=s.spins, atoms=s.atoms,
+                        charges=s.charges)
+    e_l0 = torch.complex(torch.tensor(g["e_l0_re"]), torch.tensor(g["e_l0_im"])).cuda()
+    d0 = e_l0 - e_l0.mean()
+    var0 = (d0 * d0.conj()).mean()
+    T = lambda a: torch.tensor(a)
+    step_key = lambda k: dmc.HostDmcDraws(HostTmoveDraws(T(g["rot_tm"][k]), T(g["u_sel"][k]), T(g["u_acc"][k])),
+                                          HostDraws(T(g["gauss1"][k]), T(g["gauss2"][k]), T(g["u"][k])),
+                                          T(g["rot_old"][k]), T(g["rot_new"][k]))
+    block_draws = lambda b: (float(g["u_comb"][b]), T(g["extra"][b]))
+    est, data, w, trace = main_dmc.dmc_blocks(run, ctx, params, data, e_l0, var0, nblocks, iters, float(g["feedback"]),
+                                              step_key, block_draws)
+    torch.cuda.synchronize()
+    for k in range(nblocks * iters):
+        np.testing.assert_allclose(trace["positions"][k].cpu().numpy(), g["positions"][k], rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(trace["energy"][k].real.cpu().numpy(), g["energy_re"][k], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(trace["weights"][k].cpu().numpy(), g["weights"][k], rtol=1e-12)
+    for b in range(nblocks):
+        np.testing.assert_array_equal(trace["newinds"][b].cpu().numpy(), g["newinds"][b])
+        assert abs(trace["comb_weight"][b] - g["comb_weight"][b]) <= 1e-12 * abs(g["comb_weight"][b])
+        assert abs(est[b] - g["e_est"][b]) < 1e-9 and abs(trace["e_trial"][b] - g["e_trial"][b]) < 1e-9
+    np.testing.assert_allclose(data.positions.cpu().numpy(), g["x_final"], rtol=1e-9, atol=1e-9)

@@ -105,9 +105,10 @@ def test_cos_theta_quirk():
         np.testing.assert_allclose(cfg[0, 0].numpy(), np.linalg.norm(pos.numpy()) * g, rtol=1e-15)
 
 
-def test_golden_fixture_consistent(golden_dir):
-    g = dict(np.load(os.path.join(golden_dir, "C_ecp.npz")))
-    assert g["pos"].shape == (4, 12) and g["rot"].shape == (4, 3, 3)
+@pytest.mark.parametrize("name,n3", [("C_ecp", 12), ("C2_ecp", 24)])
+def test_golden_fixture_consistent(golden_dir, name, n3):
+    g = dict(np.load(os.path.join(golden_dir, f"{name}.npz")))
+    assert g["pos"].shape == (4, n3) and g["rot"].shape == (4, 3, 3)
     np.testing.assert_allclose(np.einsum("bij,bkj->bik", g["rot"], g["rot"]), np.broadcast_to(np.eye(3), (4, 3, 3)),
                                atol=1e-12)
     assert np.all(np.isfinite(g["e_re"])) and np.all(np.isfinite(g["logq_re"]))
@@ -115,23 +116,26 @@ def test_golden_fixture_consistent(golden_dir):
 
 # ----------------------------------------------------------------------------- GPU: HIP vs oracle
 
-def _ecp_ctx(dtype):
+def _ecp_ctx(dtype, name="C_ecp"):
     from oracle import system
     from aiqmc import _lib
-    s = system.make_system("C_ecp")
+    s = system.make_system(name)
     t = s.tables()
     ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
                        t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"], dtype=dtype, device=0)
-    e = pp.c_atom_ccecp()
+    e = pp.c_atom_ccecp() if name == "C_ecp" else pp.c2_ccecp()
     ctx.set_ecp(e.rn_local, e.local_coes, e.local_exps, e.rn_non_local, e.non_local_coes, e.non_local_exps, e.list_l)
     return s, ctx
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["C_ecp", "C2_ecp"])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-def test_ecp_local_energy_golden(golden_dir, dtype):
-    g = dict(np.load(os.path.join(golden_dir, "C_ecp.npz")))
-    s, ctx = _ecp_ctx(dtype)
+def test_ecp_local_energy_golden(golden_dir, dtype, name):
+    """C atom and the C2 example (two ccECP centres off the origin: quirk E2, the rotated
+    electron NOT offset by its atom, changes the answer there)."""
+    g = dict(np.load(os.path.join(golden_dir, f"{name}.npz")))
+    s, ctx = _ecp_ctx(dtype, name)
     ctx.set_params(g["params_flat"])
     pos = torch.tensor(g["pos"], dtype=dtype, device="cuda")
     rot = torch.tensor(g["rot"], dtype=dtype, device="cuda")
@@ -151,10 +155,11 @@ def test_ecp_local_energy_golden(golden_dir, dtype):
 
 
 @pytest.mark.gpu
-def test_ecp_reuse_matches_scratch(golden_dir):
+@pytest.mark.parametrize("name", ["C_ecp", "C2_ecp"])
+def test_ecp_reuse_matches_scratch(golden_dir, name):
     """Quadrature configurations from the walker cache == evaluated from scratch (fp64)."""
-    g = dict(np.load(os.path.join(golden_dir, "C_ecp.npz")))
-    s, ctx = _ecp_ctx(torch.float64)
+    g = dict(np.load(os.path.join(golden_dir, f"{name}.npz")))
+    s, ctx = _ecp_ctx(torch.float64, name)
     ctx.set_params(g["params_flat"])
     pos = torch.tensor(g["pos"], device="cuda")
     rot = torch.tensor(g["rot"], device="cuda")
@@ -203,3 +208,21 @@ def test_ecp_errors():
     with pytest.raises(RuntimeError, match="list_l"):
         ctx.set_ecp(e.rn_local, e.local_coes, e.local_exps, np.zeros((1, 5, 2)), np.zeros((1, 5, 2)),
                     np.zeros((1, 5, 2)), 4)
+
+
+def test_c2_quadrature_not_offset_by_atom():
+    """E2 on the C2 example: the quadrature configuration of electron i about atom a puts it at
+    r_ia p_q -- on a sphere about the ORIGIN, not about the atom at z = -+1."""
+    from oracle import system
+    s = system.make_system("C2_ecp")
+    rng = np.random.default_rng(3)
+    pos = torch.tensor(system.init_electrons(rng, s.atoms, s.charges, 1, 1.0)[0])
+    atoms = torch.tensor(s.atoms)
+    groups, _ = pp.quadrature_grids()
+    cos, cfg = pp.rotated_configurations(pos, atoms, groups[0])
+    x = pos.numpy().reshape(8, 3)
+    r = np.linalg.norm(x[:, None, :] - s.atoms[None], axis=-1)               # [N, A]
+    moved = cfg.numpy().reshape(8, 2, groups[0].shape[0], 8, 3)
+    for i in range(8):
+        for a in range(2):
+            np.testing.assert_allclose(np.linalg.norm(moved[i, a, :, i], axis=-1), r[i, a], rtol=1e-7)

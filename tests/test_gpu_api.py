@@ -140,3 +140,34 @@ def test_adam_training_step_matches_oracle():
     # the reference schedule collapses after step 0: the second step leaves the parameters unchanged
     _, p2, state, _, _ = step(data, new_params, state, 1)
     np.testing.assert_allclose(system.flatten_params(p2), system.flatten_params(new_params), rtol=0, atol=1e-300)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["N2", "Be", "C2_ecp"])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_network_orbitals_match_oracle(name, dtype):
+    """Network.orbitals (nn.py:409-506,553): the complex [N, N] matrix, rows up then down
+    electrons, row r with electron r's envelope / y row (Q1), times exp(J_ee/N) exp(J_ae/N);
+    its slogdet is apply()'s output."""
+    from oracle import network, system
+    from aiqmc import systems
+    s = systems.make_system(name)
+    net = s.make_network()
+    os_ = system.make_system(name)
+    rng = np.random.default_rng(3)
+    params = system.init_params(rng, os_, randomize_aux=True)
+    pos = system.init_electrons(rng, os_.atoms, os_.charges, 6, 1.0)
+    x = torch.tensor(pos, dtype=dtype, device="cuda")
+    (m,) = net.orbitals(params, x, s.spins, s.atoms, s.charges)
+    phase, logabs = net.apply(params, x, s.spins, s.atoms, s.charges)
+    torch.cuda.synchronize()
+    assert m.shape == (6, s.nelectrons, s.nelectrons) and m.is_complex()
+    onet = network.Network(os_)
+    pt = network.to_torch(params)
+    ref = torch.stack([onet.orbitals(pt, torch.tensor(pos[b])) for b in range(6)]).numpy()
+    got = m.to(torch.complex128).cpu().numpy()
+    tol = 1e-10 if dtype == torch.float64 else 2e-4
+    scale = np.abs(ref).max(axis=(1, 2), keepdims=True)
+    assert np.all(np.abs(got - ref) <= tol * scale), float(np.max(np.abs(got - ref) / scale))
+    sign, ld = np.linalg.slogdet(got)
+    np.testing.assert_allclose(ld, logabs.double().cpu().numpy(), rtol=tol, atol=tol * 10)

@@ -34,9 +34,10 @@ def _walkers(s, B, seed=0):
     return system.init_electrons(np.random.default_rng(seed), s.atoms, s.charges, B, 1.0)
 
 
+@pytest.mark.parametrize("name", ["N2", "Ne"])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-def test_reverse_vs_forward_gradient_4096(dtype):
-    s, ctx = _ctx("N2", dtype)
+def test_reverse_vs_forward_gradient_4096(dtype, name):
+    s, ctx = _ctx(name, dtype)
     pos = torch.tensor(_walkers(s, 4096), dtype=dtype, device="cuda")
     la_r, g_r = ctx.logpsi_grad(pos)
     la_f, g_f = ctx.logpsi_grad_forward_mode(pos)
@@ -75,8 +76,10 @@ def test_float32_matches_float64_4096():
     assert np.mean(rel < 1e-2) > 0.99
 
 
-def test_philox_mc_is_deterministic_and_sane():
-    s, ctx = _ctx("N2", torch.float32)
+@pytest.mark.parametrize("name", ["N2", "Ne"])
+def test_philox_mc_is_deterministic_and_sane(name):
+    s, ctx = _ctx(name, torch.float32)
+    N = s.nelectrons
     x0 = torch.tensor(_walkers(s, 4096, seed=4), dtype=torch.float32, device="cuda")
     a = x0.clone().contiguous()
     b = x0.clone().contiguous()
@@ -85,8 +88,8 @@ def test_philox_mc_is_deterministic_and_sane():
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     assert torch.isfinite(a).all()
-    moved = (a - x0).abs().reshape(4096, 14, 3).amax(-1) > 0
-    rate = float(acc_a.sum()) / (4096 * 14 * 3)
+    moved = (a - x0).abs().reshape(4096, N, 3).amax(-1) > 0
+    rate = float(acc_a.sum()) / (4096 * N * 3)
     assert 0.05 < rate < 1.0, rate
     assert 0.05 < float(moved.float().mean()) <= 1.0
     c = x0.clone().contiguous()
@@ -108,7 +111,7 @@ def test_ragged_batches_match_full_batch(B):
         assert torch.allclose(gr, g_full[:B], rtol=1e-9, atol=1e-9)
 
 
-@pytest.mark.parametrize("name", ["H2", "Be", "C", "Ne", "C2"])
+@pytest.mark.parametrize("name", ["H2", "Be", "C", "Ne", "C2", "C2_ecp", "O2"])
 def test_other_shapes_reverse_vs_forward(name):
     s, ctx = _ctx(name, torch.float64)
     pos = torch.tensor(_walkers(s, 256), device="cuda")
@@ -119,7 +122,7 @@ def test_other_shapes_reverse_vs_forward(name):
     assert torch.allclose(la_r, la_f, rtol=1e-10, atol=1e-10)
 
 
-@pytest.mark.parametrize("name", ["H2", "Be", "C", "Ne", "C2", "N2"])
+@pytest.mark.parametrize("name", ["H2", "Be", "C", "Ne", "C2", "C2_ecp", "N2", "O2"])
 def test_proposal_reuse_matches_recompute(name):
     """Proposals from the walker cache (moved electron + its 2(N-1) pairs recomputed)
     == proposals evaluated from scratch, on the same Philox draws."""
@@ -174,7 +177,7 @@ def test_local_energy_adjoint_vs_forward_laplacian_4096(dtype):
         assert torch.all((g1 - g0).abs() <= 2e-3 * scale)
 
 
-@pytest.mark.parametrize("name", ["H2", "Be", "C", "Ne", "C2"])
+@pytest.mark.parametrize("name", ["H2", "Be", "C", "Ne", "C2", "C2_ecp", "O2"])
 def test_other_shapes_local_energy_adjoint_vs_forward(name):
     s, ctx = _ctx(name, torch.float64)
     pos = torch.tensor(_walkers(s, 256, seed=13), device="cuda")

@@ -75,3 +75,21 @@ def test_complex_energy_gradient_reduces_to_weights():
             cl = diff + e
         want = (2.0 / B) * (diff.real @ Oa + cl.imag @ Op)
         np.testing.assert_allclose(g, want, rtol=1e-12, atol=1e-12)
+
+
+def test_clip_from_median_complex_matches_oracle():
+    """loss.clip_local_values with clip_from_median=True on complex E_L (the pp drivers' path):
+    the centre is the real median (jnp.median: even count -> mean of the middle pair) and the
+    imaginary window is centred at 0 (JAX's .imag of a real array)."""
+    from aiqmc.Loss.loss import clip_local_values
+    rng = np.random.default_rng(5)
+    e = rng.standard_normal(40) + 1j * rng.standard_normal(40)
+    e[7] = 30.0 + 25.0j
+    mean = e.mean()
+    center, diff = clip_local_values(torch.tensor(e), torch.tensor(mean), 5.0, True, True)
+    med = np.median(e.real)
+    tv_re = np.mean(np.abs(e.real - med))
+    tv_im = np.mean(np.abs(e.imag - 0.0))
+    clipped = np.clip(e.real, med - 5 * tv_re, med + 5 * tv_re) + 1j * np.clip(e.imag, -5 * tv_im, 5 * tv_im)
+    np.testing.assert_allclose(center.numpy(), clipped.mean(), rtol=1e-12)
+    np.testing.assert_allclose(diff.numpy(), clipped - clipped.mean(), rtol=1e-12, atol=1e-12)
