@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_debug_set_proposal_reuse", "aiqmc_debug_phase_cycles", "aiqmc_debug_local_energy_forward",
     "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
     "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves", "aiqmc_phase_param_grad",
-    "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals",
+    "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals", "aiqmc_debug_set_ablate",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -107,6 +107,8 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_debug_logpsi_grad_forward.restype = ctypes.c_int
     lib.aiqmc_debug_local_energy_forward.argtypes = [vp, vp, i32, vp, vp, vp, vp]
     lib.aiqmc_debug_local_energy_forward.restype = ctypes.c_int
+    lib.aiqmc_debug_set_ablate.argtypes = [vp, i32]
+    lib.aiqmc_debug_set_ablate.restype = ctypes.c_int
     lib.aiqmc_debug_set_proposal_reuse.argtypes = [vp, i32]
     lib.aiqmc_debug_set_proposal_reuse.restype = ctypes.c_int
     lib.aiqmc_debug_phase_cycles.argtypes = [vp, vp]
@@ -288,6 +290,10 @@ class Context:
         check(self._lib.aiqmc_debug_logpsi_grad_forward(self._h, _ptr(p), B, _ptr(logabs), _ptr(grad),
                                                         _stream(self.device)), "aiqmc_debug_logpsi_grad_forward")
         return logabs, grad
+
+    def set_ablate(self, mask: int):
+        """Development builds (-DAQ_ABLATE) only: skip proposal phases to time them."""
+        check(self._lib.aiqmc_debug_set_ablate(self._h, int(mask)), "aiqmc_debug_set_ablate")
 
     def set_proposal_reuse(self, on: bool):
         """Diagnostics: proposals from the walker cache (default) or recomputed from scratch."""

@@ -692,6 +692,7 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
   kp.logabs = c->d_lpn;
   kp.gown = c->d_gown;
   kp.sumsq = c->d_sqn;
+  kp.ablate = c->ablate;
   if (c->reuse) {
     // moved electron's local stage for all B*N proposals, then proposals from the walker caches
     kp.wcache = c->d_wc;
@@ -1196,6 +1197,12 @@ int aiqmc_debug_logpsi_grad_forward(aiqmc_ctx* c, const void* pos, int32_t B, vo
   ka.grad = grad;
   ops.walker(c->dtype, MODE_GRAD_FWD, ka, B, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_debug_set_ablate(aiqmc_ctx* c, int32_t mask) {
+  if (!c) return fail(AIQMC_EINVAL, "null context");
+  c->ablate = mask;
   return AIQMC_OK;
 }
 

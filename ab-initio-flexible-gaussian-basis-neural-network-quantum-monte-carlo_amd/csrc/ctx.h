@@ -10,8 +10,13 @@
 #include "aiqmc.h"
 #include "walker_kernel.h"
 
-// (N, A) instantiations; the Makefile compiles shape.hip once per entry.
+// (N, A) instantiations; the Makefile compiles shape.hip once per entry.  A development build
+// may restrict the list (make dev: -DAIQMC_DEV_SHAPES, N2 only).
+#ifdef AIQMC_DEV_SHAPES
+#define AIQMC_SHAPE_LIST(X) X(14, 2)
+#else
 #define AIQMC_SHAPE_LIST(X) X(2, 2) X(4, 1) X(6, 1) X(8, 1) X(8, 2) X(10, 1) X(12, 2) X(14, 2) X(16, 2)
+#endif
 
 int aiqmc_fail(int code, const std::string& msg);
 using aq::KArgs;
@@ -37,6 +42,7 @@ struct aiqmc_ctx {
   void* d_lc = nullptr;                                     // local-energy LapCache [B][lcache_n]
   int lc_B = 0, lc_n = 0;
   bool reuse = true;                                        // proposals reuse the walker's cached stage
+  int ablate = 0;                                           // AQ_ABLATE development builds (walker_rev.h)
   double* d_taueff = nullptr;
   int64_t ws_bytes = 0;
   // pseudopotential (aiqmc_set_ecp / aiqmc_local_energy_ecp, ecp.h)

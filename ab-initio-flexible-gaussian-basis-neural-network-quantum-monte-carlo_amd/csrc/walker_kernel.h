@@ -55,6 +55,7 @@ struct KArgs {
   const void* xnew;
   int value_only;         // k_walker_rev: log|psi| and phase only (no backward pass)
   void* orb;              // k_walker_rev value_only: the orbital matrix [nconf][N][N][re,im] (nn.py:409-506)
+  int ablate;             // -DAQ_ABLATE development builds only: proposal phases to skip (walker_rev.h)
   int phase_grad;         // k_param_grad: d phase / d theta instead of d log|psi| / d theta
   // walker launch of a Metropolis sweep (k_walker_rev, PROP = false): dg1/dg2/du != nullptr:
   // lanes e < N of wave b write the sweep's Philox draws of walker b exactly as k_draws would

@@ -217,7 +217,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   const int nup = ka.nup;
   const int l49 = lane < 48 ? lane : 48;
   T* yd = sm + SM::yd;
-  const cptr<T> Lc = (const T*)ka.lapcache + (size_t)conf * LC::size;
+  const cptr<T> Lc = param_ptr<T>((const T*)ka.lapcache + (size_t)conf * LC::size);
 
   if (lane < 3 * N) xs[lane] = ((const T*)ka.pos)[(size_t)conf * 3 * N + lane];
   T h0b[D0];

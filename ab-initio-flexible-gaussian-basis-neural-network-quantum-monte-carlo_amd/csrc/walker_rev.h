@@ -44,6 +44,14 @@ static __device__ unsigned long long aq_phase_cycles[32];
   } while (0)
 #endif
 
+// Development builds (-DAQ_ABLATE): KArgs.ablate skips phases of the proposal path, so that the
+// marginal cost of each phase can be timed (results are garbage; never in a product build).
+#ifdef AQ_ABLATE
+#define AQ_ABL(b) (ka.proposal && (ka.ablate & (b)))
+#else
+#define AQ_ABL(b) false
+#endif
+
 template <typename T, int N, int A>
 struct SmemRev {
   static constexpr int D0 = 4 * A;               // layer-0 h width
@@ -215,8 +223,11 @@ __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
 // Occupancy hint per instantiation: fp32 N2 (14, 2) lands one VGPR above the
 // 4-waves/SIMD budget (128) without it and fits it without spilling with it.
 // PREP (the adjoint pass of the local energy, walker_lap.h) asks for 2.
+#ifndef AQ_PROP_WAVES
+#define AQ_PROP_WAVES 5
+#endif
 template <typename T, int N, int A, bool PREP, bool PROP> struct RevWaves {
-  static constexpr int value = PREP ? 2 : ((sizeof(T) == 4 && N == 14 && A == 2) ? (PROP ? 5 : 4) : 1);
+  static constexpr int value = PREP ? 2 : ((sizeof(T) == 4 && N == 14 && A == 2) ? (PROP ? AQ_PROP_WAVES : 4) : 1);
 };
 
 // PREP = false: value + gradient (Metropolis walker launches and single-electron proposal / ECP
@@ -363,7 +374,7 @@ k_walker_rev(KArgs ka) {
   // ------------------------------------------------------------------ F2+F3 pair stream + spin-group column means
   // lane = (column i, quarter kq): pairs (k, i) with k = kq, kq+4, ...; the three layers'
   // h2[k,i] values are summed per spin group in registers and quad-reduced with DPP.
-  if (reuse) {
+  if (reuse && !AQ_ABL(1)) {
     // patch walker pb's sums with the 2(N-1) pairs of the moved electron pi. lane = 16*part + o:
     // part 0/1: pair (pi, o) at the new/old x_pi (column o); part 2/3: pair (o, pi) (column pi)
     T* S = sm + SM::R + 4;                          // [64][12] pair-stream values
@@ -407,7 +418,7 @@ k_walker_rev(KArgs ka) {
         if (k != pi) acc += S[(32 + k) * 12 + l * 4 + f] - S[(48 + k) * 12 + l * 4 + f];
       g2[((l * 2 + G) * N + pi) * 4 + f] += acc * (G ? ginv1 : ginv0);
     }
-  } else {
+  } else if (!reuse) {
     {
       const int i = lane >> 2, kq = lane & 3;
       const bool icol = i < N;
@@ -499,6 +510,7 @@ k_walker_rev(KArgs ka) {
   const int ic = ilive ? fi : N - 1;
   const bool inG1 = ic >= nup;
   T hreg = T(0);
+  if (!AQ_ABL(2)) {
 #pragma unroll
   for (int l = 0; l < 3; ++l) {
     const int d1 = l == 0 ? D0 : NH;
@@ -578,6 +590,7 @@ k_walker_rev(KArgs ka) {
     const T hin = l == 0 ? hl[ic * D0 + ff] : hreg;
     hreg = (d1 == NH) ? (hin + sval) * RSQ2 : sval;
   }
+  }
   if (ilive) hl[SM::hoff(3) + ic * 4 + ff] = hreg;
   __syncthreads();
   if (reuse && lane < 2 * N + 2) sm[SM::pv + lane] = pvr;   // read by the Gauss-Jordan after the Phi barrier
@@ -607,8 +620,12 @@ k_walker_rev(KArgs ka) {
   T logdet, phr, phi;
   if (reuse) {
     // the walker's pivot order (partial pivoting rerun only if a pivot comes out small)
-    bool bad;
-    gj_inverse_fixed<T, N>(Ph, Yv, Mx, lane, sm + SM::pv, logdet, phr, phi, bad);
+    bool bad = false;
+    logdet = phr = phi = T(0);
+    if (!AQ_ABL(4)) gj_inverse_fixed<T, N>(Ph, Yv, Mx, lane, sm + SM::pv, logdet, phr, phi, bad);
+#ifdef AQ_ABLATE
+    if (ka.ablate) bad = false;
+#endif
     if (bad) {
 #ifdef AQ_PHASE_PROF
       if (lane == 0) atomicAdd(&aq_phase_cycles[15], 1ull);   // fallback count (diagnostics build)
@@ -649,7 +666,7 @@ k_walker_rev(KArgs ka) {
   // ------------------------------------------------------------------ B1 adjoints of H (= h^3) and Yt
   T* hbar = sm + SM::hbar;
   T* ybar = sm + SM::ybar;
-  if (lane < 4 * N) {
+  if (lane < 4 * N && !AQ_ABL(8)) {
     const int r = lane >> 2, f = lane & 3;
     const int sp = r < nup ? 0 : 1;
     T q = T(0);
@@ -685,9 +702,11 @@ k_walker_rev(KArgs ka) {
   }
   __syncthreads();   // ybar overwrites Yt
   if constexpr (!PREP) {
-    for (int idx = lane; idx < N * N; idx += 64) {
-      const int r = idx / N, c = idx - r * N;
-      ybar[idx] = BRE(c, r) * Ph[idx * 2] - BIM(c, r) * Ph[idx * 2 + 1];
+    if (!AQ_ABL(8)) {
+      for (int idx = lane; idx < N * N; idx += 64) {
+        const int r = idx / N, c = idx - r * N;
+        ybar[idx] = BRE(c, r) * Ph[idx * 2] - BIM(c, r) * Ph[idx * 2 + 1];
+      }
     }
   }
 #undef BRE
@@ -698,7 +717,7 @@ k_walker_rev(KArgs ka) {
   // ------------------------------------------------------------------ B2 back through the h-stream layers
   // lane map of F4: the adjoint of h^{l+1}[i][f] stays in a register.
   T* g2b = sm + SM::g2;    // forward g2 values are dead after F4: reuse for their adjoints
-  {
+  if (!AQ_ABL(16)) {
     T hb = hbar[SM::hoff(3) + ic * 4 + ff];
 #pragma unroll
     for (int l = 2; l >= 0; --l) {
@@ -885,7 +904,7 @@ k_walker_rev(KArgs ka) {
   // Proposals from the walker cache: the 2(N-1) pairs of the moved electron pi come first
   // (iteration 0) and recompute their forward values; every other pair takes t1, t2
   // from walker pb's cache, so iterations >= 1 skip the forward recompute.
-  for (int it = lane; it < N * (N - 1); it += 64) {
+  for (int it = lane; it < (AQ_ABL(32) ? 0 : N * (N - 1)); it += 64) {
     int k, i;
     bool fresh = true;
     if (reuse) {
@@ -1002,7 +1021,7 @@ k_walker_rev(KArgs ka) {
   }
   // ------------------------------------------------------------------ B4 gradient per direction lane (c, e)
   T g = jd1;
-  {
+  if (!AQ_ABL(64)) {
     for (int k = 0; k < N; ++k) {
       if (k == le) continue;
       g += dbar[(k * N + le) * 3 + c4] - dbar[(le * N + k) * 3 + c4];

@@ -251,6 +251,10 @@ int aiqmc_debug_local_energy_forward(aiqmc_ctx* ctx, const void* pos, int32_t B,
  * proposal from scratch; both must agree to rounding. */
 int aiqmc_debug_set_proposal_reuse(aiqmc_ctx* ctx, int32_t on);
 
+/* Development builds (-DAQ_ABLATE) only: skip proposal-kernel phases (bit mask, walker_rev.h) to
+ * time their marginal cost; results are meaningless.  No effect in product builds. */
+int aiqmc_debug_set_ablate(aiqmc_ctx* ctx, int32_t mask);
+
 /* Diagnostics: shader-clock cycles per phase of the reverse-mode kernel, summed
  * over waves since the last call ([0..15] walker, [16..31] proposal launches);
  * all zero unless the library was built with -DAQ_PHASE_PROF. */

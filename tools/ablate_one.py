@@ -1,0 +1,15 @@
+"""One ablation mask (dev build with -DAQ_ABLATE): 2 Metropolis sweeps of 4096 N2 walkers (for PMC passes)."""
+import os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ab-initio-flexible-gaussian-basis-neural-network-quantum-monte-carlo_amd"))
+import torch
+from aiqmc import systems
+from aiqmc.initial_electrons_positions.init import init_electrons
+from aiqmc.wavefunction_Ynlm.nn import flatten_params
+s = systems.make_system("N2")
+ctx = s.context(dtype=torch.float32)
+ctx.set_params(flatten_params(s.make_network().init(1)))
+ctx.set_ablate(int(sys.argv[1]))
+pos = init_electrons(1000, None, s.atoms, s.charges, s.spins, 4096, 1.0)[0].to("cuda", torch.float32).contiguous()
+ctx.mc_step(pos, 2, 0.05, seed=1, offset=0)
+torch.cuda.synchronize()

@@ -1,0 +1,32 @@
+"""Short N2 VMC loop for profiling passes: warm-up, then `iters` iterations of mc_step (10 sweeps)
++ local_energy on 4096 walkers, fp32, Philox draws.  usage: python tools/mc_loop.py [iters] [system] [walkers]"""
+import os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ab-initio-flexible-gaussian-basis-neural-network-quantum-monte-carlo_amd"))
+import torch
+from aiqmc import systems, _lib
+from aiqmc.initial_electrons_positions.init import init_electrons
+from aiqmc.wavefunction_Ynlm.nn import flatten_params
+iters = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+name = sys.argv[2] if len(sys.argv) > 2 else "N2"
+B = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
+s = systems.make_system(name)
+ctx = s.context(dtype=torch.float32)
+ctx.set_params(flatten_params(s.make_network().init(1)))
+pos = init_electrons(1000, None, s.atoms, s.charges, s.spins, B, 1.0)[0].to("cuda", torch.float32).contiguous()
+ctx.mc_step(pos, 10, 0.05, seed=1, offset=0)
+ctx.local_energy(pos)
+torch.cuda.synchronize()
+ctx.profile(True)
+t0 = time.perf_counter()
+for k in range(iters):
+    ctx.mc_step(pos, 10, 0.05, seed=1, offset=10 * (k + 1))
+    el, _, _ = ctx.local_energy(pos)
+torch.cuda.synchronize()
+dt = (time.perf_counter() - t0) / iters
+ctx.profile(False)
+pm, pn = ctx.profile_read(_lib.PROF_MC_PROPOSAL)
+wm, wn = ctx.profile_read(_lib.PROF_MC_WALKER)
+lm, ln = ctx.profile_read(_lib.PROF_LOCAL_ENERGY)
+print(f"{name} B={B}: {1e3 * dt:.3f} ms/iter  proposal {1e3 * pm / max(pn, 1):.1f} us  walker {1e3 * wm / max(wn, 1):.1f} us"
+      f"  local-energy pair {1e3 * lm / max(ln, 1):.1f} us  finite={bool(torch.isfinite(el).all())}", flush=True)
