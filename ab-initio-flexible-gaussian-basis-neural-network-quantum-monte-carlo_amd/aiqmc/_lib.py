@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_debug_set_proposal_reuse", "aiqmc_debug_phase_cycles", "aiqmc_debug_local_energy_forward",
     "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
     "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves", "aiqmc_phase_param_grad",
-    "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals", "aiqmc_debug_set_ablate",
+    "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals", "aiqmc_debug_set_ablate", "aiqmc_debug_set_fuse_accept",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -109,6 +109,8 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_debug_local_energy_forward.restype = ctypes.c_int
     lib.aiqmc_debug_set_ablate.argtypes = [vp, i32]
     lib.aiqmc_debug_set_ablate.restype = ctypes.c_int
+    lib.aiqmc_debug_set_fuse_accept.argtypes = [vp, i32]
+    lib.aiqmc_debug_set_fuse_accept.restype = ctypes.c_int
     lib.aiqmc_debug_set_proposal_reuse.argtypes = [vp, i32]
     lib.aiqmc_debug_set_proposal_reuse.restype = ctypes.c_int
     lib.aiqmc_debug_phase_cycles.argtypes = [vp, vp]
@@ -290,6 +292,10 @@ class Context:
         check(self._lib.aiqmc_debug_logpsi_grad_forward(self._h, _ptr(p), B, _ptr(logabs), _ptr(grad),
                                                         _stream(self.device)), "aiqmc_debug_logpsi_grad_forward")
         return logabs, grad
+
+    def set_fuse_accept(self, on: bool):
+        """Diagnostics: fused (default) or separate per-sweep acceptance launch in mc_step."""
+        check(self._lib.aiqmc_debug_set_fuse_accept(self._h, int(bool(on))), "aiqmc_debug_set_fuse_accept")
 
     def set_ablate(self, mask: int):
         """Development builds (-DAQ_ABLATE) only: skip proposal phases to time them."""

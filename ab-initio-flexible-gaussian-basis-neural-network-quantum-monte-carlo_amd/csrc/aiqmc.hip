@@ -622,6 +622,7 @@ int aiqmc_debug_local_energy_forward(aiqmc_ctx* c, const void* pos, int32_t B, v
   if (rc) return rc;
   if (B == 0) return AIQMC_OK;
   if (!e_l) return fail(AIQMC_EINVAL, "null e_l");
+  HIPCHK(hipSetDevice(c->device));
   ShapeOps ops;
   shape_ops(c->N, c->A, &ops);
   KArgs ka = base_args(c);
@@ -635,13 +636,16 @@ int aiqmc_debug_local_energy_forward(aiqmc_ctx* c, const void* pos, int32_t B, v
   return AIQMC_OK;
 }
 
-// One drift-diffusion Metropolis sweep (VMCmcstep.py:28-111), 6 launches; step = Philox counter,
-// st = index into host draws.  dmc (optional, device doubles [3]): DMC drift-diffusion extras
-// (DMC/drift_diffusion.py:15-22): dmc[0] = sum of the proposed coordinates, dmc[2] = tdamp =
-// sum(x_new) / dmc[0].
+// One drift-diffusion Metropolis sweep (VMCmcstep.py:28-111); step = Philox counter, st = index
+// into host draws.  Launches: walker (+ the previous sweep's acceptance when *pending is set),
+// limdrift, moved electron, proposals, limdrift, and -- unless `defer` -- the acceptance.  With
+// `defer` the sweep's acceptance is left in *pending for the next sweep's walker launch (one
+// launch and one inter-kernel gap fewer per sweep; same arithmetic, accept_one).
+// dmc (optional, device doubles [3]): DMC drift-diffusion extras (DMC/drift_diffusion.py:15-22):
+// dmc[0] = sum of the proposed coordinates, dmc[2] = tdamp = sum(x_new) / dmc[0]; never deferred.
 static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double tstep, int rng_mode, const void* gauss1,
                     const void* gauss2, const void* u, int st, uint64_t seed, uint64_t step, int32_t* accept_out,
-                    double* dmc, hipStream_t s) {
+                    double* dmc, hipStream_t s, AccArgs* pending = nullptr, bool defer = false) {
   const int N = c->N;
   const size_t es = c->dtype == AIQMC_F32 ? 4 : 8;
   const char* g1;
@@ -656,7 +660,7 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
     g2 = (const char*)c->d_g2;
     uu = (const char*)c->d_u;
   }
-  // (1) grad log|psi| at the walkers (VMCmcstep.py:41-53)
+  // (1) grad log|psi| at the walkers (VMCmcstep.py:41-53), after the previous sweep's moves
   KArgs ka = base_args(c);
   ka.nconf = B;
   ka.pos = pos;
@@ -671,6 +675,10 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
     ka.dg1 = c->d_g1;
     ka.dg2 = c->d_g2;
     ka.du = c->d_u;
+  }
+  if (pending && pending->lpn) {
+    ka.acc = *pending;
+    pending->lpn = nullptr;
   }
   timed(c, 1, s, [&] { ops.walker(c->dtype, MODE_GRAD, ka, B, s); });
   // (2) limdrift factor over the device batch (:60)
@@ -718,9 +726,23 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
                                                         (const double*)g1, c->d_taueff, tstep, B * 3 * N, dmc);
   }
   // (5) acceptance and move (:83-106)
-  ops.accept(c->dtype, pos, c->d_grad, c->d_gown, c->d_lp, c->d_lpn, g1, g2, uu, c->d_taueff, B, tstep,
-             accept_out, s);
-    if (dmc) {
+  AccArgs a;
+  a.grad = c->d_grad;
+  a.lp = c->d_lp;
+  a.lpn = c->d_lpn;
+  a.gown = c->d_gown;
+  a.gauss1 = g1;
+  a.gauss2 = g2;
+  a.u = uu;
+  a.taueff = c->d_taueff;
+  a.tstep = tstep;
+  a.count = accept_out;
+  if (defer && pending && !dmc) {
+    *pending = a;
+    return 0;
+  }
+  ops.accept(c->dtype, pos, a, B, s);
+  if (dmc) {
     if (c->dtype == AIQMC_F32)
       k_dmc_sum<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)pos, nullptr, nullptr, nullptr, tstep, B * 3 * N,
                                                        dmc);
@@ -752,11 +774,10 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
     if (rc) return rc;
   }
   hipStream_t s = (hipStream_t)stream;
-  const int N = c->N;
-  const size_t es = c->dtype == AIQMC_F32 ? 4 : 8;
+  AccArgs pending{};
   for (int st = 0; st < nsteps; ++st) {
     rc = mc_sweep(c, ops, pos, B, tstep, rng_mode, gauss1, gauss2, u, st, seed, offset + (uint64_t)st, accept_out,
-                  nullptr, s);
+                  nullptr, s, &pending, c->fuse_accept && st + 1 < nsteps);
     if (rc) return rc;
   }
   HIPCHK(hipGetLastError());
@@ -1203,6 +1224,12 @@ int aiqmc_debug_logpsi_grad_forward(aiqmc_ctx* c, const void* pos, int32_t B, vo
 int aiqmc_debug_set_ablate(aiqmc_ctx* c, int32_t mask) {
   if (!c) return fail(AIQMC_EINVAL, "null context");
   c->ablate = mask;
+  return AIQMC_OK;
+}
+
+int aiqmc_debug_set_fuse_accept(aiqmc_ctx* c, int32_t on) {
+  if (!c) return fail(AIQMC_EINVAL, "null context");
+  c->fuse_accept = on != 0;
   return AIQMC_OK;
 }
 

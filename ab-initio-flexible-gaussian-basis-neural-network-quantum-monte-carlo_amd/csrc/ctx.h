@@ -42,7 +42,8 @@ struct aiqmc_ctx {
   void* d_lc = nullptr;                                     // local-energy LapCache [B][lcache_n]
   int lc_B = 0, lc_n = 0;
   bool reuse = true;                                        // proposals reuse the walker's cached stage
-  int ablate = 0;                                           // AQ_ABLATE development builds (walker_rev.h)
+  int ablate = 0;
+  int fuse_accept = 1;   // aiqmc_debug_set_fuse_accept: acceptance fused into the next walker launch                                           // AQ_ABLATE development builds (walker_rev.h)
   double* d_taueff = nullptr;
   int64_t ws_bytes = 0;
   // pseudopotential (aiqmc_set_ecp / aiqmc_local_energy_ecp, ecp.h)
@@ -70,9 +71,7 @@ struct aiqmc_ctx {
 struct ShapeOps {
   int (*set_lds)();
   void (*walker)(int dtype, int mode, const KArgs& ka, int nconf, hipStream_t s);
-  void (*accept)(int dtype, void* pos, const void* grad, const void* gown, const void* lp, const void* lpn,
-                 const void* g1, const void* g2, const void* u, const double* te, int B, double tstep,
-                 int32_t* acc, hipStream_t s);
+  void (*accept)(int dtype, void* pos, const aq::AccArgs& a, int B, hipStream_t s);
   void (*moved)(int dtype, const KArgs& ka, hipStream_t s);   // k_moved_electron over ka.nconf proposals
   // local energy: adjoint pass (k1) + first-derivative pass (k2), walker_lap.h
   void (*lap)(int dtype, const KArgs& k1, const KArgs& k2, int nconf, hipStream_t s);

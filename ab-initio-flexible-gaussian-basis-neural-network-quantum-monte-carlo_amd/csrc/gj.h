@@ -223,19 +223,16 @@ __device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bo
   }
   T zr = T(1), zi = T(0);
   bool small = false;
+  T pkr = T(1), pki = T(0);
 #pragma unroll
   for (int k = 0; k < N; ++k) {
     const int g = k / RW, ts = k % RW;
     const T pr = rdlane(pair_re<T>(a2[ts]), 16 * g + k);
     const T pim = rdlane(pair_im<T>(a2[ts]), 16 * g + k);
     const T den = pr * pr + pim * pim;
-    {
-      const T sk = rec[N + k];
-      const T ur = pr * sk, ui = pim * sk;
-      small = small || (ur * ur + ui * ui < T(1e-2));
-      const T nr = zr * ur - zi * ui, ni = zr * ui + zi * ur;
-      zr = nr;
-      zi = ni;
+    if (lane == k) {   // pivot k parked in lane k; the relative product is formed after the loop
+      pkr = pr;
+      pki = pim;
     }
     const T rden = f_rcp(den);
     const T ir = pr * rden, ii = -pim * rden;   // 1 / pivot
@@ -257,6 +254,39 @@ __device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bo
       a2[t] = n;
     }
     if (rg == g) a2[ts] = pair_make<T>(qr, qi);
+  }
+  {
+    // z = prod_k pivot_k / |walker pivot_k| over lanes 0..N-1 of row 0 (row_ror tree)
+    const bool pl = lane < N;
+    const T sk = pl ? rec[N + lane] : T(0);
+    T ur = pl ? pkr * sk : T(1), ui = pl ? pki * sk : T(0);
+    small = __ballot(pl && (ur * ur + ui * ui < T(1e-2))) != 0;
+    {
+      const T xr = dpp<0x128>(ur), xi = dpp<0x128>(ui);
+      const T nr = ur * xr - ui * xi, ni = ur * xi + ui * xr;
+      ur = nr;
+      ui = ni;
+    }
+    {
+      const T xr = dpp<0x124>(ur), xi = dpp<0x124>(ui);
+      const T nr = ur * xr - ui * xi, ni = ur * xi + ui * xr;
+      ur = nr;
+      ui = ni;
+    }
+    {
+      const T xr = dpp<0x122>(ur), xi = dpp<0x122>(ui);
+      const T nr = ur * xr - ui * xi, ni = ur * xi + ui * xr;
+      ur = nr;
+      ui = ni;
+    }
+    {
+      const T xr = dpp<0x121>(ur), xi = dpp<0x121>(ui);
+      const T nr = ur * xr - ui * xi, ni = ur * xi + ui * xr;
+      ur = nr;
+      ui = ni;
+    }
+    zr = rdlane(ur, 0);
+    zi = rdlane(ui, 0);
   }
   const int pc = clive ? (int)rec[c] : 0;
 #pragma unroll

@@ -17,46 +17,19 @@ using namespace aq;
 
 static int fail(int code, const std::string& m) { return aiqmc_fail(code, m); }
 
-// One thread per (walker b, electron i): t_pro (sum over xyz, Q6), acceptance
-// |exp(lp_i - lp)|^2 t_pro > u, move accepted electrons (VMCmcstep.py:80-106).
+// One thread per (walker b, electron i): the acceptance of walkers_update (VMCmcstep.py:80-106)
+// for the last sweep of aiqmc_mc_step (earlier sweeps fuse it into the next walker launch) and
+// for the DMC drift-diffusion step.
 template <typename T, int N>
-__global__ __launch_bounds__(256) void k_accept(T* __restrict__ pos, const T* __restrict__ grad,
-                                                const T* __restrict__ gown, const T* __restrict__ lp,
-                                                const T* __restrict__ lpn, const T* __restrict__ gauss1,
-                                                const T* __restrict__ gauss2, const T* __restrict__ u,
-                                                const double* __restrict__ taueff, int B, double tstep_d,
-                                                int32_t* accept_count) {
+__global__ __launch_bounds__(256) void k_accept(T* __restrict__ pos, AccArgs a, int B) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= B * N) return;
   const int b = t / N, i = t - b * N;
-  const T tstep = (T)tstep_d;
-  const T sq = sqrt(tstep);
-  const T te1 = (T)taueff[0], te2 = (T)taueff[1];
-  T z1[3], z2[3];
+  T xn[3];
+  if (accept_one<T, N>(a, pos, b, i, xn)) {
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    z1[c] = gauss1[(size_t)b * 3 * N + 3 * i + c];
-    z2[c] = gauss2[((size_t)b * N + i) * 3 + c];
-  }
-  const T uu = u[(size_t)b * N + i];
-  T gmove[3];
-  T tp = T(0);
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const T ge = grad[(size_t)b * 3 * N + 3 * i + c] * te1;      // grad_eff  (:60)
-    gmove[c] = ge * tstep + sq * z1[c];                          // g         (:62)
-    const T gn = gown[((size_t)b * N + i) * 3 + c] * te2;        // grad_new_eff (:80)
-    const T g2 = sq * z2[c];                                     // gauss2    (:83)
-    const T fw = g2 * g2;
-    const T bwv = g2 + (ge + gn) * tstep;
-    tp += exp((fw - bwv * bwv) / (T(2) * tstep));                // :84-94
-  }
-  const T e = exp(lpn[(size_t)b * N + i] - lp[b]);
-  const T acc = e * e * tp;                                      // |exp(.)|^2 t_pro  (:100)
-  if (acc > uu) {                                                // :18-25
-#pragma unroll
-    for (int c = 0; c < 3; ++c) pos[(size_t)b * 3 * N + 3 * i + c] += gmove[c];
-    if (accept_count) atomicAdd(&accept_count[b], 1);
+    for (int c = 0; c < 3; ++c) pos[(size_t)b * 3 * N + 3 * i + c] = xn[c];
+    if (a.count) atomicAdd(&a.count[b], 1);
   }
 }
 
@@ -304,17 +277,13 @@ static void moved_impl(int dtype, const KArgs& ka, hipStream_t s) {
 }
 
 template <int N, int A>
-static void accept_impl(int dtype, void* pos, const void* grad, const void* gown, const void* lp, const void* lpn,
-                        const void* g1, const void* g2, const void* u, const double* te, int B, double tstep,
-                        int32_t* acc, hipStream_t s) {
-  const int nt = B * N;
-  const int nb = (nt + 255) / 256;
+static void accept_impl(int dtype, void* pos, const AccArgs& a, int B, hipStream_t s) {
+  const int nb = (B * N + 255) / 256;
   if (dtype == AIQMC_F32)
-    k_accept<float, N><<<dim3(nb), dim3(256), 0, s>>>((float*)pos, (const float*)grad, (const float*)gown, (const float*)lp, (const float*)lpn, (const float*)g1, (const float*)g2, (const float*)u, te, B, tstep, acc);
+    k_accept<float, N><<<dim3(nb), dim3(256), 0, s>>>((float*)pos, a, B);
   else
-    k_accept<double, N><<<dim3(nb), dim3(256), 0, s>>>((double*)pos, (const double*)grad, (const double*)gown, (const double*)lp, (const double*)lpn, (const double*)g1, (const double*)g2, (const double*)u, te, B, tstep, acc);
+    k_accept<double, N><<<dim3(nb), dim3(256), 0, s>>>((double*)pos, a, B);
 }
-
 
 // per-walker parameter gradients in the kernel layout: out [nconf][Lay::total]
 template <int N, int A>

@@ -33,6 +33,61 @@ constexpr int MODE_GRAD = 1;
 constexpr int MODE_LAP = 2;
 constexpr int MODE_GRAD_FWD = 3;   // forward-mode gradient (diagnostics / cross-check)
 
+// Metropolis acceptance of one sweep (VMCmcstep.py:80-106), consumed by k_accept or, fused, by
+// the next sweep's walker launch (lpn != nullptr): the walkers' gradients, log|psi| and limdrift
+// factors at the start of that sweep, the proposals' log|psi| and own-electron gradients, and
+// the sweep's draws.
+struct AccArgs {
+  const void* grad;       // [B][3N]
+  const void* lp;         // [B]
+  const void* lpn;        // [B][N]
+  const void* gown;       // [B][N][3]
+  const void* gauss1;     // [B][3N]
+  const void* gauss2;     // [B][N][3]
+  const void* u;          // [B][N]
+  const double* taueff;   // [2]
+  double tstep;
+  int32_t* count;         // [B] accepted moves (optional)
+};
+
+// Electron i of walker b: t_pro (sum over xyz, Q6), acceptance |exp(lp_i - lp)|^2 t_pro > u.
+// Returns the electron's position after the step in xn (moved or not); pos itself is not written.
+template <typename T, int N>
+__device__ __forceinline__ bool accept_one(const AccArgs& a, const T* __restrict__ pos, int b, int i, T xn[3]) {
+  const T tstep = (T)a.tstep;
+  const T sq = sqrt(tstep);
+  const T te1 = (T)a.taueff[0], te2 = (T)a.taueff[1];
+  const T* grad = (const T*)a.grad;
+  const T* gown = (const T*)a.gown;
+  const T* g1 = (const T*)a.gauss1;
+  const T* g2 = (const T*)a.gauss2;
+  T z1[3], z2[3], x[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    z1[c] = g1[(size_t)b * 3 * N + 3 * i + c];
+    z2[c] = g2[((size_t)b * N + i) * 3 + c];
+    x[c] = pos[(size_t)b * 3 * N + 3 * i + c];
+  }
+  const T uu = ((const T*)a.u)[(size_t)b * N + i];
+  T gmove[3];
+  T tp = T(0);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const T ge = grad[(size_t)b * 3 * N + 3 * i + c] * te1;      // grad_eff  (:60)
+    gmove[c] = ge * tstep + sq * z1[c];                          // g         (:62)
+    const T gn = gown[((size_t)b * N + i) * 3 + c] * te2;        // grad_new_eff (:80)
+    const T w = sq * z2[c];                                      // gauss2    (:83)
+    const T fw = w * w;
+    const T bwv = w + (ge + gn) * tstep;
+    tp += exp((fw - bwv * bwv) / (T(2) * tstep));                // :84-94
+  }
+  const T e = exp(((const T*)a.lpn)[(size_t)b * N + i] - ((const T*)a.lp)[b]);
+  const bool acc = e * e * tp > uu;                              // |exp(.)|^2 t_pro > u  (:100, :18-25)
+#pragma unroll
+  for (int c = 0; c < 3; ++c) xn[c] = acc ? x[c] + gmove[c] : x[c];
+  return acc;
+}
+
 struct KArgs {
   int nconf;
   int nup;
@@ -62,6 +117,9 @@ struct KArgs {
   // (one launch fewer per sweep).  (Fusing the limdrift reduction the same way, by the last wave
   // to finish, was measured 3.5x slower: every wave's device-scope fence writes back its L2.)
   void *dg1, *dg2, *du;
+  // walker launch of a Metropolis sweep: acc.lpn != nullptr: first apply the PREVIOUS sweep's
+  // acceptance to walker conf (fused k_accept; one launch fewer per sweep)
+  AccArgs acc;
   // Metropolis caches (walker_rev.h WCache / ECache); nullptr outside aiqmc_mc_step
   void* wcache;
   void* ecache;
@@ -275,9 +333,10 @@ __device__ __forceinline__ void h_layer(cptr<T> P, const T* xs, T* hb, const PJ<
 }
 
 template <typename T, int N, int A, int MODE>
-// Diagnostics-only kernels (forward-mode gradient and Laplacian): one wave per SIMD, so that
-// register overflow goes to the AGPR half of the register file instead of scratch.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_walker(KArgs ka) {
+// Diagnostics-only kernels (forward-mode gradient and Laplacian).  The fp64 Laplacian
+// instantiations use 256 VGPRs + 256 AGPRs and spill to scratch (N = 10: 1,980 B/lane, all
+// constant-offset spill slots; DESIGN.md "GPU fault audit").
+__global__ __launch_bounds__(64) void k_walker(KArgs ka) {
   constexpr bool LAP = (MODE == MODE_LAP);
   using Ly = Lay<N, A>;
   using SM = Smem<T, N, LAP>;

@@ -564,7 +564,7 @@ __global__ __launch_bounds__(256) void k_grad_canon(const T* __restrict__ G, int
   if (m_ >= 0) {
     v = g[m_];
   } else if (m_ <= -2) {
-    const int mc = -2 - m_, m = mc / N, c = mc - m * N;
+    const int mc = -2 - m_, m = mc / N;
     T dot = T(0);
     for (int cc = 0; cc < N; ++cc) dot += what[m * N + cc] * g[wy_off + m * N + cc];
     v = (g[wy_off + mc] - what[mc] * dot) / (T)wnorm[m];

@@ -274,7 +274,20 @@ k_walker_rev(KArgs ka) {
     pb = conf / mper;
     pi = (conf - pb * mper) / mdiv;
   }
-  if (lane < 3 * N) {
+  if (!PREP && !ka.proposal && ka.acc.lpn) {
+    // the previous sweep's acceptance of this walker's N proposals (k_accept's arithmetic)
+    if (lane < N) {
+      T xn[3];
+      const bool acc = accept_one<T, N>(ka.acc, (const T*)ka.pos, conf, lane, xn);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) xs[3 * lane + c] = xn[c];
+      if (acc) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) ((T*)ka.pos)[(size_t)conf * 3 * N + 3 * lane + c] = xn[c];
+        if (ka.acc.count) atomicAdd(&ka.acc.count[conf], 1);
+      }
+    }
+  } else if (lane < 3 * N) {
     T x = ((const T*)ka.pos)[(size_t)pb * 3 * N + lane];
     if (ka.proposal && lane / 3 == pi) {
       sm[SM::R + (lane - 3 * pi)] = x;                       // old position of the moved electron
@@ -898,40 +911,29 @@ k_walker_rev(KArgs ka) {
     return;
   }
 
+  // electron-local Jacobians of this lane's (electron, direction) for B4, fetched ahead of B3:
+  // from the walker cache, or the moved electron's entry of this proposal
+  const int c4 = lc < 3 ? lc : 0;
+  T lv[N + D0];
+  {
+    const bool mov = reuse && le == pi;
+    const T* la = mov ? Eq + EC::yd + c4 * N : Wc + WC::loc + (lane < 48 ? lane : 47);
+    const T* lb = mov ? Eq + EC::hd + c4 * D0 : Wc + WC::loc + N * 48 + (lane < 48 ? lane : 47);
+    const int st = mov ? 1 : 48;
+#pragma unroll
+    for (int m = 0; m < N; ++m) lv[m] = la[m * st];
+#pragma unroll
+    for (int m = 0; m < D0; ++m) lv[N + m] = lb[m * st];
+  }
   AQ_PH(6);
   // ------------------------------------------------------------------ B3 pair adjoints d(logpsi)/d(x_i - x_k)
   T* dbar = sm + SM::dbar;
   // Proposals from the walker cache: the 2(N-1) pairs of the moved electron pi come first
   // (iteration 0) and recompute their forward values; every other pair takes t1, t2
   // from walker pb's cache, so iterations >= 1 skip the forward recompute.
-  for (int it = lane; it < (AQ_ABL(32) ? 0 : N * (N - 1)); it += 64) {
-    int k, i;
-    bool fresh = true;
-    if (reuse) {
-      constexpr int M = 2 * (N - 1);
-      if (it < M) {
-        const int j = it < N - 1 ? it : it - (N - 1);
-        const int o = j + (j >= pi ? 1 : 0);
-        k = it < N - 1 ? pi : o;
-        i = it < N - 1 ? o : pi;
-      } else {
-        if constexpr (N > 2) {
-          const int u = it - M;
-          const int kk = u / (N - 2);
-          const int jj = u - kk * (N - 2);
-          const int ii = jj + (jj >= kk ? 1 : 0);
-          k = kk + (kk >= pi ? 1 : 0);
-          i = ii + (ii >= pi ? 1 : 0);
-          fresh = false;
-        } else {
-          k = i = 0;
-        }
-      }
-    } else {
-      k = it / (N - 1);
-      const int jj = it - k * (N - 1);
-      i = jj + (jj >= k ? 1 : 0);
-    }
+  // one ordered pair (k, i): forward values (fresh) or the cached t1, t2 of walker pb, then the
+  // adjoints back through the two double layers to d = x_i - x_k
+  auto pair_adjoint = [&](int k, int i, bool fresh, const T* tcache) {
     const int G = k >= nup ? 1 : 0;
     T d[3];
 #pragma unroll
@@ -958,14 +960,11 @@ k_walker_rev(KArgs ka) {
         t2[o] = f_tanh(s);
       }
     } else {
-      const T* tp = Wc + WC::pt + (k * N + i) * 8;
 #pragma unroll
       for (int o = 0; o < 4; ++o) {
-        t1[o] = tp[o];
-        t2[o] = tp[4 + o];
+        t1[o] = tcache[o];
+        t2[o] = tcache[4 + o];
       }
-#pragma unroll
-      for (int o = 0; o < 4; ++o) p1[o] = (p0[o] + t1[o]) * RSQ2;
     }
     // adjoints: output of layer l feeds g2[l][G][i] with weight 1/|G|
     T pb2[4], pb1[4], pb0[4];
@@ -1001,24 +1000,58 @@ k_walker_rev(KArgs ka) {
     const T ir = f_rcp(r);
 #pragma unroll
     for (int c = 0; c < 3; ++c) dbar[(k * N + i) * 3 + c] = pb0[1 + c] + rb * d[c] * ir;
+  };
+  constexpr int NPR = N * (N - 1);
+  if (reuse && !AQ_ABL(32)) {
+    // Proposals: iteration u of lane l is pair index it = l + 64 u.  The 2(N-1) pairs of the
+    // moved electron pi (it < M, all in iteration 0) recompute their forward values; every
+    // other pair takes t1, t2 from walker pb's cache.  All cached loads of the lane are issued
+    // before the first pair is processed, so their latency overlaps the fresh pairs' tanh's
+    // and the earlier iterations (instead of one exposed cache round trip per iteration).
+    constexpr int M = 2 * (N - 1);
+    constexpr int NIT = (NPR + 63) / 64;
+    T tc[NIT][8];
+    int pk[NIT], pi2[NIT];
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {
+      const int it = lane + 64 * u;
+      int k = 0, i = 0;
+      if (it < M) {
+        const int j = it < N - 1 ? it : it - (N - 1);
+        const int o = j + (j >= pi ? 1 : 0);
+        k = it < N - 1 ? pi : o;
+        i = it < N - 1 ? o : pi;
+      } else if constexpr (N > 2) {
+        const int uu = (it < NPR ? it : NPR - 1) - M;
+        const int kk = uu / (N - 2);
+        const int jj = uu - kk * (N - 2);
+        const int ii = jj + (jj >= kk ? 1 : 0);
+        k = kk + (kk >= pi ? 1 : 0);
+        i = ii + (ii >= pi ? 1 : 0);
+      }
+      pk[u] = k;
+      pi2[u] = i;
+      if (u > 0 || it >= M) {
+        const T* tp = Wc + WC::pt + (k * N + i) * 8;
+#pragma unroll
+        for (int o = 0; o < 8; ++o) tc[u][o] = tp[o];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {
+      const int it = lane + 64 * u;
+      if (it < NPR) pair_adjoint(pk[u], pi2[u], u == 0 && it < M, tc[u]);
+    }
+  } else if (!reuse) {
+    for (int it = lane; it < NPR; it += 64) {
+      const int k = it / (N - 1);
+      const int jj = it - k * (N - 1);
+      pair_adjoint(k, jj + (jj >= k ? 1 : 0), true, nullptr);
+    }
   }
   __syncthreads();
 
   AQ_PH(7);
-  // electron-local Jacobians of this lane's (electron, direction) for B4, fetched ahead of B3:
-  // from the walker cache, or the moved electron's entry of this proposal
-  const int c4 = lc < 3 ? lc : 0;
-  T lv[N + D0];
-  {
-    const bool mov = reuse && le == pi;
-    const T* la = mov ? Eq + EC::yd + c4 * N : Wc + WC::loc + (lane < 48 ? lane : 47);
-    const T* lb = mov ? Eq + EC::hd + c4 * D0 : Wc + WC::loc + N * 48 + (lane < 48 ? lane : 47);
-    const int st = mov ? 1 : 48;
-#pragma unroll
-    for (int m = 0; m < N; ++m) lv[m] = la[m * st];
-#pragma unroll
-    for (int m = 0; m < D0; ++m) lv[N + m] = lb[m * st];
-  }
   // ------------------------------------------------------------------ B4 gradient per direction lane (c, e)
   T g = jd1;
   if (!AQ_ABL(64)) {

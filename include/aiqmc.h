@@ -251,6 +251,11 @@ int aiqmc_debug_local_energy_forward(aiqmc_ctx* ctx, const void* pos, int32_t B,
  * proposal from scratch; both must agree to rounding. */
 int aiqmc_debug_set_proposal_reuse(aiqmc_ctx* ctx, int32_t on);
 
+/* Diagnostics: aiqmc_mc_step applies the acceptance of every sweep but the last inside the
+ * next sweep's walker launch (default, on = 1); on = 0 runs a separate acceptance launch per
+ * sweep.  Both are bitwise identical (same arithmetic, same order). */
+int aiqmc_debug_set_fuse_accept(aiqmc_ctx* ctx, int32_t on);
+
 /* Development builds (-DAQ_ABLATE) only: skip proposal-kernel phases (bit mask, walker_rev.h) to
  * time their marginal cost; results are meaningless.  No effect in product builds. */
 int aiqmc_debug_set_ablate(aiqmc_ctx* ctx, int32_t mask);

@@ -71,6 +71,8 @@ def test_float32_matches_float64_4096():
     np.testing.assert_allclose(l32, l64, rtol=1e-4, atol=1e-3)
     e64, e32 = e64.cpu().numpy(), e32.double().cpu().numpy()
     rel = np.abs(e32 - e64) / (np.abs(e64) + 1.0)
+    print("fp32 vs fp64 E_L, relative: median", np.median(rel), "p99", np.quantile(rel, 0.99),
+          "p99.9", np.quantile(rel, 0.999), "max", rel.max(), "frac > 1e-3", np.mean(rel > 1e-3))
     # fp32 forward Laplacian: median relative error ~1e-6, worst case near nodes larger
     assert np.median(rel) < 1e-4, np.median(rel)
     assert np.mean(rel < 1e-2) > 0.99
@@ -138,6 +140,33 @@ def test_proposal_reuse_matches_recompute(name):
     torch.cuda.synchronize()
     assert torch.equal(acc_a, acc_b)
     assert torch.allclose(a, b, rtol=0, atol=1e-11), float((a - b).abs().max())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("draws", ["philox", "host"])
+def test_fused_acceptance_is_bitwise_identical(dtype, draws):
+    """mc_step applies each sweep's acceptance inside the next sweep's walker launch (the last
+    sweep keeps its own launch); the separate-launch path must give the same bits: positions
+    and accepted-move counts."""
+    s, ctx = _ctx("N2", dtype)
+    B, NS, N = 4096, 4, s.nelectrons
+    x0 = torch.tensor(_walkers(s, B, seed=12), dtype=dtype, device="cuda")
+    kw = dict(seed=2, offset=3)
+    if draws == "host":
+        g = torch.Generator().manual_seed(0)
+        kw = dict(gauss1=torch.randn(NS, B, 3 * N, generator=g, dtype=torch.float64),
+                  gauss2=torch.randn(NS, B, N, 3, generator=g, dtype=torch.float64),
+                  u=torch.rand(NS, B, N, generator=g, dtype=torch.float64))
+    a = x0.clone().contiguous()
+    b = x0.clone().contiguous()
+    acc_a = ctx.mc_step(a, NS, 0.05, count_accepts=True, **kw)
+    ctx.set_fuse_accept(False)
+    acc_b = ctx.mc_step(b, NS, 0.05, count_accepts=True, **kw)
+    ctx.set_fuse_accept(True)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert torch.equal(acc_a, acc_b)
+    assert int(acc_a.sum()) > 0 and not torch.equal(a, x0)
 
 
 def test_proposal_reuse_matches_recompute_f32_4096():

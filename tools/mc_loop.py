@@ -13,6 +13,8 @@ B = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
 s = systems.make_system(name)
 ctx = s.context(dtype=torch.float32)
 ctx.set_params(flatten_params(s.make_network().init(1)))
+if os.environ.get("AIQMC_NOFUSE"):
+    ctx.set_fuse_accept(False)
 pos = init_electrons(1000, None, s.atoms, s.charges, s.spins, B, 1.0)[0].to("cuda", torch.float32).contiguous()
 ctx.mc_step(pos, 10, 0.05, seed=1, offset=0)
 ctx.local_energy(pos)
