@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_debug_set_proposal_reuse", "aiqmc_debug_phase_cycles", "aiqmc_debug_local_energy_forward",
     "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
     "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves", "aiqmc_phase_param_grad",
-    "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals", "aiqmc_debug_set_ablate", "aiqmc_debug_set_fuse_accept",
+    "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals", "aiqmc_debug_set_ablate", "aiqmc_debug_set_fuse_accept", "aiqmc_debug_set_lap_waves",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -111,6 +111,8 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_debug_set_ablate.restype = ctypes.c_int
     lib.aiqmc_debug_set_fuse_accept.argtypes = [vp, i32]
     lib.aiqmc_debug_set_fuse_accept.restype = ctypes.c_int
+    lib.aiqmc_debug_set_lap_waves.argtypes = [vp, i32]
+    lib.aiqmc_debug_set_lap_waves.restype = ctypes.c_int
     lib.aiqmc_debug_set_proposal_reuse.argtypes = [vp, i32]
     lib.aiqmc_debug_set_proposal_reuse.restype = ctypes.c_int
     lib.aiqmc_debug_phase_cycles.argtypes = [vp, vp]
@@ -292,6 +294,10 @@ class Context:
         check(self._lib.aiqmc_debug_logpsi_grad_forward(self._h, _ptr(p), B, _ptr(logabs), _ptr(grad),
                                                         _stream(self.device)), "aiqmc_debug_logpsi_grad_forward")
         return logabs, grad
+
+    def set_lap_waves(self, waves: int):
+        """Waves per walker of the local energy's first-derivative pass (0 = by batch size)."""
+        check(self._lib.aiqmc_debug_set_lap_waves(self._h, int(waves)), "aiqmc_debug_set_lap_waves")
 
     def set_fuse_accept(self, on: bool):
         """Diagnostics: fused (default) or separate per-sweep acceptance launch in mc_step."""

@@ -415,6 +415,8 @@ int aiqmc_create(const aiqmc_cfg* cfg, aiqmc_ctx** out) {
   if (e != hipSuccess) { delete c; return fail(AIQMC_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(e)); }
   int rc = ops.set_lds();
   if (rc) { delete c; return rc; }
+  if (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->ncu <= 0)
+    c->ncu = 256;
   const size_t s = c->dtype == AIQMC_F32 ? 4 : 8;
   e = hipMalloc(&c->d_prm, (size_t)c->nkern * s);
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_rowsrc, 16 * sizeof(int));
@@ -611,7 +613,14 @@ int aiqmc_local_energy(aiqmc_ctx* c, const void* pos, int32_t B, void* e_l, void
   k2.el = e_l;
   k2.grad = grad;
   k2.lapcache = c->d_lc;
-  timed(c, 2, (hipStream_t)stream, [&] { ops.lap(c->dtype, k1, k2, B, (hipStream_t)stream); });
+  // waves per walker of the first-derivative pass: the fewest of 1, 2, 4 that give >= 2 waves per
+  // SIMD (8 per CU); small per-GPU batches (strong scaling) split each walker over more waves
+  int lw = c->lap_waves;
+  if (lw <= 0) {
+    const int64_t want = 8 * (int64_t)c->ncu;
+    lw = (int64_t)B >= want ? 1 : ((int64_t)B * 2 >= want ? 2 : 4);
+  }
+  timed(c, 2, (hipStream_t)stream, [&] { ops.lap(c->dtype, k1, k2, B, lw, (hipStream_t)stream); });
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
 }
@@ -1224,6 +1233,13 @@ int aiqmc_debug_logpsi_grad_forward(aiqmc_ctx* c, const void* pos, int32_t B, vo
 int aiqmc_debug_set_ablate(aiqmc_ctx* c, int32_t mask) {
   if (!c) return fail(AIQMC_EINVAL, "null context");
   c->ablate = mask;
+  return AIQMC_OK;
+}
+
+int aiqmc_debug_set_lap_waves(aiqmc_ctx* c, int32_t waves) {
+  if (!c) return fail(AIQMC_EINVAL, "null context");
+  if (waves != 0 && waves != 1 && waves != 2 && waves != 4) return fail(AIQMC_EINVAL, "lap waves must be 0, 1, 2 or 4");
+  c->lap_waves = waves;
   return AIQMC_OK;
 }
 

@@ -42,8 +42,10 @@ struct aiqmc_ctx {
   void* d_lc = nullptr;                                     // local-energy LapCache [B][lcache_n]
   int lc_B = 0, lc_n = 0;
   bool reuse = true;                                        // proposals reuse the walker's cached stage
-  int ablate = 0;
-  int fuse_accept = 1;   // aiqmc_debug_set_fuse_accept: acceptance fused into the next walker launch                                           // AQ_ABLATE development builds (walker_rev.h)
+  int ablate = 0;                                           // AQ_ABLATE development builds (walker_rev.h)
+  int fuse_accept = 1;                                      // acceptance fused into the next walker launch
+  int lap_waves = 0;                                        // waves per walker of k_walker_lap (0: by batch)
+  int ncu = 256;                                            // compute units of the device
   double* d_taueff = nullptr;
   int64_t ws_bytes = 0;
   // pseudopotential (aiqmc_set_ecp / aiqmc_local_energy_ecp, ecp.h)
@@ -74,7 +76,7 @@ struct ShapeOps {
   void (*accept)(int dtype, void* pos, const aq::AccArgs& a, int B, hipStream_t s);
   void (*moved)(int dtype, const KArgs& ka, hipStream_t s);   // k_moved_electron over ka.nconf proposals
   // local energy: adjoint pass (k1) + first-derivative pass (k2), walker_lap.h
-  void (*lap)(int dtype, const KArgs& k1, const KArgs& k2, int nconf, hipStream_t s);
+  void (*lap)(int dtype, const KArgs& k1, const KArgs& k2, int nconf, int waves, hipStream_t s);
   void (*phase_read)(unsigned long long* out32);               // AQ_PHASE_PROF builds only
   int wcache_n, ecache_n;                                      // cache entries per walker / per proposal
   int lcache_n;                                                // LapCache entries per walker

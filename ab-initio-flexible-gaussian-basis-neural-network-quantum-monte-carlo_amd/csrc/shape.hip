@@ -237,7 +237,7 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
   if (dtype == AIQMC_F32) {
     if (mode == MODE_LAP)
       k_walker<float, N, A, MODE_LAP><<<dim3(nconf), dim3(64), Smem<float, N, true>::bytes, s>>>(ka);
-    else if (mode == MODE_GRAD && ka.proposal)
+    else if (mode == MODE_GRAD && ka.proposal && ka.ecache)   // proposals from the walker cache
       k_walker_rev<float, N, A, false, true><<<dim3(nconf), dim3(64), SmemRev<float, N, A>::bytes, s>>>(ka);
     else if (mode == MODE_GRAD)
       k_walker_rev<float, N, A><<<dim3(nconf), dim3(64), SmemRev<float, N, A>::bytes, s>>>(ka);
@@ -246,7 +246,7 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
   } else {
     if (mode == MODE_LAP)
       k_walker<double, N, A, MODE_LAP><<<dim3(nconf), dim3(64), Smem<double, N, true>::bytes, s>>>(ka);
-    else if (mode == MODE_GRAD && ka.proposal)
+    else if (mode == MODE_GRAD && ka.proposal && ka.ecache)   // proposals from the walker cache
       k_walker_rev<double, N, A, false, true><<<dim3(nconf), dim3(64), SmemRev<double, N, A>::bytes, s>>>(ka);
     else if (mode == MODE_GRAD)
       k_walker_rev<double, N, A><<<dim3(nconf), dim3(64), SmemRev<double, N, A>::bytes, s>>>(ka);
@@ -257,13 +257,20 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
 
 // Local energy: adjoint pass (k_walker_rev<PREP>) then first-derivative pass (k_walker_lap).
 template <int N, int A>
-static void lap_impl(int dtype, const KArgs& k1, const KArgs& k2, int nconf, hipStream_t s) {
+static void lap_impl(int dtype, const KArgs& k1, const KArgs& k2, int nconf, int waves, hipStream_t s) {
+  const dim3 wg(64 * waves);   // waves per walker in the first-derivative pass: 1, 2 or 4
   if (dtype == AIQMC_F32) {
     k_walker_rev<float, N, A, true><<<dim3(nconf), dim3(64), SmemRev<float, N, A>::bytes, s>>>(k1);
-    k_walker_lap<float, N, A><<<dim3(nconf), dim3(64), SmemLap<float, N, A>::bytes, s>>>(k2);
+    if (waves == 1)
+      k_walker_lap<float, N, A, 1><<<dim3(nconf), wg, SmemLap<float, N, A>::bytes, s>>>(k2);
+    else
+      k_walker_lap<float, N, A, 4><<<dim3(nconf), wg, SmemLap<float, N, A>::bytes, s>>>(k2);
   } else {
     k_walker_rev<double, N, A, true><<<dim3(nconf), dim3(64), SmemRev<double, N, A>::bytes, s>>>(k1);
-    k_walker_lap<double, N, A><<<dim3(nconf), dim3(64), SmemLap<double, N, A>::bytes, s>>>(k2);
+    if (waves == 1)
+      k_walker_lap<double, N, A, 1><<<dim3(nconf), wg, SmemLap<double, N, A>::bytes, s>>>(k2);
+    else
+      k_walker_lap<double, N, A, 4><<<dim3(nconf), wg, SmemLap<double, N, A>::bytes, s>>>(k2);
   }
 }
 

@@ -41,6 +41,7 @@ struct SmemLap {
   static constexpr int yd = hb + N * NH * 49;                // [2][N][49] dYt/dx, d2Yt/dx2 of row le
   static constexpr int end = yd + 2 * N * 49;
   static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
+  static_assert(end - ly >= 3 * 3 * 64, "multi-wave partial sums (W <= 4) must fit behind ly");
 };
 
 // One h-stream layer (nn.py:280-311) in first derivatives, column loop over electrons i.
@@ -49,7 +50,7 @@ struct SmemLap {
 template <typename T, int N, int A, int L>
 __device__ __forceinline__ void lap_layer(cptr<T> P, const T* xs, T* hb, const T* ly, const PJ<T>* hf, int lane,
                                           int lc, int er, int le, bool val, bool dir, bool live, int nup, T& jd1,
-                                          T& jd2, T& vv, T& acc) {
+                                          T& jd2, T& vv, T& acc, int wv, int W) {
   using Ly = Lay<N, A>;
   using LC = LapCache<N, A>;
   constexpr int DIN = (L == 0) ? 4 * A : NH;
@@ -83,10 +84,12 @@ __device__ __forceinline__ void lap_layer(cptr<T> P, const T* xs, T* hb, const T
       g1[0][m] *= ginv[0];
       g1[1][m] *= ginv[1];
     }
+    if (W > 1) __syncthreads();   // every wave has read layer L's dh/dx before any overwrites it
   }
 
+  // multi-wave mode: wave wv of the walker's workgroup takes columns i = wv, wv + W, ...
 #pragma unroll 1
-  for (int i = 0; i < N; ++i) {
+  for (int i = wv; i < N; i += W) {
     const bool diag = (le == i);
     T d[3];
 #pragma unroll
@@ -193,8 +196,15 @@ __device__ __forceinline__ void lap_layer(cptr<T> P, const T* xs, T* hb, const T
   }
 }
 
-template <typename T, int N, int A>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_walker_lap(KArgs ka) {
+// One workgroup of W = blockDim.x / 64 waves per walker (W = 1, 2 or 4; aiqmc.hip picks W so
+// that small batches still fill the chip): every wave evaluates the per-electron stage of all
+// electrons (its lanes are the 3N directions), the h-stream columns i = wv, wv + W, ... of each
+// layer and the determinant rows r of its share; per-lane partial sums are combined by wave 0 in
+// fixed order.  W = 1 is the single-wave kernel (same arithmetic, same order).
+// WMAX: the instantiation's largest W (1: the single-wave kernel, compiled as before for 64
+// threads; 4: W = 2 or 4 at run time).
+template <typename T, int N, int A, int WMAX>
+__global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) void k_walker_lap(KArgs ka) {
   using Ly = Lay<N, A>;
   using LC = LapCache<N, A>;
   using SM = SmemLap<T, N, A>;
@@ -207,7 +217,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   T* hb = sm + SM::hb;
 
   const int conf = xcd_major(blockIdx.x, gridDim.x);   // same walker -> XCD map as the adjoint pass
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wv = WMAX == 1 ? 0 : (int)(threadIdx.x >> 6), W = WMAX == 1 ? 1 : (int)(blockDim.x >> 6);
+  const bool w0 = wv == 0;
   const int lc = lane >> 4;
   const int er = lane & 15;
   const int le = er < N ? er : N - 1;
@@ -219,20 +231,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   T* yd = sm + SM::yd;
   const cptr<T> Lc = param_ptr<T>((const T*)ka.lapcache + (size_t)conf * LC::size);
 
-  if (lane < 3 * N) xs[lane] = ((const T*)ka.pos)[(size_t)conf * 3 * N + lane];
+  if (w0 && lane < 3 * N) xs[lane] = ((const T*)ka.pos)[(size_t)conf * 3 * N + lane];
   T h0b[D0];
 #pragma unroll
   for (int m = 0; m < D0; ++m) h0b[m] = Lc[LC::h0b + le * D0 + m];
-  for (int idx = lane; idx < LC::layer_n; idx += 64) ly[idx] = Lc[idx];
+  for (int idx = threadIdx.x; idx < LC::layer_n; idx += blockDim.x) ly[idx] = Lc[idx];
   __syncthreads();
 
   // ------------------------------------------------------------------ per-electron stage (electron.h)
   ElecOut<T, A> eo;
   electron_stage<T, N, A>(P, xs + le * 3, le, lc, eo);
-  T vv = (val && live) ? eo.ven : T(0);
+  T vv = (w0 && val && live) ? eo.ven : T(0);
   T acc = T(0);   // curvature sources, per direction lane
 #pragma unroll
   for (int m = 0; m < D0; ++m) acc += h0b[m] * eo.hf[m].d2;   // ae features as leaves
+  if (!w0) acc = T(0);
   // Yt row of electron le, first and second derivatives (nn.py:449-452, 479-485) -> LDS
 #pragma unroll
   for (int col = 0; col < N; ++col) {
@@ -240,22 +253,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 #pragma unroll
     for (int m = 1; m < NYW; ++m) s = s + P[Ly::wy + m * N + col] * eo.yst[m];
     const PJ<T> yt = eo.env * s;
-    yd[col * 49 + l49] = yt.d1;
-    yd[(N + col) * 49 + l49] = yt.d2;
+    if (w0) {
+      yd[col * 49 + l49] = yt.d1;
+      yd[(N + col) * 49 + l49] = yt.d2;
+    }
   }
-  T jd1 = dir ? eo.jae.d1 : T(0);
-  T jd2 = dir ? eo.jae.d2 : T(0);
+  T jd1 = (w0 && dir) ? eo.jae.d1 : T(0);
+  T jd2 = (w0 && dir) ? eo.jae.d2 : T(0);
 
   // ------------------------------------------------------------------ h stream, first derivatives
-  lap_layer<T, N, A, 0>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc);
+  lap_layer<T, N, A, 0>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W);
   __syncthreads();
-  for (int idx = lane; idx < LC::layer_n; idx += 64) ly[idx] = Lc[LC::layer_n + idx];
+  for (int idx = threadIdx.x; idx < LC::layer_n; idx += blockDim.x) ly[idx] = Lc[LC::layer_n + idx];
   __syncthreads();
-  lap_layer<T, N, A, 1>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc);
+  lap_layer<T, N, A, 1>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W);
   __syncthreads();
-  for (int idx = lane; idx < LC::layer_n; idx += 64) ly[idx] = Lc[2 * LC::layer_n + idx];
+  for (int idx = threadIdx.x; idx < LC::layer_n; idx += blockDim.x) ly[idx] = Lc[2 * LC::layer_n + idx];
   __syncthreads();
-  lap_layer<T, N, A, 2>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc);
+  lap_layer<T, N, A, 2>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W);
+  if (W > 1) __syncthreads();   // the determinant terms read every wave's columns of dh/dx
 
   // ------------------------------------------------------------------ determinant terms
   // (phases fenced so that the scheduler does not stretch their live ranges across each other)
@@ -301,16 +317,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     t2 += xr * br - xi * bi;
   }
   __builtin_amdgcn_sched_barrier(0);
-  // E3: gradient: sum_{r,f} U Re Q_f[r,r] + Re(w . b_e) + Jastrow
-  T g = jd1 + wbr;
+  // E3: gradient: sum_{r,f} U Re Q_f[r,r] + Re(w . b_e) + Jastrow  (rows r = wv, wv + W, ...)
+  T g = w0 ? jd1 + wbr : jd1;
 #pragma unroll 2
-  for (int r = 0; r < N; ++r)
+  for (int r = wv; r < N; r += W)
 #pragma unroll
     for (int f = 0; f < NH; ++f) g += UH(r, f) * Qs[((r * N + r) * NH + f) * 2];
   // E4: cross = Re sum_r z_r S_re (z = B^T w);  ss = Re sum_{r,s} S_rs S_sr,  S_rs = sum_f U_rf Q_f[r,s]
+  // (row r costs N - r: wave wv takes rows wv, 2W-1-wv, 2W+wv, ... so the shares balance)
   T cross = T(0), ss = T(0);
 #pragma unroll 1
-  for (int r = 0; r < N; ++r) {
+  for (int t = 0; t * W < N; ++t) {
+    const int r = t * W + ((t & 1) ? W - 1 - wv : wv);
+    if (r >= N) continue;
     T ur[NH];
 #pragma unroll
     for (int f = 0; f < NH; ++f) ur[f] = UH(r, f);
@@ -346,7 +365,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     }
   }
 #undef UH
-  const T lap = t2 - (ss + T(2) * cross + (wbr * wbr - wbi * wbi)) + jd2 + acc;
+  T lap = (w0 ? t2 : T(0)) - (ss + T(2) * cross + (w0 ? wbr * wbr - wbi * wbi : T(0))) + jd2 + acc;
+  if (W > 1) {
+    // partial sums of waves 1..W-1 -> wave 0, added in wave order (the ly block is free now)
+    __syncthreads();
+    if (!w0) {
+      T* red = ly + (wv - 1) * 3 * 64;   // spans ly, hb, yd: all read for the last time above
+      red[lane] = g;
+      red[64 + lane] = lap;
+      red[128 + lane] = vv;
+    }
+    __syncthreads();
+    if (!w0) return;
+    for (int k = 1; k < W; ++k) {
+      const T* red = ly + (k - 1) * 3 * 64;
+      g += red[lane];
+      lap += red[64 + lane];
+      vv += red[128 + lane];
+    }
+  }
 
   // ------------------------------------------------------------------ outputs
   const T gd = dir ? g : T(0);

@@ -47,7 +47,7 @@ static __device__ unsigned long long aq_phase_cycles[32];
 // Development builds (-DAQ_ABLATE): KArgs.ablate skips phases of the proposal path, so that the
 // marginal cost of each phase can be timed (results are garbage; never in a product build).
 #ifdef AQ_ABLATE
-#define AQ_ABL(b) (ka.proposal && (ka.ablate & (b)))
+#define AQ_ABL(b) (isprop && (ka.ablate & (b)))
 #else
 #define AQ_ABL(b) false
 #endif
@@ -250,6 +250,9 @@ k_walker_rev(KArgs ka) {
   T* sm = (T*)smem_raw;
   T* xs = sm + SM::xs;
 
+  // The PROP instantiation is launched only for proposals that read the walker cache (shape.hip
+  // routes reuse-off proposals to the general one), so there both path flags are compile-time.
+  const bool isprop = PROP ? true : (ka.proposal != 0);
   const int conf = xcd_major(blockIdx.x, gridDim.x);
   const int lane = threadIdx.x;
   const int lc = lane >> 4;
@@ -269,12 +272,12 @@ k_walker_rev(KArgs ka) {
 
   // ------------------------------------------------------------------ F0 positions (as k_walker)
   int pb = conf, pi = -1;
-  if (ka.proposal) {
+  if (isprop) {
     const int mper = ka.mper ? ka.mper : N, mdiv = ka.mdiv ? ka.mdiv : 1;
     pb = conf / mper;
     pi = (conf - pb * mper) / mdiv;
   }
-  if (!PREP && !ka.proposal && ka.acc.lpn) {
+  if (!PREP && !isprop && ka.acc.lpn) {
     // the previous sweep's acceptance of this walker's N proposals (k_accept's arithmetic)
     if (lane < N) {
       T xn[3];
@@ -289,7 +292,7 @@ k_walker_rev(KArgs ka) {
     }
   } else if (lane < 3 * N) {
     T x = ((const T*)ka.pos)[(size_t)pb * 3 * N + lane];
-    if (ka.proposal && lane / 3 == pi) {
+    if (isprop && lane / 3 == pi) {
       sm[SM::R + (lane - 3 * pi)] = x;                       // old position of the moved electron
       if (ka.xnew) {
         x = ((const T*)ka.xnew)[(size_t)conf * 3 + (lane - 3 * pi)];
@@ -308,7 +311,7 @@ k_walker_rev(KArgs ka) {
   // Walker cache: read (proposal with reuse: this proposal's walker pb) or written (by conf).
   using WC = WCache<N, A>;
   using EC = ECache<N, A>;
-  const bool reuse = !PREP && ka.proposal && ka.ecache != nullptr;
+    const bool reuse = !PREP && isprop && (PROP || ka.ecache != nullptr);
   T* Wc = (T*)ka.wcache + (size_t)(reuse ? pb : conf) * WC::size;
   T* Lw = PREP ? (T*)ka.lapcache + (size_t)conf * LCc::size : nullptr;
   const T* Eq = reuse ? (const T*)ka.ecache + (size_t)conf * EC::size : nullptr;
@@ -372,13 +375,13 @@ k_walker_rev(KArgs ka) {
     }
     jv = (val && live) ? eo.jae.v : T(0);
     jd1 = dir ? eo.jae.d1 : T(0);
-    if (!PREP && !ka.proposal) {
+    if (!PREP && !isprop) {
       if (val && live) Wc[WC::jaev + er] = eo.jae.v;
       if (lane < 48) Wc[WC::jaed + lane] = jd1;
     }
   }
   __syncthreads();
-  if (!PREP && !ka.proposal) {
+  if (!PREP && !isprop) {
     for (int idx = lane; idx < N * N; idx += 64) Wc[WC::yv + idx] = Yv[idx];
     for (int idx = lane; idx < N * D0; idx += 64) Wc[WC::h0 + idx] = sm[SM::hl + idx];
   }
@@ -476,7 +479,7 @@ k_walker_rev(KArgs ka) {
               for (int m = 0; m < 4; ++m) s += p[m] * dw[m * 4 + o];
               q[o] = f_tanh(s);
             }
-            if (!PREP && !ka.proposal && icol && !diag) {   // walker cache: t_{j+1} of pair (k, i)
+            if (!PREP && !isprop && icol && !diag) {   // walker cache: t_{j+1} of pair (k, i)
               T* tp = Wc + WC::pt + (k * N + ii) * 8 + j * 4;
 #pragma unroll
               for (int o = 0; o < 4; ++o) tp[o] = q[o];
@@ -504,7 +507,7 @@ k_walker_rev(KArgs ka) {
     }
   }
   __syncthreads();
-  if (!PREP && !ka.proposal) {
+  if (!PREP && !isprop) {
     for (int idx = lane; idx < 3 * 2 * N * 4; idx += 64) Wc[WC::g2 + idx] = g2[idx];
     const T je = wave_sum(jve);
     if (lane == 0) Wc[WC::jee] = je;
@@ -646,7 +649,7 @@ k_walker_rev(KArgs ka) {
       gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi);
     }
   } else {
-    gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi, (!PREP && !ka.proposal) ? Wc + WC::pv : nullptr);
+    gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi, (!PREP && !isprop) ? Wc + WC::pv : nullptr);
   }
   if constexpr (!PREP) {
     if (ka.value_only) {   // ECP quadrature configurations: log|psi| and phase only
@@ -1078,7 +1081,7 @@ k_walker_rev(KArgs ka) {
     if (ka.sumsq) ((T*)ka.sumsq)[conf] = sumsq;
   }
   if constexpr (!PREP) {
-    if (ka.dg1 && !ka.proposal && lane < N) {   // the sweep's draws of walker conf (k_draws)
+    if (ka.dg1 && !isprop && lane < N) {   // the sweep's draws of walker conf (k_draws)
       const uint32_t t = (uint32_t)(conf * N + lane);
       float a[3], b[3], c[4];
       philox_normal3f(ka.seed, ka.step, t, 0u, a);

@@ -258,7 +258,13 @@ def dmc_side_bench(dtype, device, walkers, steps):
     return {"config": "C atom ccECP DMC step: T-moves + drift-diffusion + 2x pp E_L + weights + comb, drop-in API",
             "walkers": walkers, "tstep": tstep, "ms_per_dmc_step": 1e3 * dt / steps,
             "walker_steps_per_s": walkers * steps / dt, "tmoves_ms": 1e3 * dtm / steps,
-            "mean_energy_re": float(eloc.real.mean()), "finite": bool(torch.isfinite(eloc.real).all())}
+            "mean_energy_re": float(eloc.real.mean()),
+            # random-init wavefunction: E_L has heavy tails near the nodes of psi, so the mean is
+            # carried by a few walkers; the quantiles show the bulk
+            "energy_re_quantiles": {q: float(v) for q, v in zip(
+                ("p01", "p10", "p50", "p90", "p99"),
+                torch.quantile(eloc.real.double().cpu(), torch.tensor([0.01, 0.1, 0.5, 0.9, 0.99], dtype=torch.float64)))},
+            "finite": bool(torch.isfinite(eloc.real).all())}
 
 
 def adam_side_bench(dtype, device, walkers, steps):

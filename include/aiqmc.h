@@ -251,6 +251,11 @@ int aiqmc_debug_local_energy_forward(aiqmc_ctx* ctx, const void* pos, int32_t B,
  * proposal from scratch; both must agree to rounding. */
 int aiqmc_debug_set_proposal_reuse(aiqmc_ctx* ctx, int32_t on);
 
+/* Waves per walker of the local energy's first-derivative pass (k_walker_lap): 1, 2 or 4, or
+ * 0 (default) = the fewest that give >= 2 waves per SIMD for the batch (small per-GPU batches
+ * under strong scaling split each walker over more waves).  Results agree to rounding. */
+int aiqmc_debug_set_lap_waves(aiqmc_ctx* ctx, int32_t waves);
+
 /* Diagnostics: aiqmc_mc_step applies the acceptance of every sweep but the last inside the
  * next sweep's walker launch (default, on = 1); on = 0 runs a separate acceptance launch per
  * sweep.  Both are bitwise identical (same arithmetic, same order). */

@@ -15,6 +15,10 @@ ctx = s.context(dtype=torch.float32)
 ctx.set_params(flatten_params(s.make_network().init(1)))
 if os.environ.get("AIQMC_NOFUSE"):
     ctx.set_fuse_accept(False)
+if os.environ.get("AIQMC_LAPW"):      # waves per walker of the local energy's second launch
+    ctx.set_lap_waves(int(os.environ["AIQMC_LAPW"]))
+if os.environ.get("AIQMC_NOREUSE"):   # every proposal from scratch (PMC comparison of the two paths)
+    ctx.set_proposal_reuse(False)
 pos = init_electrons(1000, None, s.atoms, s.charges, s.spins, B, 1.0)[0].to("cuda", torch.float32).contiguous()
 ctx.mc_step(pos, 10, 0.05, seed=1, offset=0)
 ctx.local_energy(pos)
