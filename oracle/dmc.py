@@ -262,3 +262,89 @@ def dmc_blocks(net, params, ecp, x0, e_l0, nblocks: int, iterations: int, tstep:
         trace["e_est"].append(e_est)
         trace["e_trial"].append(e_trial)
     return trace, x, weights
+
+
+def dmc_blocks_devices(net, params, ecp, x0, e_l0, nblocks: int, iterations: int, tstep: float, feedback: float,
+                       step_draws, block_draws, ndev: int):
+    """main_dmc.py:113-244 with the walkers split over `ndev` devices in contiguous blocks (the
+    pmapped driver, main_dmc.py:86-97): per device its own T-moves, drift-diffusion (tdamp is a
+    per-device ratio, drift_diffusion.py:21) and comb (branch.py under pmap, one uniform per
+    device); global over devices: esigma = jnp.std over every walker (:118), the comput_S energy
+    cut = ONE min over the stacked [ndev, B] |e_est - E_L| arrays and the branch cut (S_matrix.py
+    :10-12 on the gathered arrays), the block estimate (:190) and the e_trial feedback = log of
+    the mean over devices of the comb weights (:237).  block_draws(block) -> [(u_comb,
+    extra)] * ndev; step_draws(k) -> draws of all walkers (device d takes its rows)."""
+    B = x0.shape[0]
+    Bd = B // ndev
+    sl = [slice(d * Bd, (d + 1) * Bd) for d in range(ndev)]
+    x = np.asarray(x0, np.float64)
+    N = x.shape[1] // 3
+    e_trial = e_est = np.asarray(e_l0)
+    esigma = float(np.std(np.asarray(e_l0)))
+    branchcut = 10.0 * esigma
+    weights = np.ones(B)
+    energy_data = np.zeros((nblocks, iterations, B))
+    weights_data = np.zeros((nblocks, iterations, B))
+    trace = {"energy": [], "weights": [], "positions": [], "newinds": [], "comb_weight": [], "e_est": [],
+             "e_trial": []}
+    pick = lambda v, d: v[sl[d]] if np.ndim(v) else v
+    k = 0
+    from . import pphamiltonian as pp
+    for block in range(nblocks):
+        for t in range(iterations):
+            dr = step_draws(k)
+            k += 1
+            parts = []
+            for d in range(ndev):
+                dd = {key: np.asarray(v)[sl[d]] for key, v in dr.items()}
+                xd = torch.tensor(x[sl[d]])
+                pos_t = torch.stack([tmoves(net, params, ecp, xd[b], dd["rot_tm"][b], float(dd["u_sel"][b]),
+                                            dd["u_acc"][b], tstep)[0] for b in range(Bd)])
+                x_new, tdamp, go, gn = drift_diffusion(net, params, pos_t, torch.as_tensor(dd["gauss1"]),
+                                                       torch.as_tensor(dd["gauss2"]), torch.as_tensor(dd["u"]), tstep)
+                eo = pp.batch_local_energy_pp(net, params, ecp, xd, dd["rot_old"])[0].detach().numpy()
+                en = pp.batch_local_energy_pp(net, params, ecp, x_new, dd["rot_new"])[0].detach().numpy()
+                parts.append((x_new.numpy(), float(tdamp), go.numpy(), gn.numpy(), eo, en))
+            cut = {}
+            for which, col in (("old", 4), ("new", 5)):
+                m = min(float(np.min(np.abs(np.real(pick(e_est, d)) - np.real(parts[d][col])))) for d in range(ndev))
+                cut[which] = min(m, branchcut)
+            w_new = np.empty(B)
+            eloc = np.empty(B, complex)
+            xn = np.empty_like(x)
+            for d in range(ndev):
+                x_new, tdamp, go, gn, eo, en = parts[d]
+
+                def S(v2, el, c):
+                    v2 = np.sum(v2, axis=-1)
+                    el = np.real(el)
+                    e_cut = c * np.sign(np.real(pick(e_est, d)) - el)
+                    return np.real(pick(e_trial, d)) - np.real(pick(e_est, d)) + e_cut / (1 + (v2 * tstep / N) ** 2)
+                s_old = S(go ** 2, eo, cut["old"])
+                s_new = S(gn ** 2, en, cut["new"])
+                w_new[sl[d]] = update_weights(weights[sl[d]], tstep, tdamp, s_new, s_old)
+                eloc[sl[d]] = en
+                xn[sl[d]] = x_new
+            weights = w_new
+            x = xn
+            energy_data[block, t] = eloc.real
+            weights_data[block, t] = weights
+            trace["energy"].append(eloc)
+            trace["weights"].append(weights.copy())
+            trace["positions"].append(x.copy())
+        e_est = np.average(energy_data[:block + 1], weights=weights_data[:block + 1])
+        wns, inds = [], []
+        bd = block_draws(block)
+        for d in range(ndev):
+            u, extra = bd[d]
+            wn, newinds = branch(weights[sl[d]], u)
+            wns.append(wn)
+            inds.append(newinds)
+            x[sl[d]] = reindex(x[sl[d]], newinds, extra)
+            weights[sl[d]] = wn
+        e_trial = e_est - feedback * np.log(np.mean(wns)).real
+        trace["newinds"].append(np.stack(inds))
+        trace["comb_weight"].append(np.array(wns))
+        trace["e_est"].append(e_est)
+        trace["e_trial"].append(e_trial)
+    return trace, x, weights

@@ -8,6 +8,9 @@ T-move amplitudes are all negative: no electron moves); "attractive" (list_l = 1
 coefficients) makes the T-moves select and accept moves.
 Ne_dmc_ne_allelectron.npz: all-electron Ne (10 e-) through the same pp-only DMC step with zero
 ECP coefficients (what "Ne + DMC" maps to), B = 4, 1 block x 2 iterations.
+C_dmc_attractive_2dev.npz: the "attractive" table with the 8 walkers split over 2 devices
+(oracle.dmc.dmc_blocks_devices: per-device T-moves / drift-diffusion / comb, global cut, estimate
+and feedback), 2 blocks x 2 iterations; u_comb [2, 2], extra [2, 2, 4, 12] per (block, device).
 Arrays: params_flat, x0 [B,12], e_l0_re/_im [B] (pp energies of x0 with rot0), rot0;
 per step k (6): rot_tm, u_sel, u_acc, gauss1 [B,12], gauss2 [B,4,12], u [B,4], rot_old, rot_new;
 per block (2): u_comb, extra [B,12]; outputs: energy_re/_im [6,B], weights [6,B],
@@ -37,6 +40,43 @@ TABLES = {
     "attractive": pp.ECP([[1.0]], [[0.0]], [[1.0]], [[[2.0], [1.0]]], [[[-3.0], [-5.0]]], [[[0.7], [0.4]]], 1),
 }
 TSTEP, FEEDBACK = 0.05, 1.0
+
+
+def make_2dev(out_dir: str):
+    """The multi-device driver (main_dmc.py pmapped over 2 devices) on the attractive table."""
+    s = system.make_system("C_ecp")
+    N = s.nelectrons
+    B, NDEV, NBLOCKS, ITERS = 8, 2, 2, 2
+    rng = np.random.default_rng(54)
+    params = system.init_params(rng, s, randomize_aux=True)
+    x0 = system.init_electrons(rng, s.atoms, s.charges, B, 1.0)
+    rot0 = pp.haar_rotations(rng, B)
+    steps = []
+    for _ in range(NBLOCKS * ITERS):
+        steps.append(dict(rot_tm=pp.haar_rotations(rng, B), u_sel=rng.uniform(size=B) * 2e-3,
+                          u_acc=rng.uniform(size=(B, N)), gauss1=rng.standard_normal((B, 3 * N)),
+                          gauss2=rng.standard_normal((B, N, 3 * N)), u=rng.uniform(size=(B, N)),
+                          rot_old=pp.haar_rotations(rng, B), rot_new=pp.haar_rotations(rng, B)))
+    u_comb = rng.uniform(size=(NBLOCKS, NDEV))
+    extra = rng.uniform(size=(NBLOCKS, NDEV, B // NDEV, 3 * N))
+    net = network.Network(s)
+    pt = network.to_torch(params)
+    ecp = TABLES["attractive"]
+    e_l0 = pp.batch_local_energy_pp(net, pt, ecp, torch.tensor(x0), rot0)[0].detach().numpy()
+    trace, x, w = dmc.dmc_blocks_devices(net, pt, ecp, x0, e_l0, NBLOCKS, ITERS, TSTEP, FEEDBACK,
+                                         lambda k: steps[k],
+                                         lambda b: [(float(u_comb[b, d]), extra[b, d]) for d in range(NDEV)], NDEV)
+    out = dict(params_flat=system.flatten_params(params), x0=x0, rot0=rot0, e_l0_re=e_l0.real, e_l0_im=e_l0.imag,
+               u_comb=u_comb, extra=extra, ndev=np.int64(NDEV),
+               energy_re=np.stack(trace["energy"]).real, energy_im=np.stack(trace["energy"]).imag,
+               weights=np.stack(trace["weights"]), positions=np.stack(trace["positions"]),
+               newinds=np.stack(trace["newinds"]), comb_weight=np.stack(trace["comb_weight"]),
+               e_est=np.array(trace["e_est"]), e_trial=np.array(trace["e_trial"]), x_final=x,
+               tstep=np.float64(TSTEP), feedback=np.float64(FEEDBACK))
+    for key in steps[0]:
+        out[key] = np.stack([st[key] for st in steps])
+    np.savez_compressed(os.path.join(out_dir, "C_dmc_attractive_2dev.npz"), **out)
+    print("2dev e_est", trace["e_est"], "comb weights", trace["comb_weight"], "newinds", trace["newinds"])
 
 
 def make(out_dir: str, name: str):
@@ -80,5 +120,8 @@ def make(out_dir: str, name: str):
 
 
 if __name__ == "__main__":
-    for n in sys.argv[1:] or list(TABLES):
-        make(os.path.dirname(os.path.abspath(__file__)), n)
+    for n in sys.argv[1:] or list(TABLES) + ["attractive_2dev"]:
+        if n == "attractive_2dev":
+            make_2dev(os.path.dirname(os.path.abspath(__file__)))
+        else:
+            make(os.path.dirname(os.path.abspath(__file__)), n)
