@@ -24,22 +24,25 @@ using namespace aq;
 // ============================================================================ small kernels
 
 // v2 = sum(x[0..n)) ; taueff = (sqrt(1 + 2 tau a v2) - 1)/(a v2), a = 0.25  (VMCmcstep.py:11-14)
-// One 1024-thread block; each thread keeps all its loads in flight (fixed summation
-// order, so the result is deterministic).
+// One 1024-thread block; thread t sums x[t + 1024 j] in 8 independent partial sums (8 loads in
+// flight per thread: n = B N = 57,344 takes 7 rounds of 8), then a fixed-order tree -- the
+// result is deterministic.
 template <typename T>
 __global__ __launch_bounds__(1024) void k_taueff(const T* __restrict__ x, int n, double tstep, double* out) {
   __shared__ double red[1024];
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int i = threadIdx.x;
-  for (; i + 3 * 1024 < n; i += 4 * 1024) {
-    const T a = x[i], b = x[i + 1024], c = x[i + 2048], d = x[i + 3072];
-    s0 += (double)a;
-    s1 += (double)b;
-    s2 += (double)c;
-    s3 += (double)d;
+  for (; i + 7 * 1024 < n; i += 8 * 1024) {
+    T v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = x[i + k * 1024];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] += (double)v[k];
   }
-  for (; i < n; i += 1024) s0 += (double)x[i];
-  red[threadIdx.x] = (s0 + s1) + (s2 + s3);
+#pragma unroll
+  for (int k = 0; k < 7; ++k)
+    if (i + k * 1024 < n) s[k] += (double)x[i + k * 1024];
+  red[threadIdx.x] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __syncthreads();
   for (int w = 512; w > 0; w >>= 1) {
     if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];

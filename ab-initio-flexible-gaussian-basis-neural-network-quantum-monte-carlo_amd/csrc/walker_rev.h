@@ -173,7 +173,10 @@ __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
   using Ly = Lay<N, A>;
   using EC = ECache<N, A>;
   constexpr int D0 = 4 * A;
-  __shared__ T eb[16 * EC::size];
+  // records padded by one element in LDS: EC::size is a multiple of 16, so an unpadded record
+  // stride puts the 16 lanes of a direction row on one bank (16-way conflicts)
+  constexpr int RS = EC::size + 1;
+  __shared__ T eb[16 * RS];
   const cptr<T> P = param_ptr<T>(ka.prm);
   const int lane = threadIdx.x;
   const int lc = lane >> 4, s = lane & 15;
@@ -198,7 +201,7 @@ __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
   }
   ElecOut<T, A> eo;
   electron_stage<T, N, A>(P, xp, i, lc, eo);
-  T* E = eb + s * EC::size;
+  T* E = eb + s * RS;
 #pragma unroll
   for (int col = 0; col < N; ++col) {
     PJ<T> sy = P[Ly::wy + col] * eo.yst[0];
@@ -217,7 +220,10 @@ __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
   else E[EC::jd + lc] = eo.jae.d1;
   __syncthreads();
   T* dst = (T*)ka.ecache + (size_t)blk * 16 * EC::size;
-  for (int idx = lane; idx < nrec * EC::size; idx += 64) dst[idx] = eb[idx];
+  for (int idx = lane; idx < nrec * EC::size; idx += 64) {
+    const int rec = idx / EC::size;
+    dst[idx] = eb[idx + rec];
+  }
 }
 
 // Occupancy hint per instantiation: fp32 N2 (14, 2) lands one VGPR above the
