@@ -110,7 +110,8 @@ struct ECache {
   static constexpr int hd = yd + 3 * N; // [3][D0] dfeat/dx_c
   static constexpr int jv = hd + 3 * D0;
   static constexpr int jd = jv + 1;     // [3]
-  static constexpr int size = ((jd + 3 + 15) / 16) * 16;
+  static constexpr int xp = jd + 3;     // [3]     the moved electron's proposed position
+  static constexpr int size = ((xp + 3 + 15) / 16) * 16;
 };
 
 template <typename T, int N, int A>
@@ -218,6 +219,10 @@ __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
   }
   if (lc == 3) E[EC::jv] = eo.jae.v;
   else E[EC::jd + lc] = eo.jae.d1;
+  if (lc == 3) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) E[EC::xp + c] = xp[c];
+  }
   __syncthreads();
   T* dst = (T*)ka.ecache + (size_t)blk * 16 * EC::size;
   for (int idx = lane; idx < nrec * EC::size; idx += 64) {
@@ -296,7 +301,7 @@ k_walker_rev(KArgs ka) {
         if (ka.acc.count) atomicAdd(&ka.acc.count[conf], 1);
       }
     }
-  } else if (lane < 3 * N) {
+  } else if (!PROP && lane < 3 * N) {   // PROP: positions come with the cache loads of F1
     T x = ((const T*)ka.pos)[(size_t)pb * 3 * N + lane];
     if (isprop && lane / 3 == pi) {
       sm[SM::R + (lane - 3 * pi)] = x;                       // old position of the moved electron
@@ -310,7 +315,7 @@ k_walker_rev(KArgs ka) {
     }
     xs[lane] = x;
   }
-  __syncthreads();
+  if constexpr (!PROP) __syncthreads();
 
   AQ_PH(0);
   // ------------------------------------------------------------------ F1 per-electron stage (electron.h)
@@ -330,6 +335,14 @@ k_walker_rev(KArgs ka) {
     // all loads issued before the first LDS store
     constexpr int NY = (N * N + 63) / 64, NHh = (N * D0 + 63) / 64, NG = (3 * 2 * N * 4 + 63) / 64;
     T ry[NY], rh[NHh], rg[NG];
+    // PROP: F0's positions too (walker pb's, the moved electron's proposed position from
+    // k_moved_electron), so that every global load of F0/F1 is in flight before one barrier
+    const bool mvl = lane < 3 * N && lane / 3 == pi;
+    T x0 = T(0), xm = T(0);
+    if constexpr (PROP) {
+      if (lane < 3 * N) x0 = ((const T*)ka.pos)[(size_t)pb * 3 * N + lane];
+      if (mvl) xm = Eq[EC::xp + (lane - 3 * pi)];
+    }
 #pragma unroll
     for (int t = 0; t < NY; ++t) {
       const int idx = lane + 64 * t;
@@ -351,6 +364,10 @@ k_walker_rev(KArgs ka) {
     jd1 = dir ? ((le == pi) ? Eq[EC::jd + lc] : Wc[WC::jaed + lane]) : T(0);
     jve = lane == 0 ? Wc[WC::jee] : T(0);
     pvr = lane < 2 * N + 2 ? Wc[WC::pv + lane] : T(0);   // to LDS after F4 (SmemRev::pv)
+    if constexpr (PROP) {
+      if (mvl) sm[SM::R + (lane - 3 * pi)] = x0;             // old position of the moved electron
+      if (lane < 3 * N) xs[lane] = mvl ? xm : x0;
+    }
 #pragma unroll
     for (int t = 0; t < NY; ++t)
       if (lane + 64 * t < N * N) Yv[lane + 64 * t] = ry[t];
