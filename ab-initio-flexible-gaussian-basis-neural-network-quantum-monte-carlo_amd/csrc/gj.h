@@ -200,27 +200,16 @@ __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, in
 // sqrt per matrix instead of per step.  bad = some |pivot_k| < 0.1 |walker pivot_k| or z
 // not finite (the order may not suit this matrix: the caller falls back to gj_inverse).
 // rec: the walker's record written by gj_inverse (LDS copy).
+// The elimination of gj_inverse_fixed on a matrix already in its register layout:
+// a2[t] = A[rec[rg RW + t]][c] for lane 16 rg + c (zero outside the N x N block).
 template <typename T, int N>
-__device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bout, int lane, const T* rec,
-                                                 T& logdet, T& phr, T& phi, bool& bad) {
+__device__ __forceinline__ void gj_fixed_regs(typename Pair<T>::type* a2, T* Bout, int lane, const T* rec,
+                                              T& logdet, T& phr, T& phi, bool& bad) {
   constexpr int RW = (N + 3) / 4;
   using V2 = typename Pair<T>::type;
   const int c = lane & 15;
   const int rg = lane >> 4;
   const bool clive = c < N;
-  V2 a2[RW];
-#pragma unroll
-  for (int t = 0; t < RW; ++t) {
-    const int k = rg * RW + t;
-    T a = T(0), b = T(0);
-    if (k < N && clive) {
-      const int r = (int)rec[k];
-      const T y = Yv[r * N + c];
-      a = Ph[(r * N + c) * 2] * y;
-      b = Ph[(r * N + c) * 2 + 1] * y;
-    }
-    a2[t] = pair_make<T>(a, b);
-  }
   T zr = T(1), zi = T(0);
   bool small = false;
   T pkr = T(1), pki = T(0);
@@ -305,6 +294,30 @@ __device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bo
   phr = zr * sg;
   phi = zi * sg;
   bad = small || !zok;
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bout, int lane, const T* rec,
+                                                 T& logdet, T& phr, T& phi, bool& bad) {
+  constexpr int RW = (N + 3) / 4;
+  using V2 = typename Pair<T>::type;
+  const int c = lane & 15;
+  const int rg = lane >> 4;
+  const bool clive = c < N;
+  V2 a2[RW];
+#pragma unroll
+  for (int t = 0; t < RW; ++t) {
+    const int k = rg * RW + t;
+    T a = T(0), b = T(0);
+    if (k < N && clive) {
+      const int r = (int)rec[k];
+      const T y = Yv[r * N + c];
+      a = Ph[(r * N + c) * 2] * y;
+      b = Ph[(r * N + c) * 2 + 1] * y;
+    }
+    a2[t] = pair_make<T>(a, b);
+  }
+  gj_fixed_regs<T, N>(a2, Bout, lane, rec, logdet, phr, phi, bad);
 }
 
 }  // namespace aq

@@ -620,10 +620,14 @@ k_walker_rev(KArgs ka) {
         if (ilive && (q & 3) == ff) cqv[(l * N + ic) * SM::QM + q] = cq[q];
       }
     }
-    T z = sngb[ff];
+    T z = sngb[ff], z1 = T(0);   // even / odd q: two independent chains
 #pragma unroll
     for (int q = 0; q < SM::QM; ++q)
-      if (q < Q) z += cq[q] * sngw[q * 4 + ff];
+      if (q < Q) {
+        if (q & 1) z1 += cq[q] * sngw[q * 4 + ff];
+        else z += cq[q] * sngw[q * 4 + ff];
+      }
+    z += z1;
     const T sval = f_tanh(z);
     if (ilive) sv[(l * N + ic) * 4 + ff] = sval;
     const T hin = l == 0 ? hl[ic * D0 + ff] : hreg;
@@ -639,7 +643,9 @@ k_walker_rev(KArgs ka) {
   T* Ph = sm + SM::ph;
   T* Mx = sm + SM::mx;
   const T* H3 = hl + SM::hoff(3);
-  for (int idx = lane; idx < N * N; idx += 64) {
+  // proposals: Phi is formed in the fixed-pivot Gauss-Jordan's register layout below (no LDS
+  // round trip, no barrier); the general path keeps the LDS copy for gj_inverse
+  for (int idx = PROP ? N * N : lane; idx < N * N; idx += 64) {
     const int r = idx / N, col = idx - r * N;
     const int src = rowsrc[r];
     const int sp = r < nup ? 0 : 1;
@@ -655,12 +661,45 @@ k_walker_rev(KArgs ka) {
     Ph[idx * 2 + 0] = re;
     Ph[idx * 2 + 1] = im;
   }
-  __syncthreads();
+  if constexpr (!PROP) __syncthreads();   // PROP: one wave, the Gauss-Jordan below forms Phi itself
   T logdet, phr, phi;
   if (reuse) {
     // the walker's pivot order (partial pivoting rerun only if a pivot comes out small)
     bool bad = false;
     logdet = phr = phi = T(0);
+    if constexpr (PROP) {
+      // A[r][c] = Phi[r][c] Yt[r][c] for the lane's rows r = rec[rg RW + t] (column c = lane & 15),
+      // Phi[r][c] = h3[rowsrc[r]] . W_{s(r)}[:, c] + b_{s(r)}[c]; Phi also to LDS for B1
+      constexpr int RW = (N + 3) / 4;
+      using V2 = typename Pair<T>::type;
+      const int cc = lane & 15, rg = lane >> 4;
+      const T* rec = sm + SM::pv;
+      V2 a2[RW];
+#pragma unroll
+      for (int t = 0; t < RW; ++t) {
+        const int k = rg * RW + t;
+        T a = T(0), b = T(0);
+        if (k < N && cc < N) {
+          const int r = (int)rec[k];
+          const int src = rowsrc[r];
+          const int sp = r < nup ? 0 : 1;
+          T re = P[Ly::orb_b + (sp * N + cc) * 2 + 0], im = P[Ly::orb_b + (sp * N + cc) * 2 + 1];
+#pragma unroll
+          for (int f = 0; f < 4; ++f) {
+            const T hv = H3[src * 4 + f];
+            re += hv * P[Ly::orb_w + ((sp * 4 + f) * N + cc) * 2 + 0];
+            im += hv * P[Ly::orb_w + ((sp * 4 + f) * N + cc) * 2 + 1];
+          }
+          Ph[(r * N + cc) * 2 + 0] = re;
+          Ph[(r * N + cc) * 2 + 1] = im;
+          const T y = Yv[r * N + cc];
+          a = re * y;
+          b = im * y;
+        }
+        a2[t] = pair_make<T>(a, b);
+      }
+      if (!AQ_ABL(4)) gj_fixed_regs<T, N>(a2, Mx, lane, rec, logdet, phr, phi, bad);
+    } else
     if (!AQ_ABL(4)) gj_inverse_fixed<T, N>(Ph, Yv, Mx, lane, sm + SM::pv, logdet, phr, phi, bad);
 #ifdef AQ_ABLATE
     if (ka.ablate) bad = false;
@@ -708,13 +747,16 @@ k_walker_rev(KArgs ka) {
   if (lane < 4 * N && !AQ_ABL(8)) {
     const int r = lane >> 2, f = lane & 3;
     const int sp = r < nup ? 0 : 1;
-    T q = T(0);
+    T q = T(0), q1 = T(0);   // even / odd c: two independent chains
+#pragma unroll
     for (int c = 0; c < N; ++c) {
       const T yv = Yv[r * N + c];
       const T wr = P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2] * yv;
       const T wi = P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 1] * yv;
-      q += wr * BRE(c, r) - wi * BIM(c, r);
+      if (c & 1) q1 += wr * BRE(c, r) - wi * BIM(c, r);
+      else q += wr * BRE(c, r) - wi * BIM(c, r);
     }
+    q += q1;
     hbar[SM::hoff(3) + rowsrc[r] * 4 + f] = q;
   }
   if constexpr (PREP) {
@@ -1081,14 +1123,25 @@ k_walker_rev(KArgs ka) {
   // ------------------------------------------------------------------ B4 gradient per direction lane (c, e)
   T g = jd1;
   if (!AQ_ABL(64)) {
+    // four partial sums: the LDS reads and FMAs of one chain do not wait on each other
+    T ga = T(0), gb = T(0), gc = T(0);
+#pragma unroll
     for (int k = 0; k < N; ++k) {
-      if (k == le) continue;
-      g += dbar[(k * N + le) * 3 + c4] - dbar[(le * N + k) * 3 + c4];
+      const T dk = dbar[(k * N + le) * 3 + c4] - dbar[(le * N + k) * 3 + c4];
+      if (k & 1) ga += (k == le) ? T(0) : dk;
+      else g += (k == le) ? T(0) : dk;
     }
 #pragma unroll
-    for (int col = 0; col < N; ++col) g += ybar[le * N + col] * lv[col];
+    for (int col = 0; col < N; ++col) {
+      if (col & 1) gc = f_fma(ybar[le * N + col], lv[col], gc);
+      else gb = f_fma(ybar[le * N + col], lv[col], gb);
+    }
 #pragma unroll
-    for (int m = 0; m < D0; ++m) g += hbar[le * D0 + m] * lv[N + m];
+    for (int m = 0; m < D0; ++m) {
+      if (m & 1) gc = f_fma(hbar[le * D0 + m], lv[N + m], gc);
+      else gb = f_fma(hbar[le * D0 + m], lv[N + m], gb);
+    }
+    g = (g + ga) + (gb + gc);
   }
 
   AQ_PH(8);
