@@ -15,6 +15,17 @@ KERNELS = {
     "walker": "k_walker_rev<float, 14, 2, false, false>",
     "moved_electron": "k_moved_electron<float, 14, 2>",
 }
+PROPOSAL_WAVES = 4096 * 14   # reuse off: the proposals run in the general instantiation
+
+
+def classify(name, grid, wg):
+    """Kernel key of one dispatch (by name; the general instantiation by its grid)."""
+    for key, pat in KERNELS.items():
+        if pat in name:
+            if key == "walker" and grid // wg == PROPOSAL_WAVES:
+                return "proposal"
+            return key
+    return None
 
 
 def per_pass(root, name):
@@ -24,10 +35,10 @@ def per_pass(root, name):
         acc = collections.defaultdict(lambda: collections.defaultdict(float))
         disp = collections.defaultdict(set)
         for r in csv.DictReader(open(f)):
-            for key, pat in KERNELS.items():
-                if pat in r["Kernel_Name"]:
-                    acc[key][r["Counter_Name"]] += float(r["Counter_Value"])
-                    disp[key].add(r["Dispatch_Id"])
+            key = classify(r["Kernel_Name"], int(r["Grid_Size"]), int(r["Workgroup_Size"]))
+            if key is not None:
+                acc[key][r["Counter_Name"]] += float(r["Counter_Value"])
+                disp[key].add(r["Dispatch_Id"])
         for key, d in acc.items():
             n = max(len(disp[key]), 1)
             out[key] = {c: v / n for c, v in d.items()}
