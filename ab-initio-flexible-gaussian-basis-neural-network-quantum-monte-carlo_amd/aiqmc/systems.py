@@ -121,6 +121,17 @@ _C_NONLOCAL = ([[2.0, 2.0], [2.0, 2.0], [2.0, 2.0]], [[52.13345, 0], [0, 0], [0,
                [[7.76079, 0], [0, 0], [0, 0]])
 
 
+def all_electron_tables(name: str, list_l: int = 2) -> EcpTables:
+    """Zero pseudopotential tables: the pp local energy and T-moves of dmc_propagate (which is
+    pp-only, DMC/dmc.py:13-94) reduce to the all-electron Hamiltonian -- zero local coefficients
+    leave the -Z/r part of local_pp_energy (pseudopotential.py:86-117), zero nonlocal
+    coefficients make E_nl = 0 and every T-move amplitude 0.  How "Ne + DMC" runs."""
+    A = make_system(name).natoms
+    one = lambda v: np.full((A, 1), v, np.float64)
+    nl = lambda v: np.full((A, list_l + 1, 1), v, np.float64)
+    return EcpTables(one(1.0), one(0.0), one(1.0), nl(2.0), nl(0.0), nl(1.0), list_l)
+
+
 def ccecp_tables(name: str) -> EcpTables:
     """The ccECP tables of a pseudopotential example system (one carbon block per atom)."""
     if name not in ("C_ecp", "C2_ecp"):

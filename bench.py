@@ -205,11 +205,12 @@ def pp_adam_side_bench(dtype, device, walkers, steps):
             "energy": lv, "finite": bool(math.isfinite(lv))}
 
 
-def dmc_side_bench(dtype, device, walkers, steps):
+def dmc_side_bench(dtype, device, walkers, steps, system="C_ecp"):
     """DMC propagation through the drop-in API (DMC/dmc.py:72-93 + branch.py, as main_dmc.py:160-210
     drives it): T-moves, drift-diffusion, pp local energies before/after, weight update, stochastic
-    comb, on the C-atom ccECP system (the only pseudopotential tables the reference ships;
-    dmc_propagate always uses the pp Hamiltonian)."""
+    comb.  system "C_ecp": the C-atom ccECP tables (the only ones the reference ships);
+    "Ne": all-electron Ne through the same pp-only step with zero tables (BASELINE's "Ne + DMC",
+    DESIGN.md 4d)."""
     from aiqmc import spin_indices
     from aiqmc.DMC import dmc
     from aiqmc.DMC.Tmoves import compute_tmoves
@@ -217,15 +218,16 @@ def dmc_side_bench(dtype, device, walkers, steps):
     from aiqmc.wavefunction_Ynlm import nn
     from aiqmc.initial_electrons_positions.init import init_electrons
     from aiqmc import systems
-    s = systems.make_system("C_ecp")
+    s = systems.make_system(system)
+    N, A = s.nelectrons, s.natoms
     network = s.make_network()
     params = network.init(3)
-    e = systems.ccecp_tables("C_ecp")
+    e = systems.ccecp_tables(system) if system.endswith("_ecp") else systems.all_electron_tables(system)
     tstep = 0.01
-    run = dmc.dmc_propagate(network.apply, nn.make_log_network(network.apply), network.apply, e.list_l, 4, 1, 3,
+    run = dmc.dmc_propagate(network.apply, nn.make_log_network(network.apply), network.apply, e.list_l, N, A, 3,
                             walkers, tstep, 1, s.charges, s.spins, e.rn_local, e.local_coes, e.local_exps,
                             e.rn_non_local, e.non_local_coes, e.non_local_exps)
-    tm = compute_tmoves(e.list_l, tstep, 4, 1, 3, nn.make_log_network(network.apply), e.rn_non_local,
+    tm = compute_tmoves(e.list_l, tstep, N, A, 3, nn.make_log_network(network.apply), e.rn_non_local,
                         e.non_local_coes, e.non_local_exps)
     pos, sp = init_electrons(11, None, s.atoms, s.charges, s.spins, walkers, 1.0)
     data = nn.AINetData(positions=pos.to(device, dtype).contiguous(), spins=sp, atoms=s.atoms, charges=s.charges)
@@ -233,9 +235,11 @@ def dmc_side_bench(dtype, device, walkers, steps):
     w = torch.ones(walkers, dtype=dtype, device=device)
     bc = torch.full((walkers,), 10.0)
 
+    e_ref = -5.4 if system == "C_ecp" else -128.9   # rough ground-state energies (trial/estimate)
+
     def one(k):
         nonlocal data, w
-        eloc, w, data = run(params, PhiloxKey(21, k), data, w, bc, -5.4, -5.4)
+        eloc, w, data = run(params, PhiloxKey(21, k), data, w, bc, e_ref, e_ref)
         wn, idx = ctx.dmc_branch(w, 0.37)
         data = nn.AINetData(positions=data.positions[idx.long()].contiguous(), spins=data.spins, atoms=data.atoms,
                             charges=data.charges)
@@ -255,7 +259,8 @@ def dmc_side_bench(dtype, device, walkers, steps):
         tm(data, params, PhiloxKey(5, k))
     torch.cuda.synchronize()
     dtm = time.perf_counter() - t0
-    return {"config": "C atom ccECP DMC step: T-moves + drift-diffusion + 2x pp E_L + weights + comb, drop-in API",
+    label = "C atom ccECP" if system == "C_ecp" else f"{system} all-electron (zero pp tables)"
+    return {"config": f"{label} DMC step: T-moves + drift-diffusion + 2x pp E_L + weights + comb, drop-in API",
             "walkers": walkers, "tstep": tstep, "ms_per_dmc_step": 1e3 * dt / steps,
             "walker_steps_per_s": walkers * steps / dt, "tmoves_ms": 1e3 * dtm / steps,
             "mean_energy_re": float(eloc.real.mean()),
@@ -467,6 +472,10 @@ def main():
                 out["dmc_c_atom"] = dmc_side_bench(dtype, dev, 4096, 5)
             except Exception as e:  # a side measurement, never a failure of the headline bench
                 out["dmc_c_atom"] = {"error": repr(e)}
+            try:
+                out["dmc_ne_atom"] = dmc_side_bench(dtype, dev, 4096, 5, system="Ne")
+            except Exception as e:  # a side measurement, never a failure of the headline bench
+                out["dmc_ne_atom"] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(args.system, params, atoms, charges, args.nsteps, args.tstep,

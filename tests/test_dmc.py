@@ -405,8 +405,9 @@ _TRAJ_TABLES = {
     "ccecp": lambda opp: opp.c_atom_ccecp(),
     "attractive": lambda opp: opp.ECP([[1.0]], [[0.0]], [[1.0]], [[[2.0], [1.0]]], [[[-3.0], [-5.0]]],
                                       [[[0.7], [0.4]]], 1),
-    "ne_allelectron": lambda opp: opp.ECP([[1.0]], [[0.0]], [[1.0]], [[[2.0], [2.0], [2.0]]], [[[0.0], [0.0], [0.0]]],
-                                          [[[1.0], [1.0], [1.0]]], 2),
+    # the product's zero tables (aiqmc.systems.all_electron_tables); the fixture was made with the
+    # oracle's identical ECP([[1]], [[0]], [[1]], [[[2]]*3], [[[0]]*3], [[[1]]*3], 2)
+    "ne_allelectron": lambda opp: __import__("aiqmc.systems", fromlist=["x"]).all_electron_tables("Ne"),
 }
 
 
