@@ -910,6 +910,9 @@ int aiqmc_set_ecp(aiqmc_ctx* c, const aiqmc_ecp* e) {
   c->ecp_KL = KL;
   c->ecp_KN = KN;
   c->ecp_L = L;
+  c->ecp_nl_zero = true;
+  for (size_t k = 0; k < (size_t)A * L * KN; ++k)
+    if (e->non_local_coes[k] != 0.0) c->ecp_nl_zero = false;
   c->ecp_set = true;
   return AIQMC_OK;
 }
@@ -1013,10 +1016,25 @@ int aiqmc_local_energy_ecp(aiqmc_ctx* c, const void* pos, int32_t B, int32_t rng
   }
   rc = aiqmc_local_energy(c, pos, B, c->d_ecp_el, nullptr, nullptr, stream);
   if (rc) return rc;
-  // (2)-(4) rotations, quadrature positions, log psi at the walkers and the quadrature points
+  // (2)-(4) rotations, quadrature positions, log psi at the walkers and the quadrature points --
+  // skipped when every nonlocal coefficient is 0 (all-electron tables, "Ne + DMC"): each
+  // quadrature term is 0 times a finite log-ratio (E4), so only the local part remains
   EcpArgs ea;
-  rc = ecp_quadrature(c, pos, B, rng_mode, rot, seed, offset, logabs_q, phase_q, ea, s);
-  if (rc) return rc;
+  if (c->ecp_nl_zero && !logabs_q && !phase_q) {
+    std::memset(&ea, 0, sizeof(ea));
+    ea.B = B;
+    ea.N = c->N;
+    ea.A = c->A;
+    ea.KL = c->ecp_KL;
+    ea.KN = c->ecp_KN;
+    ea.L = c->ecp_L;
+    ea.tab = c->d_ecp_tab;
+    ea.pos = pos;
+    ea.skip_nl = 1;
+  } else {
+    rc = ecp_quadrature(c, pos, B, rng_mode, rot, seed, offset, logabs_q, phase_q, ea, s);
+    if (rc) return rc;
+  }
   ea.eall = c->d_ecp_el;
   ea.e_re = e_re;
   ea.e_im = e_im;
@@ -1040,6 +1058,15 @@ int aiqmc_dmc_tmoves(aiqmc_ctx* c, void* pos, int32_t B, double tstep, int32_t r
   if (B == 0) return AIQMC_OK;
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
+  if (c->ecp_nl_zero) {   // no T-move amplitude: nothing moves, acceptance exactly 1 (k_tmove_none)
+    if (acceptance) {
+      const int n = B * c->N;
+      if (c->dtype == AIQMC_F32) k_tmove_none<float><<<dim3((n + 255) / 256), dim3(256), 0, s>>>((float*)acceptance, n);
+      else k_tmove_none<double><<<dim3((n + 255) / 256), dim3(256), 0, s>>>((double*)acceptance, n);
+      HIPCHK(hipGetLastError());
+    }
+    return AIQMC_OK;
+  }
   {
     ShapeOps ops0;
     shape_ops(c->N, c->A, &ops0);

@@ -51,6 +51,7 @@ struct aiqmc_ctx {
   // pseudopotential (aiqmc_set_ecp / aiqmc_local_energy_ecp, ecp.h)
   bool ecp_set = false;
   int ecp_KL = 0, ecp_KN = 0, ecp_L = 0;
+  bool ecp_nl_zero = false;   // every nonlocal coefficient 0 (all-electron through the pp path)
   double* d_ecp_tab = nullptr;
   int ecp_B = 0;
   void *d_ecp_rot = nullptr, *d_ecp_x = nullptr, *d_ecp_lq = nullptr, *d_ecp_pq = nullptr, *d_ecp_ec = nullptr,

@@ -85,6 +85,7 @@ struct EcpArgs {
   void* e_im;
   void* xnew;           // k_ecp_points output [B*N*A*50][3]
   uint64_t seed, step;  // k_ecp_rot
+  int skip_nl;          // k_ecp_energy: nonlocal coefficients all zero -- no quadrature was run
   // T-moves (k_tmove)
   double tstep;
   const void* usel;     // [B] selection uniform (NULL: Philox)
@@ -171,10 +172,12 @@ __global__ __launch_bounds__(64) void k_ecp_energy(EcpArgs ea) {
   const double* tabs = ea.tab + 4 * A;
   const T* x = (const T*)ea.pos + (size_t)b * 3 * N;
   const T* R = (const T*)ea.rot + (size_t)b * 9;
-  const double la0 = (double)((const T*)ea.lp0)[b], ph0 = (double)((const T*)ea.ph0)[b];
+  const double la0 = ea.skip_nl ? 1.0 : (double)((const T*)ea.lp0)[b];
+  const double ph0 = ea.skip_nl ? 0.0 : (double)((const T*)ea.ph0)[b];
   const double dn = 1.0 / (la0 * la0 + ph0 * ph0);   // 1 / den, den = la0 + i ph0 (E4)
   double er = 0.0, ei = 0.0;
-  for (int idx = lane; idx < M; idx += 64) {
+  // zero nonlocal coefficients: every term is v_l(r) = 0 times a finite ratio, exactly 0
+  for (int idx = ea.skip_nl ? M : lane; idx < M; idx += 64) {
     const int i = idx / (A * ECP_NQ);
     const int a = (idx / ECP_NQ) % A;
     const int q = idx % ECP_NQ;
@@ -242,6 +245,14 @@ __global__ __launch_bounds__(64) void k_ecp_energy(EcpArgs ea) {
     ((T*)ea.e_re)[b] = (T)((double)((const T*)ea.eall)[b] - ven + er);
     ((T*)ea.e_im)[b] = (T)ei;
   }
+}
+
+// Acceptance of T-moves with zero nonlocal coefficients: every amplitude is 0, norm = back norm
+// = 1, nothing moves and the acceptance is exactly 1 (what k_tmove computes for such tables).
+template <typename T>
+__global__ __launch_bounds__(256) void k_tmove_none(T* __restrict__ acc, int n) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) acc[t] = T(1);
 }
 
 // T-moves (DMC/Tmoves.py:68-224; oracle/dmc.py tmoves, quirks T1-T8), one wave per walker.
