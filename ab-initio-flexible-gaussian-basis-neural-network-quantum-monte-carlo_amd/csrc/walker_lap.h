@@ -37,9 +37,14 @@ struct SmemLap {
   static constexpr int ly = 48;                              // one layer's LapCache block
   // lane-private arrays [..][49]: direction lanes 0..47 own a column; the 16 value-row
   // lanes share column 48 (they carry no derivatives; their stores there are don't-cares)
-  static constexpr int hb = ly + LapCache<N, A>::layer_n;    // [N][4][49] dh/dx
-  static constexpr int yd = hb + N * NH * 49;                // [2][N][49] dYt/dx, d2Yt/dx2 of row le
-  static constexpr int end = yd + 2 * N * 49;
+  static constexpr int yd = ly + LapCache<N, A>::layer_n;    // [2][N][49] dYt/dx, d2Yt/dx2 of row le
+  static constexpr int hb = yd + 2 * N * 49;                 // [N][4][49] dh/dx
+  static constexpr int end = hb + N * NH * 49;
+  // Q_f [N][N][4][2] (and B [N][N][2] where it fits) staged over ly + yd once both are dead
+  static constexpr int qs = ly;
+  static constexpr int bs = qs + 8 * N * N;
+  static constexpr bool stage_b = 10 * N * N <= LapCache<N, A>::layer_n + 2 * N * 49;
+  static_assert(8 * N * N <= LapCache<N, A>::layer_n + 2 * N * 49, "Q_f must fit over ly + yd");
   static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
   static_assert(end - ly >= 3 * 3 * 64, "multi-wave partial sums (W <= 4) must fit behind ly");
 };
@@ -276,10 +281,8 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
   // ------------------------------------------------------------------ determinant terms
   // (phases fenced so that the scheduler does not stretch their live ranges across each other)
   const int* rowsrc = ka.rowsrc;
-  using cT = const __attribute__((address_space(4))) T;   // wave-uniform reads -> scalar loads
-  cT* Qs = (cT*)(Lc + LC::qs);
-  cT* Bu = (cT*)(Lc + LC::bm);
-  const cptr<T> Bm = Lc + LC::bm;
+  const T* Qs = nullptr;                     // LDS copy, set after E1
+  const T* Bu = (const T*)(Lc + LC::bm);     // LDS copy after E1 where it fits
   const cptr<T> Ph = Lc + LC::ph;
 #define UH(r, f) hb[(rowsrc[r] * NH + (f)) * 49 + l49]
   // E1: Yt row jets of electron le (stored after the per-electron stage)
@@ -290,6 +293,20 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
     Yd2[col] = yd[(N + col) * 49 + l49];
   }
   __builtin_amdgcn_sched_barrier(0);
+  // Q_f (and B) to LDS over the dead layer block and Yt jets: E2-E4 read them at wave-uniform
+  // and per-lane offsets; their scalar loads from L2 were E4's latency chain
+  __syncthreads();   // every wave has read its Yt jets (E1)
+  {
+    T* qd = sm + SM::qs;
+    for (int idx = threadIdx.x; idx < 8 * N * N; idx += blockDim.x) qd[idx] = Lc[LC::qs + idx];
+    if constexpr (SM::stage_b) {
+      T* bd = sm + SM::bs;
+      for (int idx = threadIdx.x; idx < 2 * N * N; idx += blockDim.x) bd[idx] = Lc[LC::bm + idx];
+    }
+  }
+  __syncthreads();
+  Qs = sm + SM::qs;
+  if constexpr (SM::stage_b) Bu = sm + SM::bs;
   // E2: w = Phi[e,:] * dYt[e,:], w.b_e, and t2 = Re sum_col (2 dPhi[e,col] Yt'[col] +
   //     Phi[e,col] Yt''[col]) B[col,e] with e = le (U of row e)
   const int spe = le < nup ? 0 : 1;
@@ -301,7 +318,7 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
 #pragma unroll
   for (int col = 0; col < N; ++col) {
     const T pr = Ph[(le * N + col) * 2], pm = Ph[(le * N + col) * 2 + 1];
-    const T br = Bm[(col * N + le) * 2], bi = Bm[(col * N + le) * 2 + 1];
+    const T br = Bu[(col * N + le) * 2], bi = Bu[(col * N + le) * 2 + 1];
     wr[col] = pr * Yd1[col];
     wi[col] = pm * Yd1[col];
     wbr += wr[col] * br - wi[col] * bi;
