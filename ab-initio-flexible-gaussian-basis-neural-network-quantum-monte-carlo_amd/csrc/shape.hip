@@ -238,7 +238,9 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
     if (mode == MODE_LAP)
       k_walker<float, N, A, MODE_LAP><<<dim3(nconf), dim3(64), Smem<float, N, true>::bytes, s>>>(ka);
     else if (mode == MODE_GRAD && ka.proposal && ka.ecache)   // proposals from the walker cache
-      k_walker_rev<float, N, A, false, true><<<dim3(nconf), dim3(64), SmemRev<float, N, A>::bytes, s>>>(ka);
+      k_walker_rev<float, N, A, false, true><<<dim3((nconf + RevWpb<float, true>::value - 1) / RevWpb<float, true>::value),
+                                              dim3(64 * RevWpb<float, true>::value),
+                                              RevWpb<float, true>::value * SmemRev<float, N, A>::bytes, s>>>(ka);
     else if (mode == MODE_GRAD)
       k_walker_rev<float, N, A><<<dim3(nconf), dim3(64), SmemRev<float, N, A>::bytes, s>>>(ka);
     else
@@ -247,7 +249,9 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
     if (mode == MODE_LAP)
       k_walker<double, N, A, MODE_LAP><<<dim3(nconf), dim3(64), Smem<double, N, true>::bytes, s>>>(ka);
     else if (mode == MODE_GRAD && ka.proposal && ka.ecache)   // proposals from the walker cache
-      k_walker_rev<double, N, A, false, true><<<dim3(nconf), dim3(64), SmemRev<double, N, A>::bytes, s>>>(ka);
+      k_walker_rev<double, N, A, false, true><<<dim3((nconf + RevWpb<double, true>::value - 1) / RevWpb<double, true>::value),
+                                              dim3(64 * RevWpb<double, true>::value),
+                                              RevWpb<double, true>::value * SmemRev<double, N, A>::bytes, s>>>(ka);
     else if (mode == MODE_GRAD)
       k_walker_rev<double, N, A><<<dim3(nconf), dim3(64), SmemRev<double, N, A>::bytes, s>>>(ka);
     else

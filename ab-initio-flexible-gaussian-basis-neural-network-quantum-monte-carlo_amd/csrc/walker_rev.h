@@ -62,8 +62,10 @@ struct SmemRev {
   static constexpr int xs = 0;                   // 48
   static constexpr int hl = 48;                  // h^0 [N][D0], h^3 [N][4] (F1..F5)
   static constexpr int hbar = hl;                // their adjoints, same layout (B1..B4)
-  static constexpr int cq = hl + hl_n;           // [3][N][QM]  conv outputs (kept for backward)
-  static constexpr int sv = cq + 3 * N * QM;     // [3][N][4]   single outputs
+  static constexpr int QL = (3 * 4 + 8) / 4;     // conv outputs of layers 1, 2
+  static constexpr int cq = hl + hl_n;           // conv outputs (kept for backward): [N][QM], [2][N][QL]
+  static constexpr int sv = cq + N * QM + 2 * N * QL;   // [3][N][4]   single outputs
+  static constexpr int cqo(int l, int i) { return l == 0 ? i * QM : N * QM + ((l - 1) * N + i) * QL; }
   static constexpr int g2 = sv + 3 * N * 4;      // [3][2][N][4] g2 values (forward) / adjoints (backward)
   static constexpr int yv = g2 + 3 * 2 * N * 4;  // [N][N]  Yt (F1..B1)
   static constexpr int ybar = yv;                // [N][N]  its adjoint (B1..B4)
@@ -249,23 +251,52 @@ template <typename T, int N, int A, bool PREP, bool PROP> struct RevWaves {
 // PREP = true : first launch of the local energy (walker_lap.h): values, the adjoint pass
 //   through the h stream, and the pair stream's derivative sums and curvature, written to
 //   the walker's LapCache; no gradient (B3/B4) and no Metropolis cache.
+// Proposal launches: AQ_PROP_WPB configurations (one wave each) per workgroup; the waves share
+// nothing, so their LDS regions are disjoint and every barrier is wave-local.
+#ifndef AQ_PROP_WPB
+#define AQ_PROP_WPB 2
+#endif
+template <typename T, bool PROP> struct RevWpb {
+  static constexpr int value = (PROP && sizeof(T) == 4) ? AQ_PROP_WPB : 1;
+};
+// Barrier of a one-configuration wave: LDS traffic of one wave is processed in order, so a
+// wavefront-scope fence (a compiler barrier, no s_waitcnt) orders its cross-lane LDS accesses.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+#ifdef AQ_WAVE_SYNC
+#define AQ_SYNC() wave_sync()
+#else
+#define AQ_SYNC()                                   \
+  do {                                              \
+    if constexpr (WPB > 1) wave_sync();             \
+    else __syncthreads();                           \
+  } while (0)
+#endif
+
 template <typename T, int N, int A, bool PREP = false, bool PROP = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RevWaves<T, N, A, PREP, PROP>::value))) void
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * RevWpb<T, PROP>::value))) __attribute__((amdgpu_waves_per_eu(RevWaves<T, N, A, PREP, PROP>::value))) void
 k_walker_rev(KArgs ka) {
   using Ly = Lay<N, A>;
   using SM = SmemRev<T, N, A>;
   using LCc = LapCache<N, A>;
   constexpr int D0 = SM::D0;
+  constexpr int WPB = RevWpb<T, PROP>::value;
   const cptr<T> P = param_ptr<T>(ka.prm);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  T* sm = (T*)smem_raw;
+  // wave index within the workgroup, wave-uniform (scalar)
+  const int wv = WPB > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+  T* sm = (T*)(smem_raw + wv * SM::bytes);
   T* xs = sm + SM::xs;
 
   // The PROP instantiation is launched only for proposals that read the walker cache (shape.hip
   // routes reuse-off proposals to the general one), so there both path flags are compile-time.
   const bool isprop = PROP ? true : (ka.proposal != 0);
-  const int conf = xcd_major(blockIdx.x, gridDim.x);
-  const int lane = threadIdx.x;
+  const int conf = xcd_major(blockIdx.x, gridDim.x) * WPB + wv;
+  if (WPB > 1 && conf >= ka.nconf) return;
+  const int lane = WPB > 1 ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   const int lc = lane >> 4;
   const int er = lane & 15;
   const int le = er < N ? er : N - 1;
@@ -315,7 +346,7 @@ k_walker_rev(KArgs ka) {
     }
     xs[lane] = x;
   }
-  if constexpr (!PROP) __syncthreads();
+  if constexpr (!PROP) AQ_SYNC();
 
   AQ_PH(0);
   // ------------------------------------------------------------------ F1 per-electron stage (electron.h)
@@ -403,7 +434,7 @@ k_walker_rev(KArgs ka) {
       if (lane < 48) Wc[WC::jaed + lane] = jd1;
     }
   }
-  __syncthreads();
+  AQ_SYNC();
   if (!PREP && !isprop) {
     for (int idx = lane; idx < N * N; idx += 64) Wc[WC::yv + idx] = Yv[idx];
     for (int idx = lane; idx < N * D0; idx += 64) Wc[WC::h0 + idx] = sm[SM::hl + idx];
@@ -437,7 +468,7 @@ k_walker_rev(KArgs ka) {
         jve += part == 0 ? je : -je;
       }
     }
-    __syncthreads();
+    AQ_SYNC();
     if (lane < 16) {
       if (lane < N && lane != pi) {
         const int Gp = pi >= nup ? 1 : 0;
@@ -529,7 +560,7 @@ k_walker_rev(KArgs ka) {
           }
     }
   }
-  __syncthreads();
+  AQ_SYNC();
   if (!PREP && !isprop) {
     for (int idx = lane; idx < 3 * 2 * N * 4; idx += 64) Wc[WC::g2 + idx] = g2[idx];
     const T je = wave_sum(jve);
@@ -606,7 +637,7 @@ k_walker_rev(KArgs ka) {
         const int q0 = 4 * s4;
         const T zs = ff == 0 ? zc[q0] : (ff == 1 ? zc[q0 + 1] : (ff == 2 ? zc[q0 + 2] : zc[q0 + 3]));
         const T c = f_tanh(zs * T(0.25) + convb[q0 + ff]);
-        if (ilive) cqv[(l * N + ic) * SM::QM + q0 + ff] = c;
+        if (ilive) cqv[SM::cqo(l, ic) + q0 + ff] = c;
         cq[q0 + 0] = quad_bcast<0>(c);
         cq[q0 + 1] = quad_bcast<1>(c);
         cq[q0 + 2] = quad_bcast<2>(c);
@@ -617,7 +648,7 @@ k_walker_rev(KArgs ka) {
     for (int q = 0; q < SM::QM; ++q) {
       if (q >= 4 * QF && q < Q) {
         cq[q] = f_tanh(zc[q] * T(0.25) + convb[q]);
-        if (ilive && (q & 3) == ff) cqv[(l * N + ic) * SM::QM + q] = cq[q];
+        if (ilive && (q & 3) == ff) cqv[SM::cqo(l, ic) + q] = cq[q];
       }
     }
     T z = sngb[ff], z1 = T(0);   // even / odd q: two independent chains
@@ -635,7 +666,7 @@ k_walker_rev(KArgs ka) {
   }
   }
   if (ilive) hl[SM::hoff(3) + ic * 4 + ff] = hreg;
-  __syncthreads();
+  AQ_SYNC();
   if (reuse && lane < 2 * N + 2) sm[SM::pv + lane] = pvr;   // read by the Gauss-Jordan after the Phi barrier
 
   AQ_PH(3);
@@ -661,7 +692,7 @@ k_walker_rev(KArgs ka) {
     Ph[idx * 2 + 0] = re;
     Ph[idx * 2 + 1] = im;
   }
-  if constexpr (!PROP) __syncthreads();   // PROP: one wave, the Gauss-Jordan below forms Phi itself
+  if constexpr (!PROP) AQ_SYNC();   // PROP: one wave, the Gauss-Jordan below forms Phi itself
   T logdet, phr, phi;
   if (reuse) {
     // the walker's pivot order (partial pivoting rerun only if a pivot comes out small)
@@ -736,7 +767,7 @@ k_walker_rev(KArgs ka) {
       return;
     }
   }
-  __syncthreads();
+  AQ_SYNC();
 #define BRE(c, s) Mx[((c) * N + (s)) * 2]
 #define BIM(c, s) Mx[((c) * N + (s)) * 2 + 1]
 
@@ -781,7 +812,7 @@ k_walker_rev(KArgs ka) {
       Lw[LCc::qs + idx * 2 + 1] = qi;
     }
   }
-  __syncthreads();   // ybar overwrites Yt
+  AQ_SYNC();   // ybar overwrites Yt
   if constexpr (!PREP) {
     if (!AQ_ABL(8)) {
       for (int idx = lane; idx < N * N; idx += 64) {
@@ -792,7 +823,7 @@ k_walker_rev(KArgs ka) {
   }
 #undef BRE
 #undef BIM
-  __syncthreads();
+  AQ_SYNC();
 
   AQ_PH(5);
   // ------------------------------------------------------------------ B2 back through the h-stream layers
@@ -835,7 +866,7 @@ k_walker_rev(KArgs ka) {
           T cb = T(0);
 #pragma unroll
           for (int m = 0; m < 4; ++m) cb += zq[m] * sngw[qq * 4 + m];
-          const T c = cqv[(l * N + ic) * SM::QM + qq];
+          const T c = cqv[SM::cqo(l, ic) + qq];
           const T g = cb * (T(1) - c * c) * T(0.25);
           if constexpr (PREP) {
             // conv node (stored once, by the lane of its quad position): tanh', abar * tanh''
@@ -884,7 +915,7 @@ k_walker_rev(KArgs ka) {
       hb = hn;
     }
   }
-  __syncthreads();
+  AQ_SYNC();
 
   if constexpr (PREP) {
     // ---------------------------------------------------------------- local-energy adjoint pass: tail
@@ -1117,7 +1148,7 @@ k_walker_rev(KArgs ka) {
       pair_adjoint(k, jj + (jj >= k ? 1 : 0), true, nullptr);
     }
   }
-  __syncthreads();
+  AQ_SYNC();
 
   AQ_PH(7);
   // ------------------------------------------------------------------ B4 gradient per direction lane (c, e)
