@@ -77,37 +77,47 @@ __global__ __launch_bounds__(256) void k_draws(uint64_t seed, uint64_t step, int
   u[t] = (T)(c[0] - 5.9604644775390625e-08f);   // [0,1)
 }
 
-// DMC drift-diffusion extras (DMC/drift_diffusion.py:15-22), one 1024-thread block, fixed order:
+// DMC reductions run over DMC_NB blocks (partial sums / minima per block in a fixed order), then
+// one thread combines the block results in block order: deterministic, and the chip is not
+// reduced to one block (the single-block forms took 29 us (sum), 72 us (weights) at B = 4096).
+constexpr int DMC_NB = 64;
+
+// DMC drift-diffusion extras (DMC/drift_diffusion.py:15-22):
 // grad != nullptr: out[0] = sum over all coordinates of the proposed configuration
 //   x + limdrift(grad) tau + sqrt(tau) gauss1 (the `changed_configuration` of :66);
 // grad == nullptr: out[1] = sum of x (after acceptance), out[2] = tdamp = out[1] / out[0].
+// k_dmc_sum_part: part[blk] = this block's share; k_dmc_sum_fin: the sum of part[0..DMC_NB) in order.
 template <typename T>
-__global__ __launch_bounds__(1024) void k_dmc_sum(const T* __restrict__ x, const T* __restrict__ grad,
-                                                  const T* __restrict__ g1, const double* __restrict__ taueff,
-                                                  double tstep_d, int n, double* out) {
-  __shared__ double red[1024];
+__global__ __launch_bounds__(256) void k_dmc_sum_part(const T* __restrict__ x, const T* __restrict__ grad,
+                                                      const T* __restrict__ g1, const double* __restrict__ taueff,
+                                                      double tstep_d, int n, double* __restrict__ part) {
+  __shared__ double red[256];
   const T tstep = (T)tstep_d;
   const T sq = sqrt(tstep);
   const T te = grad ? (T)taueff[0] : T(0);
   double acc = 0.0;
-  for (int i = threadIdx.x; i < n; i += 1024) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += 256 * DMC_NB) {
     T v = x[i];
     if (grad) v = v + (grad[i] * te * tstep + sq * g1[i]);
     acc += (double)v;
   }
   red[threadIdx.x] = acc;
   __syncthreads();
-  for (int w = 512; w > 0; w >>= 1) {
+  for (int w = 128; w > 0; w >>= 1) {
     if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    if (grad) {
-      out[0] = red[0];
-    } else {
-      out[1] = red[0];
-      out[2] = red[0] / out[0];
-    }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+__global__ void k_dmc_sum_fin(const double* __restrict__ part, int proposed, double* out) {
+  if (threadIdx.x != 0) return;
+  double a = 0.0;
+  for (int b = 0; b < DMC_NB; ++b) a += part[b];
+  if (proposed) {
+    out[0] = a;
+  } else {
+    out[1] = a;
+    out[2] = a / out[0];
   }
 }
 
@@ -121,14 +131,17 @@ __global__ __launch_bounds__(256) void k_scale_grad(const T* __restrict__ g, con
 
 // DMC energy cut minima (S_matrix.py:21-22): jnp.min over the stacked [|e_est - eloc|, branchcut]
 // array is ONE minimum over every walker (of every device: the reference stacks the pmapped
-// [ndev, B] arrays) and the cut.  out[0] / out[1] = that minimum for eloc_old / eloc_new.
+// [ndev, B] arrays) and the cut.  k_dmc_cut_part: part[2 blk], part[2 blk + 1] = this block's
+// minima for eloc_old / eloc_new (the branch cut included); a minimum is exact in any order, so
+// the consumers take the min over the DMC_NB block results directly.
 // eest_b (nullable): per-walker e_est (the first block, main_dmc.py:115-116), else e_est.
 template <typename T>
-__device__ __forceinline__ void dmc_cut_minima(int B, const T* __restrict__ eold, const T* __restrict__ enew,
-                                               const T* __restrict__ eest_b, double e_est, double branchcut,
-                                               double* mo, double* mn, double& cut_o, double& cut_n) {
+__global__ __launch_bounds__(256) void k_dmc_cut_part(int B, const T* __restrict__ eold, const T* __restrict__ enew,
+                                                      const T* __restrict__ eest_b, double e_est, double branchcut,
+                                                      double* __restrict__ part) {
+  __shared__ double mo[256], mn[256];
   double a = branchcut, b = branchcut;
-  for (int i = threadIdx.x; i < B; i += 1024) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < B; i += 256 * DMC_NB) {
     const double ee = eest_b ? (double)eest_b[i] : e_est;
     a = fmin(a, fabs(ee - (double)eold[i]));
     b = fmin(b, fabs(ee - (double)enew[i]));
@@ -136,88 +149,106 @@ __device__ __forceinline__ void dmc_cut_minima(int B, const T* __restrict__ eold
   mo[threadIdx.x] = a;
   mn[threadIdx.x] = b;
   __syncthreads();
-  for (int s = 512; s > 0; s >>= 1) {
+  for (int s = 128; s > 0; s >>= 1) {
     if ((int)threadIdx.x < s) {
       mo[threadIdx.x] = fmin(mo[threadIdx.x], mo[threadIdx.x + s]);
       mn[threadIdx.x] = fmin(mn[threadIdx.x], mn[threadIdx.x + s]);
     }
     __syncthreads();
   }
-  cut_o = mo[0];
-  cut_n = mn[0];
-}
-
-template <typename T>
-__global__ __launch_bounds__(1024) void k_dmc_cut_minima(int B, const T* __restrict__ eold, const T* __restrict__ enew,
-                                                         const T* __restrict__ eest_b, double e_est, double branchcut,
-                                                         double* __restrict__ out) {
-  __shared__ double mo[1024], mn[1024];
-  double co, cn;
-  dmc_cut_minima<T>(B, eold, enew, eest_b, e_est, branchcut, mo, mn, co, cn);
   if (threadIdx.x == 0) {
-    out[0] = co;
-    out[1] = cn;
+    part[2 * blockIdx.x] = mo[0];
+    part[2 * blockIdx.x + 1] = mn[0];
   }
 }
+__global__ void k_dmc_cut_fin(const double* __restrict__ part, double* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  double a = part[0], b = part[1];
+  for (int k = 1; k < DMC_NB; ++k) {
+    a = fmin(a, part[2 * k]);
+    b = fmin(b, part[2 * k + 1]);
+  }
+  out[0] = a;
+  out[1] = b;
+}
 
-// DMC weights (DMC/S_matrix.py:4-24, dmc.py:80-92), one block:
+// DMC weights (DMC/S_matrix.py:4-24, dmc.py:80-92), one thread per walker:
 //   S = e_trial - e_est + e_cut / (1 + (v2 tau / N)^2), v2 = |grad_eff|^2 per walker,
-//   e_cut = cut * sign(e_est - eloc_b), cut = the global minimum above (computed here from this
-//   batch, or the caller's all-reduced cuts[2] for a multi-device run),
+//   e_cut = cut * sign(e_est - eloc_b), cut = the global minimum above: the caller's all-reduced
+//   cuts[2] (multi-device run), or the min over k_dmc_cut_part's block minima of this batch (cpart),
 //   w *= exp(tau tdamp (S_new + S_old) / 2).
 // etr_b / eest_b (nullable): per-walker e_trial / e_est of the first DMC block.
 template <typename T>
-__global__ __launch_bounds__(1024) void k_dmc_weights(int B, int N, const T* __restrict__ eold, const T* __restrict__ enew,
-                                                      const T* __restrict__ gold, const T* __restrict__ gnew,
-                                                      const double* __restrict__ tdamp, double tau,
-                                                      const T* __restrict__ etr_b, const T* __restrict__ eest_b,
-                                                      double e_trial, double e_est, double branchcut,
-                                                      const double* __restrict__ cuts, T* __restrict__ w) {
-  __shared__ double mo[1024], mn[1024];
+__global__ __launch_bounds__(256) void k_dmc_weights(int B, int N, const T* __restrict__ eold, const T* __restrict__ enew,
+                                                     const T* __restrict__ gold, const T* __restrict__ gnew,
+                                                     const double* __restrict__ tdamp, double tau,
+                                                     const T* __restrict__ etr_b, const T* __restrict__ eest_b,
+                                                     double e_trial, double e_est, const double* __restrict__ cuts,
+                                                     const double* __restrict__ cpart, T* __restrict__ w) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B) return;
   double cut_o, cut_n;
   if (cuts) {
     cut_o = cuts[0];
     cut_n = cuts[1];
   } else {
-    dmc_cut_minima<T>(B, eold, enew, eest_b, e_est, branchcut, mo, mn, cut_o, cut_n);
+    cut_o = cpart[0];
+    cut_n = cpart[1];
+    for (int k = 1; k < DMC_NB; ++k) {
+      cut_o = fmin(cut_o, cpart[2 * k]);
+      cut_n = fmin(cut_n, cpart[2 * k + 1]);
+    }
   }
   const double td = tdamp[2];   // [sum proposed, sum new, tdamp] of aiqmc_dmc_drift_diffusion
-  for (int i = threadIdx.x; i < B; i += 1024) {
-    double vo = 0.0, vn = 0.0;
-    for (int k = 0; k < 3 * N; ++k) {
-      const double x = (double)gold[(size_t)i * 3 * N + k], y = (double)gnew[(size_t)i * 3 * N + k];
-      vo += x * x;
-      vn += y * y;
-    }
-    const double ee = eest_b ? (double)eest_b[i] : e_est;
-    const double et = etr_b ? (double)etr_b[i] : e_trial;
-    const double co = ee - (double)eold[i], cn = ee - (double)enew[i];
-    const double so = et - ee + cut_o * (double)((co > 0) - (co < 0)) / (1.0 + (vo * tau / N) * (vo * tau / N));
-    const double sn = et - ee + cut_n * (double)((cn > 0) - (cn < 0)) / (1.0 + (vn * tau / N) * (vn * tau / N));
-    w[i] = (T)(exp(tau * td * (0.5 * sn + 0.5 * so)) * (double)w[i]);
+  double vo = 0.0, vn = 0.0;
+  for (int k = 0; k < 3 * N; ++k) {
+    const double x = (double)gold[(size_t)i * 3 * N + k], y = (double)gnew[(size_t)i * 3 * N + k];
+    vo += x * x;
+    vn += y * y;
   }
+  const double ee = eest_b ? (double)eest_b[i] : e_est;
+  const double et = etr_b ? (double)etr_b[i] : e_trial;
+  const double co = ee - (double)eold[i], cn = ee - (double)enew[i];
+  const double so = et - ee + cut_o * (double)((co > 0) - (co < 0)) / (1.0 + (vo * tau / N) * (vo * tau / N));
+  const double sn = et - ee + cut_n * (double)((cn > 0) - (cn < 0)) / (1.0 + (vn * tau / N) * (vn * tau / N));
+  w[i] = (T)(exp(tau * td * (0.5 * sn + 0.5 * so)) * (double)w[i]);
 }
 
-// Stochastic comb (DMC/branch.py:10-33), one block: cumulative weights in a fixed order, then
-// newinds[j] = searchsorted_left(cumsum, (u wtot + j wtot / n) mod wtot); wout[0] = wtot / n.
+// Stochastic comb (DMC/branch.py:10-33), one block: cumulative weights in a fixed (sequential)
+// order, then newinds[j] = searchsorted_left(cumsum, (u wtot + j wtot / n) mod wtot);
+// wout[0] = wtot / n.  The running sum is carried by one thread through chunks of the weights
+// staged in LDS (its loads are LDS hits, not dependent global round trips: 196 -> ~15 us at
+// n = 4096); the searches run over the LDS copy when the whole cumsum fits.
 template <typename T>
 __global__ __launch_bounds__(1024) void k_dmc_branch(int n, const T* __restrict__ w, double u, double* __restrict__ csum,
                                                      int32_t* __restrict__ newinds, T* __restrict__ wout) {
-  if (threadIdx.x == 0) {
-    double a = 0.0;
-    for (int i = 0; i < n; ++i) {
-      a += (double)w[i];
-      csum[i] = a;
+  constexpr int COMB_CH = sizeof(T) == 4 ? 4096 : 2048;   // 48 KB of LDS either way
+  __shared__ T ws[COMB_CH];
+  __shared__ double cs[COMB_CH];
+  double a = 0.0;   // thread 0's running sum
+  for (int c0 = 0; c0 < n; c0 += COMB_CH) {
+    const int m = n - c0 < COMB_CH ? n - c0 : COMB_CH;
+    for (int i = threadIdx.x; i < m; i += 1024) ws[i] = w[c0 + i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int i = 0; i < m; ++i) {
+        a += (double)ws[i];
+        cs[i] = a;
+      }
     }
+    __syncthreads();
+    if (n > COMB_CH)
+      for (int i = threadIdx.x; i < m; i += 1024) csum[c0 + i] = cs[i];
+    __syncthreads();
   }
-  __syncthreads();
-  const double wtot = csum[n - 1];
+  const double* cp = n > COMB_CH ? csum : cs;
+  const double wtot = cp[n - 1];
   for (int j = threadIdx.x; j < n; j += 1024) {
     const double t = fmod(u * wtot + (double)j * (wtot / (double)n), wtot);
     int lo = 0, hi = n;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      if (csum[mid] < t) lo = mid + 1;
+      if (cp[mid] < t) lo = mid + 1;
       else hi = mid;
     }
     newinds[j] = lo;
@@ -245,6 +276,12 @@ static bool shape_ops(int N, int A, ShapeOps* ops) {
   AIQMC_SHAPE_LIST(AIQMC_CASE)
 #undef AIQMC_CASE
   return false;
+}
+
+// DMC reduction scratch (2 * DMC_NB doubles), allocated on first use
+static double* dmc_scratch(aiqmc_ctx* c) {
+  if (!c->d_dscr && hipMalloc((void**)&c->d_dscr, 2 * DMC_NB * sizeof(double)) != hipSuccess) c->d_dscr = nullptr;
+  return c->d_dscr;
 }
 
 static hipEvent_t ev_get(aiqmc_ctx* c) {
@@ -448,6 +485,7 @@ int aiqmc_destroy(aiqmc_ctx* c) {
   free_ws(c);
   free_ecp_ws(c);
   if (c->d_tm_scr) (void)hipFree(c->d_tm_scr);
+  if (c->d_dscr) (void)hipFree(c->d_dscr);
   if (c->d_ecp_tab) (void)hipFree(c->d_ecp_tab);
   void* pgp[] = {c->d_gmap, c->d_wnorm, c->d_pg, c->d_pgr};
   for (void* p : pgp)
@@ -660,6 +698,8 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
                     double* dmc, hipStream_t s, AccArgs* pending = nullptr, bool defer = false) {
   const int N = c->N;
   const size_t es = c->dtype == AIQMC_F32 ? 4 : 8;
+  double* dscr = dmc ? dmc_scratch(c) : nullptr;
+  if (dmc && !dscr) return fail(AIQMC_EHIP, "hipMalloc: DMC scratch");
   const char* g1;
   const char* g2;
   const char* uu;
@@ -731,11 +771,12 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
                        c->d_taueff + 1);
   if (dmc) {
     if (c->dtype == AIQMC_F32)
-      k_dmc_sum<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)pos, (const float*)c->d_grad, (const float*)g1,
-                                                       c->d_taueff, tstep, B * 3 * N, dmc);
+      k_dmc_sum_part<float><<<dim3(DMC_NB), dim3(256), 0, s>>>((const float*)pos, (const float*)c->d_grad,
+                                                               (const float*)g1, c->d_taueff, tstep, B * 3 * N, dscr);
     else
-      k_dmc_sum<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)pos, (const double*)c->d_grad,
-                                                        (const double*)g1, c->d_taueff, tstep, B * 3 * N, dmc);
+      k_dmc_sum_part<double><<<dim3(DMC_NB), dim3(256), 0, s>>>((const double*)pos, (const double*)c->d_grad,
+                                                                (const double*)g1, c->d_taueff, tstep, B * 3 * N, dscr);
+    k_dmc_sum_fin<<<dim3(1), dim3(64), 0, s>>>(dscr, 1, dmc);
   }
   // (5) acceptance and move (:83-106)
   AccArgs a;
@@ -756,11 +797,12 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
   ops.accept(c->dtype, pos, a, B, s);
   if (dmc) {
     if (c->dtype == AIQMC_F32)
-      k_dmc_sum<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)pos, nullptr, nullptr, nullptr, tstep, B * 3 * N,
-                                                       dmc);
+      k_dmc_sum_part<float><<<dim3(DMC_NB), dim3(256), 0, s>>>((const float*)pos, nullptr, nullptr, nullptr, tstep,
+                                                               B * 3 * N, dscr);
     else
-      k_dmc_sum<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)pos, nullptr, nullptr, nullptr, tstep,
-                                                        B * 3 * N, dmc);
+      k_dmc_sum_part<double><<<dim3(DMC_NB), dim3(256), 0, s>>>((const double*)pos, nullptr, nullptr, nullptr, tstep,
+                                                                B * 3 * N, dscr);
+    k_dmc_sum_fin<<<dim3(1), dim3(64), 0, s>>>(dscr, 0, dmc);
   }
   return 0;
 }
@@ -823,7 +865,8 @@ static int param_grad(aiqmc_ctx* c, const void* pos, int32_t B, const void* weig
     c->d_pg = c->d_pgr = nullptr;
     c->pg_B = 0;
     HIPCHK(hipMalloc(&c->d_pg, (size_t)B * c->nkern * es));
-    HIPCHK(hipMalloc(&c->d_pgr, (size_t)c->nkern * es));
+    // row 0: the weighted sum; rows 1..: k_grad_partial's per-chunk sums
+    HIPCHK(hipMalloc(&c->d_pgr, (size_t)(1 + (B + GR_CH - 1) / GR_CH) * c->nkern * es));
     c->pg_B = B;
   }
   hipStream_t s = (hipStream_t)stream;
@@ -840,12 +883,17 @@ static int param_grad(aiqmc_ctx* c, const void* pos, int32_t B, const void* weig
   const void* G = c->d_pg;
   int rows = B;
   if (weights) {
-    if (c->dtype == AIQMC_F32)
-      k_grad_reduce<float><<<dim3((nk + 63) / 64), dim3(256), 0, s>>>((const float*)c->d_pg, (const float*)weights, B,
-                                                                     nk, (float*)c->d_pgr);
-    else
-      k_grad_reduce<double><<<dim3((nk + 63) / 64), dim3(256), 0, s>>>((const double*)c->d_pg, (const double*)weights,
-                                                                      B, nk, (double*)c->d_pgr);
+    const int nch = (B + GR_CH - 1) / GR_CH;
+    const dim3 gp((nk + 63) / 64, nch), gf((nk + 255) / 256);
+    if (c->dtype == AIQMC_F32) {
+      float* pr = (float*)c->d_pgr;
+      k_grad_partial<float><<<gp, dim3(256), 0, s>>>((const float*)c->d_pg, (const float*)weights, B, nk, pr + nk);
+      k_grad_final<float><<<gf, dim3(256), 0, s>>>(pr + nk, nch, nk, pr);
+    } else {
+      double* pr = (double*)c->d_pgr;
+      k_grad_partial<double><<<gp, dim3(256), 0, s>>>((const double*)c->d_pg, (const double*)weights, B, nk, pr + nk);
+      k_grad_final<double><<<gf, dim3(256), 0, s>>>(pr + nk, nch, nk, pr);
+    }
     G = c->d_pgr;
     rows = 1;
   }
@@ -1158,17 +1206,29 @@ int aiqmc_dmc_weights_ex(aiqmc_ctx* c, int32_t B, const void* eloc_old, const vo
     return fail(AIQMC_EINVAL, "null argument");
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
+  const double* cpart = nullptr;
+  if (!cut_minima) {   // this batch's minima (single device)
+    double* d = dmc_scratch(c);
+    if (!d) return fail(AIQMC_EHIP, "hipMalloc: DMC scratch");
+    if (c->dtype == AIQMC_F32)
+      k_dmc_cut_part<float><<<dim3(DMC_NB), dim3(256), 0, s>>>(B, (const float*)eloc_old, (const float*)eloc_new,
+                                                               (const float*)e_est_b, e_est, branchcut, d);
+    else
+      k_dmc_cut_part<double><<<dim3(DMC_NB), dim3(256), 0, s>>>(B, (const double*)eloc_old, (const double*)eloc_new,
+                                                                (const double*)e_est_b, e_est, branchcut, d);
+    cpart = d;
+  }
+  const dim3 gw((B + 255) / 256);
   if (c->dtype == AIQMC_F32)
-    k_dmc_weights<float><<<dim3(1), dim3(1024), 0, s>>>(B, c->N, (const float*)eloc_old, (const float*)eloc_new,
-                                                         (const float*)grad_eff_old, (const float*)grad_new_eff, tdamp,
-                                                         tstep, (const float*)e_trial_b, (const float*)e_est_b, e_trial,
-                                                         e_est, branchcut, cut_minima, (float*)weights_inout);
+    k_dmc_weights<float><<<gw, dim3(256), 0, s>>>(B, c->N, (const float*)eloc_old, (const float*)eloc_new,
+                                                  (const float*)grad_eff_old, (const float*)grad_new_eff, tdamp, tstep,
+                                                  (const float*)e_trial_b, (const float*)e_est_b, e_trial, e_est,
+                                                  cut_minima, cpart, (float*)weights_inout);
   else
-    k_dmc_weights<double><<<dim3(1), dim3(1024), 0, s>>>(B, c->N, (const double*)eloc_old, (const double*)eloc_new,
-                                                          (const double*)grad_eff_old, (const double*)grad_new_eff,
-                                                          tdamp, tstep, (const double*)e_trial_b, (const double*)e_est_b,
-                                                          e_trial, e_est, branchcut, cut_minima,
-                                                          (double*)weights_inout);
+    k_dmc_weights<double><<<gw, dim3(256), 0, s>>>(B, c->N, (const double*)eloc_old, (const double*)eloc_new,
+                                                   (const double*)grad_eff_old, (const double*)grad_new_eff, tdamp,
+                                                   tstep, (const double*)e_trial_b, (const double*)e_est_b, e_trial,
+                                                   e_est, cut_minima, cpart, (double*)weights_inout);
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
 }
@@ -1187,12 +1247,15 @@ int aiqmc_dmc_cut_minima(aiqmc_ctx* c, int32_t B, const void* eloc_old, const vo
   if (!out || (B > 0 && (!eloc_old || !eloc_new))) return fail(AIQMC_EINVAL, "null argument");
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
+  double* d = dmc_scratch(c);
+  if (!d) return fail(AIQMC_EHIP, "hipMalloc: DMC scratch");
   if (c->dtype == AIQMC_F32)
-    k_dmc_cut_minima<float><<<dim3(1), dim3(1024), 0, s>>>(B, (const float*)eloc_old, (const float*)eloc_new,
-                                                            (const float*)e_est_b, e_est, branchcut, out);
+    k_dmc_cut_part<float><<<dim3(DMC_NB), dim3(256), 0, s>>>(B, (const float*)eloc_old, (const float*)eloc_new,
+                                                             (const float*)e_est_b, e_est, branchcut, d);
   else
-    k_dmc_cut_minima<double><<<dim3(1), dim3(1024), 0, s>>>(B, (const double*)eloc_old, (const double*)eloc_new,
-                                                             (const double*)e_est_b, e_est, branchcut, out);
+    k_dmc_cut_part<double><<<dim3(DMC_NB), dim3(256), 0, s>>>(B, (const double*)eloc_old, (const double*)eloc_new,
+                                                              (const double*)e_est_b, e_est, branchcut, d);
+  k_dmc_cut_fin<<<dim3(1), dim3(64), 0, s>>>(d, out);
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
 }

@@ -58,6 +58,7 @@ struct aiqmc_ctx {
        *d_ecp_el = nullptr, *d_ecp_lp0 = nullptr, *d_ecp_ph0 = nullptr;
   int64_t ecp_bytes = 0;
   double* d_tm_scr = nullptr;      // T-moves per-walker amplitudes [tm_B][N*A*50][4]
+  double* d_dscr = nullptr;        // DMC reduction scratch: block partial sums / cut minima [2*64]
   int tm_B = 0;
   // parameter gradients (aiqmc_logpsi_param_grad, walker_pgrad.h)
   int* d_gmap = nullptr;            // [ncanon]

@@ -530,20 +530,45 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
   if (lane == 0 && ka.phase) ((T*)ka.phase)[conf] = f_atan2(phi, phr);
 }
 
-// out[j] = sum_b w[b] O[b][j] over the kernel layout (deterministic order): one block of 256
-// threads per 64 columns, thread (t / 64) strides the walkers.
+// out[j] = sum_b w[b] O[b][j] over the kernel layout, deterministic, in two launches:
+// k_grad_partial: block (x, c) sums walkers [c*GR_CH, (c+1)*GR_CH) of columns 64x .. 64x+63
+// (four waves stride the chunk, combined in wave order) -> part[c][j];
+// k_grad_final: out[j] = sum_c part[c][j] in chunk order.  (One block per 64 columns over all
+// walkers took 261 us for B = 4096 and 12 blocks; the chunked form fills the chip.)
+constexpr int GR_CH = 64;
 template <typename T>
-__global__ __launch_bounds__(256) void k_grad_reduce(const T* __restrict__ O, const T* __restrict__ w, int B, int n,
-                                                     T* __restrict__ out) {
-  __shared__ T part[4][64];
+__global__ __launch_bounds__(256) void k_grad_partial(const T* __restrict__ O, const T* __restrict__ w, int B, int n,
+                                                      T* __restrict__ part) {
+  __shared__ T ps[4][64];
   const int j = blockIdx.x * 64 + (threadIdx.x & 63);
   const int s = threadIdx.x >> 6;
-  T a = T(0);
-  if (j < n)
-    for (int b = s; b < B; b += 4) a += w[b] * O[(size_t)b * n + j];
-  part[s][threadIdx.x & 63] = a;
+  const int b0 = blockIdx.y * GR_CH, b1 = b0 + GR_CH < B ? b0 + GR_CH : B;
+  T a = T(0), a1 = T(0);
+  if (j < n) {
+    int b = b0 + s;
+    for (; b + 4 < b1; b += 8) {
+      a += w[b] * O[(size_t)b * n + j];
+      a1 += w[b + 4] * O[(size_t)(b + 4) * n + j];
+    }
+    if (b < b1) a += w[b] * O[(size_t)b * n + j];
+  }
+  ps[s][threadIdx.x & 63] = a + a1;
   __syncthreads();
-  if (s == 0 && j < n) out[j] = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
+  if (s == 0 && j < n)
+    part[(size_t)blockIdx.y * n + j] = (ps[0][threadIdx.x] + ps[1][threadIdx.x]) + (ps[2][threadIdx.x] + ps[3][threadIdx.x]);
+}
+template <typename T>
+__global__ __launch_bounds__(256) void k_grad_final(const T* __restrict__ part, int nchunk, int n, T* __restrict__ out) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  T a[4] = {T(0), T(0), T(0), T(0)};
+  int c = 0;
+  for (; c + 3 < nchunk; c += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] += part[(size_t)(c + u) * n + j];
+  }
+  for (; c < nchunk; ++c) a[0] += part[(size_t)c * n + j];
+  out[j] = (a[0] + a[1]) + (a[2] + a[3]);
 }
 
 // Kernel layout -> canonical (tree_flatten) order for `rows` gradient vectors.  map[k] >= 0: the
