@@ -7,6 +7,7 @@
 
 #include "ctx.h"
 #include "walker_lap.h"
+#include "quad_small.h"
 #include "walker_pgrad.h"
 
 using namespace aq;
@@ -232,8 +233,23 @@ static int set_lds_impl() {
 
 // MODE_GRAD -> reverse-mode value+gradient kernel (walker_rev.h); MODE_LAP -> forward
 // Laplacian kernel (walker_kernel.h); MODE_GRAD_FWD -> forward-mode gradient (diagnostics).
+// value-only single-electron-moved configurations from the walker cache (pp quadrature), N <= 4:
+// four configurations per wave (quad_small.h)
+template <typename T, int N, int A>
+static bool quad_small(const KArgs& ka, int nconf, hipStream_t s) {
+  if constexpr (N <= 4) {
+    if (ka.proposal && ka.ecache && ka.value_only && !ka.orb) {
+      k_quad_value<T, N, A><<<dim3((nconf + 3) / 4), dim3(64), 0, s>>>(ka);
+      return true;
+    }
+  }
+  return false;
+}
+
 template <int N, int A>
 static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStream_t s) {
+  if (mode == MODE_GRAD && (dtype == AIQMC_F32 ? quad_small<float, N, A>(ka, nconf, s) : quad_small<double, N, A>(ka, nconf, s)))
+    return;
   if (dtype == AIQMC_F32) {
     if (mode == MODE_LAP)
       k_walker<float, N, A, MODE_LAP><<<dim3(nconf), dim3(64), Smem<float, N, true>::bytes, s>>>(ka);
