@@ -258,7 +258,9 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
                                               dim3(64 * RevWpb<float, true>::value),
                                               RevWpb<float, true>::value * SmemRev<float, N, A>::bytes, s>>>(ka);
     else if (mode == MODE_GRAD)
-      k_walker_rev<float, N, A><<<dim3(nconf), dim3(64), SmemRev<float, N, A>::bytes, s>>>(ka);
+      k_walker_rev<float, N, A><<<dim3((nconf + RevWpb<float, false>::value - 1) / RevWpb<float, false>::value),
+                                  dim3(64 * RevWpb<float, false>::value),
+                                  RevWpb<float, false>::value * SmemRev<float, N, A>::bytes, s>>>(ka);
     else
       k_walker<float, N, A, MODE_GRAD><<<dim3(nconf), dim3(64), Smem<float, N, false>::bytes, s>>>(ka);
   } else {

@@ -254,10 +254,13 @@ template <typename T, int N, int A, bool PREP, bool PROP> struct RevWaves {
 // Proposal launches: AQ_PROP_WPB configurations (one wave each) per workgroup; the waves share
 // nothing, so their LDS regions are disjoint and every barrier is wave-local.
 #ifndef AQ_PROP_WPB
-#define AQ_PROP_WPB 2
+#define AQ_PROP_WPB 4
 #endif
-template <typename T, bool PROP> struct RevWpb {
-  static constexpr int value = (PROP && sizeof(T) == 4) ? AQ_PROP_WPB : 1;
+#ifndef AQ_WALK_WPB
+#define AQ_WALK_WPB 1
+#endif
+template <typename T, bool PROP, bool PREP = false> struct RevWpb {
+  static constexpr int value = sizeof(T) != 4 ? 1 : (PROP ? AQ_PROP_WPB : (PREP ? 1 : AQ_WALK_WPB));
 };
 // Barrier of a one-configuration wave: LDS traffic of one wave is processed in order, so a
 // wavefront-scope fence (a compiler barrier, no s_waitcnt) orders its cross-lane LDS accesses.
@@ -277,13 +280,13 @@ __device__ __forceinline__ void wave_sync() {
 #endif
 
 template <typename T, int N, int A, bool PREP = false, bool PROP = false>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * RevWpb<T, PROP>::value))) __attribute__((amdgpu_waves_per_eu(RevWaves<T, N, A, PREP, PROP>::value))) void
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * RevWpb<T, PROP, PREP>::value))) __attribute__((amdgpu_waves_per_eu(RevWaves<T, N, A, PREP, PROP>::value))) void
 k_walker_rev(KArgs ka) {
   using Ly = Lay<N, A>;
   using SM = SmemRev<T, N, A>;
   using LCc = LapCache<N, A>;
   constexpr int D0 = SM::D0;
-  constexpr int WPB = RevWpb<T, PROP>::value;
+  constexpr int WPB = RevWpb<T, PROP, PREP>::value;
   const cptr<T> P = param_ptr<T>(ka.prm);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   // wave index within the workgroup, wave-uniform (scalar)
@@ -368,33 +371,45 @@ k_walker_rev(KArgs ka) {
     T ry[NY], rh[NHh], rg[NG];
     // PROP: F0's positions too (walker pb's, the moved electron's proposed position from
     // k_moved_electron), so that every global load of F0/F1 is in flight before one barrier
+    // Every load is issued unconditionally at a clamped, in-bounds index and the moved electron's
+    // entries are selected afterwards: no divergent branch (exec-mask save/restore) per element.
     const bool mvl = lane < 3 * N && lane / 3 == pi;
     T x0 = T(0), xm = T(0);
     if constexpr (PROP) {
-      if (lane < 3 * N) x0 = ((const T*)ka.pos)[(size_t)pb * 3 * N + lane];
-      if (mvl) xm = Eq[EC::xp + (lane - 3 * pi)];
+      const int l3 = lane < 3 * N ? lane : 3 * N - 1;
+      x0 = ((const T*)ka.pos)[(size_t)pb * 3 * N + l3];
+      xm = Eq[EC::xp + (mvl ? lane - 3 * pi : 0)];
     }
 #pragma unroll
     for (int t = 0; t < NY; ++t) {
       const int idx = lane + 64 * t;
-      const int r = idx / N;
-      ry[t] = idx < N * N ? ((r == pi) ? Eq[EC::yv + (idx - r * N)] : Wc[WC::yv + idx]) : T(0);
+      const int ix = idx < N * N ? idx : N * N - 1;
+      const int r = ix / N;
+      const T a = Wc[WC::yv + ix], b = Eq[EC::yv + (ix - r * N)];
+      ry[t] = (r == pi) ? b : a;
     }
 #pragma unroll
     for (int t = 0; t < NHh; ++t) {
       const int idx = lane + 64 * t;
-      const int e = idx / D0;
-      rh[t] = idx < N * D0 ? ((e == pi) ? Eq[EC::h0 + (idx - e * D0)] : Wc[WC::h0 + idx]) : T(0);
+      const int ix = idx < N * D0 ? idx : N * D0 - 1;
+      const int e = ix / D0;
+      const T a = Wc[WC::h0 + ix], b = Eq[EC::h0 + (ix - e * D0)];
+      rh[t] = (e == pi) ? b : a;
     }
 #pragma unroll
     for (int t = 0; t < NG; ++t) {
       const int idx = lane + 64 * t;
-      rg[t] = idx < 3 * 2 * N * 4 ? Wc[WC::g2 + idx] : T(0);
+      rg[t] = Wc[WC::g2 + (idx < 3 * 2 * N * 4 ? idx : 3 * 2 * N * 4 - 1)];
     }
-    jv = (val && live) ? ((er == pi) ? Eq[EC::jv] : Wc[WC::jaev + er]) : T(0);
-    jd1 = dir ? ((le == pi) ? Eq[EC::jd + lc] : Wc[WC::jaed + lane]) : T(0);
-    jve = lane == 0 ? Wc[WC::jee] : T(0);
-    pvr = lane < 2 * N + 2 ? Wc[WC::pv + lane] : T(0);   // to LDS after F4 (SmemRev::pv)
+    {
+      const T a = Wc[WC::jaev + le], b = Eq[EC::jv];
+      jv = (val && live) ? ((er == pi) ? b : a) : T(0);
+      const T a1 = Wc[WC::jaed + (lane < 48 ? lane : 47)], b1 = Eq[EC::jd + (lc < 3 ? lc : 0)];
+      jd1 = dir ? ((le == pi) ? b1 : a1) : T(0);
+      const T a2 = Wc[WC::jee];
+      jve = lane == 0 ? a2 : T(0);
+      pvr = Wc[WC::pv + (lane < 2 * N + 2 ? lane : 2 * N + 1)];   // to LDS after F4 (SmemRev::pv)
+    }
     if constexpr (PROP) {
       if (mvl) sm[SM::R + (lane - 3 * pi)] = x0;             // old position of the moved electron
       if (lane < 3 * N) xs[lane] = mvl ? xm : x0;
