@@ -53,8 +53,11 @@ struct SmemQ {
   static constexpr int size = h3 + 16;
 };
 
+// waves per workgroup (independent; the launch pays per workgroup, see walker_rev.h AQ_PROP_WPB)
+constexpr int QUAD_WPB = 1;   // 4 measured 0.354 vs 0.346 ms (C atom): per-workgroup cost is not the limit here
+
 template <typename T, int N, int A>
-__global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
+__global__ __launch_bounds__(64 * QUAD_WPB) void k_quad_value(KArgs ka) {
   static_assert(N <= 4, "four configurations per wave need N <= 4");
   using Ly = Lay<N, A>;
   using WC = WCache<N, A>;
@@ -62,13 +65,14 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
   using SQ = SmemQ<T, N, A>;
   constexpr int D0 = 4 * A;
   const cptr<T> P = param_ptr<T>(ka.prm);
-  __shared__ T smq[4 * SQ::size];
-  const int lane = threadIdx.x;
+  __shared__ T smq[QUAD_WPB * 4 * SQ::size];
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
   const int slot = lane >> 4, sl = lane & 15;
-  const int c0 = xcd_major(blockIdx.x, gridDim.x) * 4 + slot;
+  const int c0 = (xcd_major(blockIdx.x, gridDim.x) * QUAD_WPB + wv) * 4 + slot;
   const bool act = c0 < ka.nconf;
   const int conf = act ? c0 : ka.nconf - 1;
-  T* sm = smq + slot * SQ::size;
+  T* sm = smq + (wv * 4 + slot) * SQ::size;
   T* xs = sm + SQ::xs;
   T* Yv = sm + SQ::yv;
   T* hl = sm + SQ::hl;

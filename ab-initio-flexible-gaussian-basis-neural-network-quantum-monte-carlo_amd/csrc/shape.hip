@@ -228,6 +228,14 @@ static int set_lds_impl() {
       if (e != hipSuccess) return fail(AIQMC_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
     }
   }
+  {   // proposal launches: RevWpb configurations per workgroup
+    const int pb = RevWpb<float, true>::value * SmemRev<float, N, A>::bytes;
+    if (pb > 65536) {
+      hipError_t e = hipFuncSetAttribute((const void*)&k_walker_rev<float, N, A, false, true>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, pb);
+      if (e != hipSuccess) return fail(AIQMC_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+    }
+  }
   return 0;
 }
 
@@ -239,7 +247,7 @@ template <typename T, int N, int A>
 static bool quad_small(const KArgs& ka, int nconf, hipStream_t s) {
   if constexpr (N <= 4) {
     if (ka.proposal && ka.ecache && ka.value_only && !ka.orb) {
-      k_quad_value<T, N, A><<<dim3((nconf + 3) / 4), dim3(64), 0, s>>>(ka);
+      k_quad_value<T, N, A><<<dim3((nconf + 4 * QUAD_WPB - 1) / (4 * QUAD_WPB)), dim3(64 * QUAD_WPB), 0, s>>>(ka);
       return true;
     }
   }

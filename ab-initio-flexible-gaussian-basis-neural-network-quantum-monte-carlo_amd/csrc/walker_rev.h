@@ -239,8 +239,11 @@ __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
 #ifndef AQ_PROP_WAVES
 #define AQ_PROP_WAVES 5
 #endif
+#ifndef AQ_PREP_WAVES
+#define AQ_PREP_WAVES 4
+#endif
 template <typename T, int N, int A, bool PREP, bool PROP> struct RevWaves {
-  static constexpr int value = PREP ? 2 : ((sizeof(T) == 4 && N == 14 && A == 2) ? (PROP ? AQ_PROP_WAVES : 4) : 1);
+  static constexpr int value = PREP ? (sizeof(T) == 4 ? AQ_PREP_WAVES : 2) : ((sizeof(T) == 4 && N == 14 && A == 2) ? (PROP ? AQ_PROP_WAVES : 4) : 1);
 };
 
 // PREP = false: value + gradient (Metropolis walker launches and single-electron proposal / ECP
