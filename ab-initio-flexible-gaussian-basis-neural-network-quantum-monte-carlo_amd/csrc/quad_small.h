@@ -315,4 +315,509 @@ __global__ __launch_bounds__(64 * QUAD_WPB) void k_quad_value(KArgs ka) {
   }
 }
 
+
+// ============================================================================================
+// k_quad_grad: the Metropolis proposals of N <= 4 electrons (Be, the C atom's pseudo-valence
+// electrons), value AND gradient, four configurations per wave (one 16-lane row each) --
+// k_walker_rev's PROP path (walker_rev.h) restated in the row layout:
+//   F1/F2/F4 as k_quad_value, keeping the conv and single-layer outputs for the backward pass;
+//   F5 Phi (x) Yt and its inverse by Gauss-Jordan with partial pivoting (izamax rule, virtual
+//      row exchanges, gj_inverse's arithmetic) in the row's first quad, lane c = column c;
+//   B1 dL/dh^3 = Re Q_f[r,r], dL/dYt = Re(B^T (x) Phi)   (lanes 4r + f / the N^2 entries);
+//   B2 back through the three layers (lane 4i + f, class sums inside the row);
+//   B3 the N(N-1) pair adjoints (lane = ordered pair, forward values recomputed: 12 pairs);
+//   B4 d log|psi| / d x_{e,c} on lane 4c + e from the pair adjoints and the electron-local
+//      Jacobians (walker cache, or the moved electron's record).
+// Outputs as the proposal path: log|psi|, |grad|^2, the moved electron's own gradient (and
+// the full gradient / phase when asked).
+template <typename T, int N, int A>
+struct SmemQG {
+  static constexpr int D0 = 4 * A;
+  static constexpr int QM = (3 * D0 + 8) / 4;    // conv outputs of layer 0
+  static constexpr int QL = (3 * 4 + 8) / 4;     // conv outputs of layers 1, 2
+  static constexpr int xs = 0;                   // [12] positions; [12..15] old position of the moved electron
+  static constexpr int xo = 12;
+  static constexpr int yv = 16;                  // [N][N] Yt, then its adjoint
+  static constexpr int hl = yv + 16;             // h^0 [4][D0], h^3 [4][4]; then their adjoints
+  static constexpr int h3 = hl + 4 * D0;
+  static constexpr int g2 = h3 + 16;             // [3][2][N][4] pair column means, then their adjoints
+  static constexpr int S = g2 + 96;              // [16][12] patch pair values; then dbar [N][N][3]
+  static constexpr int cq = S + 192;             // conv outputs [4][QM] + [2][4][QL]
+  static constexpr int sv = cq + 4 * QM + 8 * QL;   // [3][4][4] single outputs
+  static constexpr int ph = sv + 48;             // [N][N][2] Phi
+  static constexpr int mx = ph + 32;             // [N][N][2] B = A^{-1}
+  static constexpr int size = mx + 32;
+  static constexpr int cqo(int l, int i) { return l == 0 ? i * QM : 4 * QM + ((l - 1) * 4 + i) * QL; }
+};
+
+template <typename T, int N, int A>
+__global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
+  static_assert(N <= 4, "four configurations per wave need N <= 4");
+  using Ly = Lay<N, A>;
+  using WC = WCache<N, A>;
+  using EC = ECache<N, A>;
+  using SQ = SmemQG<T, N, A>;
+  constexpr int D0 = 4 * A;
+  constexpr int QM = SQ::QM;
+  const cptr<T> P = param_ptr<T>(ka.prm);
+  __shared__ T smq[4 * SQ::size];
+  const int lane = threadIdx.x;
+  const int slot = lane >> 4, sl = lane & 15;
+  const int c0 = xcd_major(blockIdx.x, gridDim.x) * 4 + slot;
+  const bool act = c0 < ka.nconf;
+  const int conf = act ? c0 : ka.nconf - 1;
+  T* sm = smq + slot * SQ::size;
+  T* xs = sm + SQ::xs;
+  T* Yv = sm + SQ::yv;
+  T* hl = sm + SQ::hl;
+  T* H3 = sm + SQ::h3;
+  T* g2 = sm + SQ::g2;
+  T* S = sm + SQ::S;
+  T* cqv = sm + SQ::cq;
+  T* svv = sm + SQ::sv;
+  T* Ph = sm + SQ::ph;
+  T* Mx = sm + SQ::mx;
+  const int mper = ka.mper ? ka.mper : N, mdiv = ka.mdiv ? ka.mdiv : 1;
+  const int pb = conf / mper, pi = (conf - pb * mper) / mdiv;
+  const int nup = ka.nup;
+  const int* rowsrc = ka.rowsrc;
+  const T RSQ2 = T(0.70710678118654752);
+  const T ginv0 = T(1) / T(nup), ginv1 = T(1) / T(N - nup);
+  const T* Wc = (const T*)ka.wcache + (size_t)pb * WC::size;
+  const T* Eq = (const T*)ka.ecache + (size_t)conf * EC::size;
+
+  // ---------------------------------------------------------------- F1 cached stage of walker pb
+  if (sl < 3 * N) {
+    const T x0 = ((const T*)ka.pos)[(size_t)pb * 3 * N + sl];
+    const bool mv = sl / 3 == pi;
+    if (mv) sm[SQ::xo + sl - 3 * pi] = x0;
+    xs[sl] = mv ? Eq[EC::xp + sl - 3 * pi] : x0;
+  }
+  if (sl < N * N) {
+    const int r = sl / N;
+    Yv[sl] = r == pi ? Eq[EC::yv + sl - r * N] : Wc[WC::yv + sl];
+  }
+  for (int idx = sl; idx < N * D0; idx += 16) {
+    const int e = idx / D0;
+    hl[idx] = e == pi ? Eq[EC::h0 + idx - e * D0] : Wc[WC::h0 + idx];
+  }
+  for (int idx = sl; idx < 3 * 2 * N * 4; idx += 16) g2[idx] = Wc[WC::g2 + idx];
+  T jsum = sl < N ? (sl == pi ? Eq[EC::jv] : Wc[WC::jaev + sl]) : T(0);
+  if (sl == 0) jsum += Wc[WC::jee];
+  wave_sync();
+
+  // ---------------------------------------------------------------- F2 pairs of the moved electron
+  {
+    const int part = sl >> 2, o = sl & 3;
+    const int os = o < N ? o : N - 1;
+    const T* xp = (part & 1) ? sm + SQ::xo : xs + pi * 3;
+    T d[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) d[c] = part < 2 ? xs[os * 3 + c] - xp[c] : xp[c] - xs[os * 3 + c];
+    T v[3][4];
+    pair_values<T, N, A>(d, P, v);
+#pragma unroll
+    for (int l = 0; l < 3; ++l)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) S[sl * 12 + l * 4 + f] = v[l][f];
+    if (part < 2 && o < N && o != pi) {
+      const T cusp = P[Ly::jee_c + pi * N + o], al = P[Ly::jee_a + pi * N + o];
+      const T je = f_div(cusp * v[0][0], al * v[0][0] + T(1));
+      jsum += part == 0 ? je : -je;
+    }
+  }
+  wave_sync();
+  if (sl < N && sl != pi) {
+    const int Gp = pi >= nup ? 1 : 0;
+    const T gw = Gp ? ginv1 : ginv0;
+#pragma unroll
+    for (int l = 0; l < 3; ++l)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+        g2[((l * 2 + Gp) * N + sl) * 4 + f] += (S[sl * 12 + l * 4 + f] - S[(4 + sl) * 12 + l * 4 + f]) * gw;
+  }
+#pragma unroll
+  for (int t0 = 0; t0 < 24; t0 += 16) {
+    const int t = t0 + sl;
+    if (t < 24) {
+      const int l = t >> 3, G = (t >> 2) & 1, f = t & 3;
+      const int k0 = G ? nup : 0, k1 = G ? N : nup;
+      T acc = T(0);
+      for (int k = k0; k < k1; ++k)
+        if (k != pi) acc += S[(8 + k) * 12 + l * 4 + f] - S[(12 + k) * 12 + l * 4 + f];
+      g2[((l * 2 + G) * N + pi) * 4 + f] += acc * (G ? ginv1 : ginv0);
+    }
+  }
+  wave_sync();
+
+  // ---------------------------------------------------------------- F4 h-stream layers (values kept)
+  const int fi = sl >> 2, ff = sl & 3;
+  const bool ilive = fi < N;
+  const int ic = ilive ? fi : N - 1;
+  const bool inG1 = ic >= nup;
+  T hreg = T(0);
+#pragma unroll
+  for (int l = 0; l < 3; ++l) {
+    const int d1 = l == 0 ? D0 : NH;
+    const int DF = 3 * d1 + 8;
+    const int Q = DF / 4;
+    const int T4 = d1 / 4;
+    const cptr<T> convw = P + (l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2)) + ic * DF;
+    const cptr<T> convb = P + (l == 0 ? Ly::conv_b0 : (l == 1 ? Ly::conv_b1 : Ly::conv_b2)) + ic * Q;
+    const cptr<T> sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
+    const cptr<T> sngb = P + (l == 0 ? Ly::sng_b0 : (l == 1 ? Ly::sng_b1 : Ly::sng_b2));
+    T hown[D0 / 4];
+#pragma unroll
+    for (int t = 0; t < D0 / 4; ++t) hown[t] = l == 0 ? hl[ic * D0 + ff + 4 * t] : hreg;
+    T gown[2][D0 / 4];
+#pragma unroll
+    for (int t = 0; t < D0 / 4; ++t) {
+      if (t < T4) {
+        const T x = ilive ? hown[t] : T(0);
+        gown[0][t] = row_class4_sum(inG1 ? T(0) : x) * ginv0;
+        gown[1][t] = row_class4_sum(inG1 ? x : T(0)) * ginv1;
+      }
+    }
+    T zc[QM];
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+      if (q < Q) {
+        T F;
+        if (q < T4) F = hown[q];
+        else if (q < 3 * T4) F = gown[(q - T4) / T4][(q - T4) % T4];
+        else F = g2[((l * 2 + (q - 3 * T4)) * N + ic) * 4 + ff];
+        T z = F * convw[4 * q + ff];
+        z += dpp<0xB1>(z);
+        z += dpp<0x4E>(z);
+        zc[q] = z;
+      }
+    }
+    const int QF = Q / 4;
+    T cq[QM];
+#pragma unroll
+    for (int s4 = 0; s4 < QM / 4; ++s4) {
+      if (s4 < QF) {
+        const int q0 = 4 * s4;
+        const T zs = ff == 0 ? zc[q0] : (ff == 1 ? zc[q0 + 1] : (ff == 2 ? zc[q0 + 2] : zc[q0 + 3]));
+        const T c = f_tanh(zs * T(0.25) + convb[q0 + ff]);
+        if (ilive) cqv[SQ::cqo(l, ic) + q0 + ff] = c;
+        cq[q0 + 0] = quad_bcast<0>(c);
+        cq[q0 + 1] = quad_bcast<1>(c);
+        cq[q0 + 2] = quad_bcast<2>(c);
+        cq[q0 + 3] = quad_bcast<3>(c);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < QM; ++q)
+      if (q >= 4 * QF && q < Q) {
+        cq[q] = f_tanh(zc[q] * T(0.25) + convb[q]);
+        if (ilive && (q & 3) == ff) cqv[SQ::cqo(l, ic) + q] = cq[q];
+      }
+    T z = sngb[ff], z1 = T(0);
+#pragma unroll
+    for (int q = 0; q < QM; ++q)
+      if (q < Q) {
+        if (q & 1) z1 += cq[q] * sngw[q * 4 + ff];
+        else z += cq[q] * sngw[q * 4 + ff];
+      }
+    z += z1;
+    const T sval = f_tanh(z);
+    if (ilive) svv[(l * 4 + ic) * 4 + ff] = sval;
+    const T hin = l == 0 ? hl[ic * D0 + ff] : hreg;
+    hreg = (d1 == NH) ? (hin + sval) * RSQ2 : sval;
+  }
+  if (ilive) H3[ic * 4 + ff] = hreg;
+  wave_sync();
+
+  // ---------------------------------------------------------------- F5 Phi, A = Phi (x) Yt, B = A^{-1}
+  T lsum = T(0), ur = T(1), ui = T(0);
+  int inv = 0;
+  if (sl < 4) {
+    const int c = sl;
+    T ar[4], ai[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      T a = T(0), b = T(0);
+      if (r < N && c < N) {
+        const int src = rowsrc[r];
+        const int sp = r < nup ? 0 : 1;
+        T re = P[Ly::orb_b + (sp * N + c) * 2 + 0], im = P[Ly::orb_b + (sp * N + c) * 2 + 1];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const T hv = H3[src * 4 + f];
+          re += hv * P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 0];
+          im += hv * P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 1];
+        }
+        Ph[(r * N + c) * 2 + 0] = re;
+        Ph[(r * N + c) * 2 + 1] = im;
+        const T y = Yv[r * N + c];
+        a = re * y;
+        b = im * y;
+      }
+      ar[r] = a;
+      ai[r] = b;
+    }
+    // in-place Gauss-Jordan with virtual partial pivoting (gj_inverse's steps): after step k the
+    // pivot row p_k holds q = row / pivot (q_k = 1 / pivot), every other row r has
+    // a[r][c] - a[r][k] q_c (column k: -a[r][k] q_k); then B[k][p_c] = X[p_k][c]
+    unsigned used = 0;
+    int stepk[4] = {0, 0, 0, 0};
+    int myp = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      T kr[4], ki[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        kr[r] = k == 0 ? quad_bcast<0>(ar[r]) : (k == 1 ? quad_bcast<1>(ar[r]) : (k == 2 ? quad_bcast<2>(ar[r]) : quad_bcast<3>(ar[r])));
+        ki[r] = k == 0 ? quad_bcast<0>(ai[r]) : (k == 1 ? quad_bcast<1>(ai[r]) : (k == 2 ? quad_bcast<2>(ai[r]) : quad_bcast<3>(ai[r])));
+      }
+      int p = 0;
+      T best = T(-1);
+#pragma unroll
+      for (int r = 0; r < N; ++r) {
+        const T m = f_abs(kr[r]) + f_abs(ki[r]);
+        const bool take = !((used >> r) & 1u) && m > best;
+        best = take ? m : best;
+        p = take ? r : p;
+      }
+      T pr = T(0), pim = T(0), spr = T(0), spi = T(0);
+#pragma unroll
+      for (int r = 0; r < N; ++r)
+        if (r == p) {
+          pr = kr[r];
+          pim = ki[r];
+          spr = ar[r];
+          spi = ai[r];
+        }
+      inv += __builtin_popcount(used >> p);
+      used |= 1u << p;
+      const T den = pr * pr + pim * pim;
+      const T rden = f_rcp(den);
+      lsum += f_log(den);
+      {
+        const T rm = f_sqrt(rden);
+        const T xr = pr * rm, xi = pim * rm;
+        const T nr = ur * xr - ui * xi, ni = ur * xi + ui * xr;
+        ur = nr;
+        ui = ni;
+      }
+      const T ir = pr * rden, ii = -pim * rden;   // 1 / pivot
+      const bool ck = (c == k);
+      const T qr = ck ? ir : spr * ir - spi * ii;
+      const T qi = ck ? ii : spr * ii + spi * ir;
+#pragma unroll
+      for (int r = 0; r < N; ++r) {
+        const T br = ck ? T(0) : ar[r], bi = ck ? T(0) : ai[r];
+        const T nr = br - (kr[r] * qr - ki[r] * qi);
+        const T ni = bi - (kr[r] * qi + ki[r] * qr);
+        ar[r] = r == p ? qr : nr;
+        ai[r] = r == p ? qi : ni;
+        stepk[r] = r == p ? k : stepk[r];
+      }
+      myp = ck ? p : myp;
+    }
+    if (c < N) {
+#pragma unroll
+      for (int r = 0; r < N; ++r) {
+        Mx[(stepk[r] * N + myp) * 2 + 0] = ar[r];
+        Mx[(stepk[r] * N + myp) * 2 + 1] = ai[r];
+      }
+    }
+  }
+  wave_sync();
+#define BRE(c, s) Mx[((c) * N + (s)) * 2]
+#define BIM(c, s) Mx[((c) * N + (s)) * 2 + 1]
+
+  // ---------------------------------------------------------------- B1 adjoints of h^3 and Yt
+  T* hbar = hl;   // h^0 / h^3 are dead from here: their adjoints take their places
+  if (sl < 4 * N) {
+    const int r = sl >> 2, f = sl & 3;
+    const int sp = r < nup ? 0 : 1;
+    T q = T(0);
+#pragma unroll
+    for (int c = 0; c < N; ++c) {
+      const T yv = Yv[r * N + c];
+      const T wr = P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2] * yv;
+      const T wi = P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 1] * yv;
+      q += wr * BRE(c, r) - wi * BIM(c, r);
+    }
+    H3[rowsrc[r] * 4 + f] = q;   // adjoint of h^3 (same place)
+  }
+  wave_sync();   // ybar overwrites Yt
+  if (sl < N * N) {
+    const int r = sl / N, c = sl - r * N;
+    Yv[sl] = BRE(c, r) * Ph[sl * 2] - BIM(c, r) * Ph[sl * 2 + 1];
+  }
+#undef BRE
+#undef BIM
+  wave_sync();
+
+  // ---------------------------------------------------------------- B2 back through the layers
+  T* g2b = g2;   // the g2 values are dead after F4
+  {
+    T hb = H3[ic * 4 + ff];
+#pragma unroll
+    for (int l = 2; l >= 0; --l) {
+      const int d1 = l == 0 ? D0 : NH;
+      const int DF = 3 * d1 + 8;
+      const int Q = DF / 4;
+      const int T4 = d1 / 4;
+      const cptr<T> convw = P + (l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2)) + ic * DF;
+      const cptr<T> sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
+      const T sval = svv[(l * 4 + ic) * 4 + ff];
+      const T sb = (d1 == NH) ? hb * RSQ2 : hb;
+      const T zs = sb * (T(1) - sval * sval);
+      const T zq[4] = {quad_bcast<0>(zs), quad_bcast<1>(zs), quad_bcast<2>(zs), quad_bcast<3>(zs)};
+      const int QF = Q / 4;
+      T cg[QM];
+#pragma unroll
+      for (int q = 0; q < QM; ++q) {
+        const bool full = q < 4 * QF;
+        if (q < Q && (!full || (q & 3) == 0)) {
+          const int qq = full ? q + ff : q;
+          T cb = T(0);
+#pragma unroll
+          for (int m = 0; m < 4; ++m) cb += zq[m] * sngw[qq * 4 + m];
+          const T c = cqv[SQ::cqo(l, ic) + qq];
+          const T g = cb * (T(1) - c * c) * T(0.25);
+          if (full) {
+            cg[q + 0] = quad_bcast<0>(g);
+            cg[q + 1] = quad_bcast<1>(g);
+            cg[q + 2] = quad_bcast<2>(g);
+            cg[q + 3] = quad_bcast<3>(g);
+          } else {
+            cg[q] = g;
+          }
+        }
+      }
+      T fb[QM];
+#pragma unroll
+      for (int q = 0; q < QM; ++q)
+        if (q < Q) fb[q] = cg[q] * convw[4 * q + ff];
+      if (ilive) {   // pre-scaled by the group-mean weights 1/|G| of the pair sums
+        g2b[((l * 2 + 0) * N + ic) * 4 + ff] = fb[3 * T4 + 0] * ginv0;
+        g2b[((l * 2 + 1) * N + ic) * 4 + ff] = fb[3 * T4 + 1] * ginv1;
+      }
+      T hn = T(0);
+#pragma unroll
+      for (int t = 0; t < D0 / 4; ++t) {
+        if (t < T4) {
+          const T s0 = row_class4_sum(ilive ? fb[T4 + t] : T(0)) * ginv0;
+          const T s1 = row_class4_sum(ilive ? fb[2 * T4 + t] : T(0)) * ginv1;
+          T v = fb[t] + (inG1 ? s1 : s0);
+          if (d1 == NH) v += hb * RSQ2;
+          if (l == 0) {
+            if (ilive) hbar[ic * D0 + ff + 4 * t] = v;
+          } else {
+            hn = v;
+          }
+        }
+      }
+      hb = hn;
+    }
+  }
+  wave_sync();
+
+  // ---------------------------------------------------------------- B3 pair adjoints (every pair fresh)
+  T* dbar = S;   // [N][N][3]
+  if (sl < N * (N - 1)) {
+    const int k = sl / (N - 1), jj = sl - k * (N - 1);
+    const int i = jj + (jj >= k ? 1 : 0);
+    const int G = k >= nup ? 1 : 0;
+    T d[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) d[c] = xs[i * 3 + c] - xs[k * 3 + c];
+    const T r = f_sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    const T p0[4] = {r, d[0], d[1], d[2]};
+    T t1[4], p1[4], t2[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      T s = P[Ly::dbl_b0 + o];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) s += p0[m] * P[Ly::dbl_w0 + m * 4 + o];
+      t1[o] = f_tanh(s);
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) p1[o] = (p0[o] + t1[o]) * RSQ2;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      T s = P[Ly::dbl_b1 + o];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) s += p1[m] * P[Ly::dbl_w1 + m * 4 + o];
+      t2[o] = f_tanh(s);
+    }
+    T pb2[4], pb1[4], pb0[4], z2[4], z1[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) pb2[f] = g2b[((2 * 2 + G) * N + i) * 4 + f];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) z2[o] = pb2[o] * RSQ2 * (T(1) - t2[o] * t2[o]);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      T s = g2b[((1 * 2 + G) * N + i) * 4 + m] + pb2[m] * RSQ2;
+#pragma unroll
+      for (int o = 0; o < 4; ++o) s += z2[o] * P[Ly::dbl_w1 + m * 4 + o];
+      pb1[m] = s;
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) z1[o] = pb1[o] * RSQ2 * (T(1) - t1[o] * t1[o]);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      T s = g2b[((0 * 2 + G) * N + i) * 4 + m] + pb1[m] * RSQ2;
+#pragma unroll
+      for (int o = 0; o < 4; ++o) s += z1[o] * P[Ly::dbl_w0 + m * 4 + o];
+      pb0[m] = s;
+    }
+    T rb = pb0[0];
+    if (k < i) {   // Pade e-e Jastrow once per unordered pair
+      const T cusp = P[Ly::jee_c + k * N + i], al = P[Ly::jee_a + k * N + i];
+      const T den = al * r + T(1);
+      rb += cusp * f_rcp(den * den);
+    }
+    const T ir = f_rcp(r);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) dbar[(k * N + i) * 3 + c] = pb0[1 + c] + rb * d[c] * ir;
+  }
+  wave_sync();
+
+  // ---------------------------------------------------------------- B4 gradient, lane 4c + e
+  const int gc = sl >> 2, ge = sl & 3;
+  const bool gdir = gc < 3 && ge < N;
+  const int gcc = gc < 3 ? gc : 0, gee = ge < N ? ge : N - 1;
+  T g = T(0);
+  {
+    const bool mov = gee == pi;
+    const int l64 = 16 * gcc + gee;   // the walker cache's direction-lane index
+    T jd = Wc[WC::jaed + l64];
+    if (mov) jd = Eq[EC::jd + gcc];
+    g = jd;
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      if (k != gee) g += dbar[(k * N + gee) * 3 + gcc] - dbar[(gee * N + k) * 3 + gcc];
+#pragma unroll
+    for (int col = 0; col < N; ++col) {
+      const T lw = mov ? Eq[EC::yd + gcc * N + col] : Wc[WC::loc + col * 48 + l64];
+      g = f_fma(Yv[gee * N + col], lw, g);
+    }
+#pragma unroll
+    for (int m = 0; m < D0; ++m) {
+      const T lw = mov ? Eq[EC::hd + gcc * D0 + m] : Wc[WC::loc + (N + m) * 48 + l64];
+      g = f_fma(hbar[gee * D0 + m], lw, g);
+    }
+  }
+  const T gd = gdir ? g : T(0);
+  const T sumsq = row16_sum(gd * gd);
+  const T jt = row16_sum(jsum);
+  const T lsum0 = quad_bcast<0>(lsum), ur0 = quad_bcast<0>(ur), ui0 = quad_bcast<0>(ui);
+  if (act) {
+    if (ka.grad && gdir) ((T*)ka.grad)[(size_t)conf * 3 * N + 3 * gee + gcc] = g;
+    if (ka.gown && gdir && gee == pi) ((T*)ka.gown)[(size_t)conf * 3 + gcc] = g;
+    if (sl == 0) {
+      const T sg = (inv & 1) ? T(-1) : T(1);
+      if (ka.logabs) ((T*)ka.logabs)[conf] = T(0.5) * lsum0 + jt;
+      if (ka.phase) ((T*)ka.phase)[conf] = f_atan2(ui0 * sg, ur0 * sg);
+      if (ka.sumsq) ((T*)ka.sumsq)[conf] = sumsq;
+    }
+  }
+}
+
 }  // namespace aq

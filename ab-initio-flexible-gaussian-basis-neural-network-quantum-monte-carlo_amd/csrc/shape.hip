@@ -241,8 +241,8 @@ static int set_lds_impl() {
 
 // MODE_GRAD -> reverse-mode value+gradient kernel (walker_rev.h); MODE_LAP -> forward
 // Laplacian kernel (walker_kernel.h); MODE_GRAD_FWD -> forward-mode gradient (diagnostics).
-// value-only single-electron-moved configurations from the walker cache (pp quadrature), N <= 4:
-// four configurations per wave (quad_small.h)
+// single-electron-moved configurations from the walker cache, N <= 4: four configurations per
+// wave (quad_small.h): value only (pp quadrature) or value + gradient (Metropolis proposals)
 template <typename T, int N, int A>
 static bool quad_small(const KArgs& ka, int nconf, hipStream_t s) {
   if constexpr (N <= 4) {
@@ -250,8 +250,19 @@ static bool quad_small(const KArgs& ka, int nconf, hipStream_t s) {
       k_quad_value<T, N, A><<<dim3((nconf + 4 * QUAD_WPB - 1) / (4 * QUAD_WPB)), dim3(64 * QUAD_WPB), 0, s>>>(ka);
       return true;
     }
+    if (ka.proposal && ka.ecache && !ka.value_only && !ka.orb && !ka.ablate) {   // Metropolis proposals
+      k_quad_grad<T, N, A><<<dim3((nconf + 3) / 4), dim3(64), 0, s>>>(ka);
+      return true;
+    }
   }
   return false;
+}
+
+// proposal-launch grid: ceil(nconf / wpb) workgroups, padded to a multiple of the 8 XCDs so that
+// xcd_major keeps each walker's proposals on one XCD (the padding workgroups exit at once)
+static inline unsigned prop_blocks(int nconf, int wpb) {
+  const unsigned nb = (unsigned)((nconf + wpb - 1) / wpb);
+  return wpb > 1 ? (nb + 7u) & ~7u : nb;
 }
 
 template <int N, int A>
@@ -262,7 +273,7 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
     if (mode == MODE_LAP)
       k_walker<float, N, A, MODE_LAP><<<dim3(nconf), dim3(64), Smem<float, N, true>::bytes, s>>>(ka);
     else if (mode == MODE_GRAD && ka.proposal && ka.ecache)   // proposals from the walker cache
-      k_walker_rev<float, N, A, false, true><<<dim3((nconf + RevWpb<float, true>::value - 1) / RevWpb<float, true>::value),
+      k_walker_rev<float, N, A, false, true><<<dim3(prop_blocks(nconf, RevWpb<float, true>::value)),
                                               dim3(64 * RevWpb<float, true>::value),
                                               RevWpb<float, true>::value * SmemRev<float, N, A>::bytes, s>>>(ka);
     else if (mode == MODE_GRAD)
@@ -275,7 +286,7 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
     if (mode == MODE_LAP)
       k_walker<double, N, A, MODE_LAP><<<dim3(nconf), dim3(64), Smem<double, N, true>::bytes, s>>>(ka);
     else if (mode == MODE_GRAD && ka.proposal && ka.ecache)   // proposals from the walker cache
-      k_walker_rev<double, N, A, false, true><<<dim3((nconf + RevWpb<double, true>::value - 1) / RevWpb<double, true>::value),
+      k_walker_rev<double, N, A, false, true><<<dim3(prop_blocks(nconf, RevWpb<double, true>::value)),
                                               dim3(64 * RevWpb<double, true>::value),
                                               RevWpb<double, true>::value * SmemRev<double, N, A>::bytes, s>>>(ka);
     else if (mode == MODE_GRAD)

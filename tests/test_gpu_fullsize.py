@@ -242,3 +242,33 @@ def test_other_shapes_local_energy_adjoint_vs_forward(name):
     torch.cuda.synchronize()
     assert torch.allclose(e1, e0, rtol=1e-9, atol=1e-8), float((e1 - e0).abs().max())
     assert torch.allclose(g1, g0, rtol=1e-8, atol=1e-8)
+
+
+@pytest.mark.parametrize("name", ["Be", "H2"])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_small_n_packed_proposals_match_one_wave_path(name, dtype):
+    """N <= 4: the Metropolis proposals run four configurations per wave (quad_small.h
+    k_quad_grad); with the walker cache off every proposal goes through k_walker_rev's general
+    path instead.  Same host draws -> same trajectory (fp64: to 1e-10, identical accept
+    counts; fp32: all but rounding-level acceptance flips)."""
+    s, ctx = _ctx(name, dtype)
+    B, NS, N = 1000, 3, s.nelectrons    # B*N not a multiple of 16: a ragged last wave
+    x0 = torch.tensor(_walkers(s, B, seed=4), dtype=dtype, device="cuda")
+    g = torch.Generator().manual_seed(1)
+    kw = dict(gauss1=torch.randn(NS, B, 3 * N, generator=g, dtype=torch.float64),
+              gauss2=torch.randn(NS, B, N, 3, generator=g, dtype=torch.float64),
+              u=torch.rand(NS, B, N, generator=g, dtype=torch.float64))
+    a = x0.clone().contiguous()
+    b = x0.clone().contiguous()
+    acc_a = ctx.mc_step(a, NS, 0.05, count_accepts=True, **kw)
+    ctx.set_proposal_reuse(False)
+    acc_b = ctx.mc_step(b, NS, 0.05, count_accepts=True, **kw)
+    ctx.set_proposal_reuse(True)
+    torch.cuda.synchronize()
+    assert int(acc_a.sum()) > 0
+    if dtype == torch.float64:
+        assert torch.allclose(a, b, rtol=0, atol=1e-10), float((a - b).abs().max())
+        assert torch.equal(acc_a, acc_b)
+    else:
+        differ = ((a - b).abs().reshape(B, -1).amax(1) > 1e-4).float().mean()
+        assert float(differ) < 5e-3, float(differ)
