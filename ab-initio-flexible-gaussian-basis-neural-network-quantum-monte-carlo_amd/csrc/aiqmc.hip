@@ -24,14 +24,21 @@ using namespace aq;
 // ============================================================================ small kernels
 
 // v2 = sum(x[0..n)) ; taueff = (sqrt(1 + 2 tau a v2) - 1)/(a v2), a = 0.25  (VMCmcstep.py:11-14)
-// One 1024-thread block; thread t sums x[t + 1024 j] in 8 independent partial sums (8 loads in
-// flight per thread: n = B N = 57,344 takes 7 rounds of 8), then a fixed-order tree -- the
-// result is deterministic.
+// One 1024-thread block; thread t sums x[t + 1024 j] in 8 independent partial sums, 32 loads in
+// flight per thread (n = B N = 57,344 takes two rounds; with 8 in flight it took 7 and the
+// launch 4.8 us), then a fixed-order tree -- the result is deterministic.
 template <typename T>
 __global__ __launch_bounds__(1024) void k_taueff(const T* __restrict__ x, int n, double tstep, double* out) {
   __shared__ double red[1024];
   double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int i = threadIdx.x;
+  for (; i + 31 * 1024 < n; i += 32 * 1024) {
+    T v[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) v[k] = x[i + k * 1024];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) s[k & 7] += (double)v[k];
+  }
   for (; i + 7 * 1024 < n; i += 8 * 1024) {
     T v[8];
 #pragma unroll

@@ -350,7 +350,11 @@ struct SmemQG {
   static constexpr int cqo(int l, int i) { return l == 0 ? i * QM : 4 * QM + ((l - 1) * 4 + i) * QL; }
 };
 
-template <typename T, int N, int A>
+// WALK = true: the walker launch of a sweep (k_walker_rev's walker path): the previous sweep's
+// acceptance (fused), every electron's stage on lane 4c + e (its local Jacobians stay in the
+// lane's registers for B4), the full pair stream on lane k N + i, and the complete walker cache
+// (WCache, including the pair tanh's and the pivot record the one-wave proposal path reads).
+template <typename T, int N, int A, bool WALK = false>
 __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
   static_assert(N <= 4, "four configurations per wave need N <= 4");
   using Ly = Lay<N, A>;
@@ -378,14 +382,131 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
   T* Ph = sm + SQ::ph;
   T* Mx = sm + SQ::mx;
   const int mper = ka.mper ? ka.mper : N, mdiv = ka.mdiv ? ka.mdiv : 1;
-  const int pb = conf / mper, pi = (conf - pb * mper) / mdiv;
+  const int pb = WALK ? conf : conf / mper, pi = WALK ? -1 : (conf - pb * mper) / mdiv;
   const int nup = ka.nup;
   const int* rowsrc = ka.rowsrc;
   const T RSQ2 = T(0.70710678118654752);
   const T ginv0 = T(1) / T(nup), ginv1 = T(1) / T(N - nup);
-  const T* Wc = (const T*)ka.wcache + (size_t)pb * WC::size;
-  const T* Eq = (const T*)ka.ecache + (size_t)conf * EC::size;
-
+  T* Wc = (T*)ka.wcache + (size_t)pb * WC::size;
+  const T* Eq = WALK ? nullptr : (const T*)ka.ecache + (size_t)conf * EC::size;
+  T lv[N + D0];      // WALK: d(Yt row e, ae features of e) / d x_{e,c} of lane 4c + e
+  T jd1w = T(0);     // WALK: d J_ae / d x_{e,c}
+  T jsum = T(0);
+  if constexpr (WALK) {
+    // ---------------------------------------------------------------- F0 positions (+ acceptance)
+    if (ka.acc.lpn) {
+      if (sl < N) {   // the previous sweep's acceptance of this walker's N proposals
+        T xn[3];
+        const bool acc = accept_one<T, N>(ka.acc, (const T*)ka.pos, conf, sl, xn);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) xs[3 * sl + c] = xn[c];
+        if (acc && act) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) ((T*)ka.pos)[(size_t)conf * 3 * N + 3 * sl + c] = xn[c];
+          if (ka.acc.count) atomicAdd(&ka.acc.count[conf], 1);
+        }
+      }
+    } else if (sl < 3 * N) {
+      xs[sl] = ((const T*)ka.pos)[(size_t)conf * 3 * N + sl];
+    }
+    wave_sync();
+    // ---------------------------------------------------------------- F1 electron stage, lane 4c + e
+    {
+      const int c = sl >> 2, e = sl & 3;
+      const int ee = e < N ? e : N - 1;
+      const bool elive = e < N, ev = c == 3;
+      ElecOut<T, A> eo;
+      electron_stage<T, N, A>(P, xs + ee * 3, ee, c, eo);
+      T* Wl = Wc + WC::loc + 16 * (ev ? 0 : c) + ee;
+#pragma unroll
+      for (int col = 0; col < N; ++col) {
+        PJ<T> sy = P[Ly::wy + col] * eo.yst[0];
+#pragma unroll
+        for (int m = 1; m < NYW; ++m) sy = sy + P[Ly::wy + m * N + col] * eo.yst[m];
+        const PJ<T> yt = eo.env * sy;
+        lv[col] = yt.d1;
+        if (elive && ev) {
+          Yv[e * N + col] = yt.v;
+          if (act) Wc[WC::yv + e * N + col] = yt.v;
+        }
+        if (elive && !ev && act) Wl[col * 48] = yt.d1;
+      }
+#pragma unroll
+      for (int m = 0; m < D0; ++m) {
+        lv[N + m] = eo.hf[m].d1;
+        if (elive && ev) {
+          hl[e * D0 + m] = eo.hf[m].v;
+          if (act) Wc[WC::h0 + e * D0 + m] = eo.hf[m].v;
+        }
+        if (elive && !ev && act) Wl[(N + m) * 48] = eo.hf[m].d1;
+      }
+      if (elive && ev) {
+        jsum = eo.jae.v;
+        if (act) Wc[WC::jaev + e] = eo.jae.v;
+      }
+      if (elive && !ev) {
+        jd1w = eo.jae.d1;
+        if (act) Wc[WC::jaed + 16 * c + e] = jd1w;
+      }
+    }
+    // ---------------------------------------------------------------- F2 pair stream, lane k N + i
+    {
+      const bool pl = sl < N * N;
+      const int k = pl ? sl / N : 0, i = pl ? sl - (sl / N) * N : 0;
+      const bool diag = k == i;
+      T d[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) d[c] = xs[i * 3 + c] - xs[k * 3 + c];
+      const T r2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+      const T r = f_sqrt(diag ? T(1) : r2);
+      T pp[4] = {diag ? T(0) : r, diag ? T(0) : d[0], diag ? T(0) : d[1], diag ? T(0) : d[2]};
+      T jl = T(0);
+      if (pl && k < i) {   // Pade e-e Jastrow, each pair once (Jastrow.py:51-52)
+        const T cusp = P[Ly::jee_c + k * N + i], al = P[Ly::jee_a + k * N + i];
+        jl = f_div(cusp * r, al * r + T(1));
+      }
+#pragma unroll
+      for (int f = 0; f < 4; ++f) S[sl * 12 + f] = pp[f];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const cptr<T> dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
+        const cptr<T> db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
+        T q[4];
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+          T z = db[o];
+#pragma unroll
+          for (int m = 0; m < 4; ++m) z += pp[m] * dw[m * 4 + o];
+          q[o] = f_tanh(z);
+        }
+        if (pl && !diag && act) {   // walker cache: t_{j+1} of pair (k, i) (the one-wave proposal path)
+#pragma unroll
+          for (int o = 0; o < 4; ++o) Wc[WC::pt + (k * N + i) * 8 + j * 4 + o] = q[o];
+        }
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+          pp[o] = (pp[o] + q[o]) * RSQ2;
+          S[sl * 12 + (j + 1) * 4 + o] = pp[o];
+        }
+      }
+      jsum += jl;
+      const T jee = row16_sum(jl);
+      if (sl == 0 && act) Wc[WC::jee] = jee;
+    }
+    wave_sync();
+    // spin-group column means g2[l][G][i][f] = sum_{k in G} h2^l[k, i][f] / |G| (nn.py:151)
+    for (int t = sl; t < 24 * N; t += 16) {
+      const int f = t & 3, ci = (t >> 2) % N, lg = (t >> 2) / N;
+      const int l = lg >> 1, G = lg & 1;
+      const int k0 = G ? nup : 0, k1 = G ? N : nup;
+      T acc = T(0);
+      for (int k = k0; k < k1; ++k) acc += S[(k * N + ci) * 12 + l * 4 + f];
+      const T v = acc * (G ? ginv1 : ginv0);
+      g2[((l * 2 + G) * N + ci) * 4 + f] = v;
+      if (act) Wc[WC::g2 + ((l * 2 + G) * N + ci) * 4 + f] = v;
+    }
+    wave_sync();
+  } else {
   // ---------------------------------------------------------------- F1 cached stage of walker pb
   if (sl < 3 * N) {
     const T x0 = ((const T*)ka.pos)[(size_t)pb * 3 * N + sl];
@@ -402,7 +523,7 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
     hl[idx] = e == pi ? Eq[EC::h0 + idx - e * D0] : Wc[WC::h0 + idx];
   }
   for (int idx = sl; idx < 3 * 2 * N * 4; idx += 16) g2[idx] = Wc[WC::g2 + idx];
-  T jsum = sl < N ? (sl == pi ? Eq[EC::jv] : Wc[WC::jaev + sl]) : T(0);
+  jsum = sl < N ? (sl == pi ? Eq[EC::jv] : Wc[WC::jaev + sl]) : T(0);
   if (sl == 0) jsum += Wc[WC::jee];
   wave_sync();
 
@@ -449,6 +570,7 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
     }
   }
   wave_sync();
+  }   // proposal path
 
   // ---------------------------------------------------------------- F4 h-stream layers (values kept)
   const int fi = sl >> 2, ff = sl & 3;
@@ -601,6 +723,10 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
         ur = nr;
         ui = ni;
       }
+      if (WALK && c == 0 && act) {   // pivot record (gj.h: row of step k, 1 / |pivot_k|)
+        Wc[WC::pv + k] = T(p);
+        Wc[WC::pv + N + k] = f_sqrt(rden);
+      }
       const T ir = pr * rden, ii = -pim * rden;   // 1 / pivot
       const bool ck = (c == k);
       const T qr = ck ? ir : spr * ir - spi * ii;
@@ -622,6 +748,10 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
         Mx[(stepk[r] * N + myp) * 2 + 0] = ar[r];
         Mx[(stepk[r] * N + myp) * 2 + 1] = ai[r];
       }
+    }
+    if (WALK && c == 0 && act) {
+      Wc[WC::pv + 2 * N] = T(inv & 1);
+      Wc[WC::pv + 2 * N + 1] = T(0.5) * lsum;
     }
   }
   wave_sync();
@@ -784,7 +914,17 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
   const bool gdir = gc < 3 && ge < N;
   const int gcc = gc < 3 ? gc : 0, gee = ge < N ? ge : N - 1;
   T g = T(0);
-  {
+  if constexpr (WALK) {
+    // lane 4c + e: the same lane as in F1, whose local Jacobians are in registers
+    g = jd1w;
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      if (k != gee) g += dbar[(k * N + gee) * 3 + gcc] - dbar[(gee * N + k) * 3 + gcc];
+#pragma unroll
+    for (int col = 0; col < N; ++col) g = f_fma(Yv[gee * N + col], lv[col], g);
+#pragma unroll
+    for (int m = 0; m < D0; ++m) g = f_fma(hbar[gee * D0 + m], lv[N + m], g);
+  } else {
     const bool mov = gee == pi;
     const int l64 = 16 * gcc + gee;   // the walker cache's direction-lane index
     T jd = Wc[WC::jaed + l64];
@@ -816,6 +956,19 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
       if (ka.logabs) ((T*)ka.logabs)[conf] = T(0.5) * lsum0 + jt;
       if (ka.phase) ((T*)ka.phase)[conf] = f_atan2(ui0 * sg, ur0 * sg);
       if (ka.sumsq) ((T*)ka.sumsq)[conf] = sumsq;
+    }
+    if (WALK && ka.dg1 && sl < N) {   // the sweep's draws of walker conf (k_draws' arithmetic)
+      const uint32_t t = (uint32_t)(conf * N + sl);
+      float a[3], b[3], c[4];
+      philox_normal3f(ka.seed, ka.step, t, 0u, a);
+      philox_normal3f(ka.seed, ka.step, t, 1u, b);
+      philox_u4(ka.seed, ka.step, t, 2u, c);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        ((T*)ka.dg1)[(size_t)t * 3 + k] = (T)a[k];
+        ((T*)ka.dg2)[(size_t)t * 3 + k] = (T)b[k];
+      }
+      ((T*)ka.du)[t] = (T)(c[0] - 5.9604644775390625e-08f);
     }
   }
 }

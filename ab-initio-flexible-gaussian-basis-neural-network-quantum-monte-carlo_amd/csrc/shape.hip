@@ -254,6 +254,10 @@ static bool quad_small(const KArgs& ka, int nconf, hipStream_t s) {
       k_quad_grad<T, N, A><<<dim3((nconf + 3) / 4), dim3(64), 0, s>>>(ka);
       return true;
     }
+    if (!ka.proposal && ka.wcache && !ka.value_only && !ka.orb && !ka.lapcache) {   // walker launches
+      k_quad_grad<T, N, A, true><<<dim3((nconf + 3) / 4), dim3(64), 0, s>>>(ka);
+      return true;
+    }
   }
   return false;
 }
