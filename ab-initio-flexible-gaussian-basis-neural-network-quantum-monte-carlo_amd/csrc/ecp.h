@@ -160,6 +160,23 @@ __device__ __forceinline__ double ecp_pl(int l, double x) {
   return 7.0 * c * 0.5 * (5.0 * x * x * x - 3.0 * x);
 }
 
+// E3's Frobenius norm of a grid group's rotated coordinates r p'_q is r^2 F_g with
+// F_g = sum_{q in g} |p_q R|^2, which depends on the walker's rotation only: one point per lane,
+// four masked wave sums (instead of a loop over the group's points for every quadrature entry).
+template <typename T>
+__device__ __forceinline__ void ecp_group_norms(const T* R, int lane, double Fg[4]) {
+  double v = 0.0;
+  int gl = -1;
+  if (lane < ECP_NQ) {
+    double p[3], pr[3];
+    ecp_point(lane, p, gl);
+    ecp_rotate<T>(R, p, pr);
+    v = pr[0] * pr[0] + pr[1] * pr[1] + pr[2] * pr[2];
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) Fg[g] = wave_sum(gl == g ? v : 0.0);
+}
+
 template <typename T>
 __global__ __launch_bounds__(64) void k_ecp_energy(EcpArgs ea) {
   const int b = blockIdx.x;
@@ -172,6 +189,8 @@ __global__ __launch_bounds__(64) void k_ecp_energy(EcpArgs ea) {
   const double* tabs = ea.tab + 4 * A;
   const T* x = (const T*)ea.pos + (size_t)b * 3 * N;
   const T* R = (const T*)ea.rot + (size_t)b * 9;
+  double Fg[4] = {0.0, 0.0, 0.0, 0.0};
+  if (!ea.skip_nl) ecp_group_norms<T>(R, lane, Fg);   // skip_nl: no rotations drawn
   const double la0 = ea.skip_nl ? 1.0 : (double)((const T*)ea.lp0)[b];
   const double ph0 = ea.skip_nl ? 0.0 : (double)((const T*)ea.ph0)[b];
   const double dn = 1.0 / (la0 * la0 + ph0 * ph0);   // 1 / den, den = la0 + i ph0 (E4)
@@ -193,15 +212,7 @@ __global__ __launch_bounds__(64) void k_ecp_energy(EcpArgs ea) {
     ecp_point(q, p, grp);
     ecp_rotate<T>(R, p, pr);
     // Frobenius norm of the group's rotated coordinates r p'_q (E3)
-    double fro2 = 0.0;
-    for (int qq = ecp_group_begin(grp); qq < ecp_group_end(grp); ++qq) {
-      double pp[3], ppr[3];
-      int gg;
-      ecp_point(qq, pp, gg);
-      ecp_rotate<T>(R, pp, ppr);
-#pragma unroll
-      for (int d = 0; d < 3; ++d) fro2 += (r * ppr[d]) * (r * ppr[d]);
-    }
+    const double fro2 = r * r * Fg[grp];
     const double dot = ae[0] * (r * pr[0]) + ae[1] * (r * pr[1]) + ae[2] * (r * pr[2]);
     const double cs = dot / (r * sqrt(fro2));
     const size_t conf = (size_t)b * M + idx;
@@ -276,6 +287,8 @@ __global__ __launch_bounds__(64) void k_tmove(EcpArgs ea) {
   const double* tabs = ea.tab + 4 * A;
   const T* x = (const T*)ea.pos + (size_t)b * 3 * N;
   const T* R = (const T*)ea.rot + (size_t)b * 9;
+  double Fg[4];
+  ecp_group_norms<T>(R, lane, Fg);
   const double la0 = (double)((const T*)ea.lp0)[b], ph0 = (double)((const T*)ea.ph0)[b];
   const double dn = 1.0 / (la0 * la0 + ph0 * ph0);
   double* scr = ea.scr + (size_t)b * M * 4;
@@ -295,15 +308,7 @@ __global__ __launch_bounds__(64) void k_tmove(EcpArgs ea) {
     int grp;
     ecp_point(q, p, grp);
     ecp_rotate<T>(R, p, pr);
-    double fro2 = 0.0;   // E3
-    for (int qq = ecp_group_begin(grp); qq < ecp_group_end(grp); ++qq) {
-      double pp[3], ppr[3];
-      int gg;
-      ecp_point(qq, pp, gg);
-      ecp_rotate<T>(R, pp, ppr);
-#pragma unroll
-      for (int d = 0; d < 3; ++d) fro2 += (r * ppr[d]) * (r * ppr[d]);
-    }
+    const double fro2 = r * r * Fg[grp];   // E3
     const double dot = ae[0] * (r * pr[0]) + ae[1] * (r * pr[1]) + ae[2] * (r * pr[2]);
     const double cs = dot / (r * sqrt(fro2));
     const size_t conf = (size_t)b * M + idx;

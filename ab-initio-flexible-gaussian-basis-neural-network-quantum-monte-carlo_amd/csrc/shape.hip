@@ -323,9 +323,9 @@ template <int N, int A>
 static void moved_impl(int dtype, const KArgs& ka, hipStream_t s) {
   const int nb = (ka.nconf + 15) / 16;
   if (dtype == AIQMC_F32)
-    k_moved_electron<float, N, A><<<dim3(nb), dim3(64), 0, s>>>(ka);
+    k_moved_electron<float, N, A><<<dim3(prop_blocks(nb, MOVED_WPB)), dim3(64 * MOVED_WPB), 0, s>>>(ka);
   else
-    k_moved_electron<double, N, A><<<dim3(nb), dim3(64), 0, s>>>(ka);
+    k_moved_electron<double, N, A><<<dim3(prop_blocks(nb, MOVED_WPB)), dim3(64 * MOVED_WPB), 0, s>>>(ka);
 }
 
 template <int N, int A>

@@ -160,6 +160,14 @@ template <int M, typename T> __device__ __forceinline__ T quad_bcast(T x) {
   return dpp<M | (M << 2) | (M << 4) | (M << 6)>(x);
 }
 
+// Barrier of a one-configuration wave: LDS traffic of one wave is processed in order, so a
+// wavefront-scope fence (a compiler barrier, no s_waitcnt) orders its cross-lane LDS accesses.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2):
 // give every XCD a contiguous range of configurations, so the N proposals of a
 // walker (and that walker's cache) land on one L2.
@@ -171,19 +179,25 @@ __device__ __forceinline__ int xcd_major(int blk, int n) {
 // Electron-local stage of the moved electron of proposals q = 16*block + s (lane = 16c + s).
 // The wave's 16 records are contiguous in the cache: they are assembled in LDS and written
 // with coalesced stores (direct per-lane stores scatter over 16 records x 4 lanes).
+// MOVED_WPB independent waves (16 proposals each) per workgroup: the launch pays per workgroup
+// (see AQ_PROP_WPB); the grid is padded to a multiple of 8 and the padding waves exit.
+constexpr int MOVED_WPB = 4;
 template <typename T, int N, int A>
-__global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
+__global__ __launch_bounds__(64 * MOVED_WPB) void k_moved_electron(KArgs ka) {
   using Ly = Lay<N, A>;
   using EC = ECache<N, A>;
   constexpr int D0 = 4 * A;
   // records padded by one element in LDS: EC::size is a multiple of 16, so an unpadded record
   // stride puts the 16 lanes of a direction row on one bank (16-way conflicts)
   constexpr int RS = EC::size + 1;
-  __shared__ T eb[16 * RS];
+  __shared__ T ebw[MOVED_WPB][16 * RS];
   const cptr<T> P = param_ptr<T>(ka.prm);
-  const int lane = threadIdx.x;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  T* eb = ebw[wv];
+  const int lane = threadIdx.x & 63;
   const int lc = lane >> 4, s = lane & 15;
-  const int blk = xcd_major(blockIdx.x, gridDim.x);
+  const int blk = xcd_major(blockIdx.x, gridDim.x) * MOVED_WPB + wv;
+  if (blk * 16 >= ka.nconf) return;
   const int nrec = ka.nconf - blk * 16 < 16 ? ka.nconf - blk * 16 : 16;
   const int q = blk * 16 + (s < nrec ? s : nrec - 1);
   const int mper = ka.mper ? ka.mper : N, mdiv = ka.mdiv ? ka.mdiv : 1;
@@ -225,7 +239,7 @@ __global__ __launch_bounds__(64) void k_moved_electron(KArgs ka) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) E[EC::xp + c] = xp[c];
   }
-  __syncthreads();
+  wave_sync();   // the wave's own records (waves of a workgroup share nothing)
   T* dst = (T*)ka.ecache + (size_t)blk * 16 * EC::size;
   for (int idx = lane; idx < nrec * EC::size; idx += 64) {
     const int rec = idx / EC::size;
@@ -265,13 +279,6 @@ template <typename T, int N, int A, bool PREP, bool PROP> struct RevWaves {
 template <typename T, bool PROP, bool PREP = false> struct RevWpb {
   static constexpr int value = sizeof(T) != 4 ? 1 : (PROP ? AQ_PROP_WPB : (PREP ? 1 : AQ_WALK_WPB));
 };
-// Barrier of a one-configuration wave: LDS traffic of one wave is processed in order, so a
-// wavefront-scope fence (a compiler barrier, no s_waitcnt) orders its cross-lane LDS accesses.
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 #ifdef AQ_WAVE_SYNC
 #define AQ_SYNC() wave_sync()
 #else

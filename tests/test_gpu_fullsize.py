@@ -252,7 +252,7 @@ def test_small_n_packed_proposals_match_one_wave_path(name, dtype):
     path instead.  Same host draws -> same trajectory (fp64: to 1e-10, identical accept
     counts; fp32: all but rounding-level acceptance flips)."""
     s, ctx = _ctx(name, dtype)
-    B, NS, N = 1000, 3, s.nelectrons    # B*N not a multiple of 16: a ragged last wave
+    B, NS, N = 1001, 3, s.nelectrons    # odd B: the last wave of the walker launch (and of H2's proposals) is partial
     x0 = torch.tensor(_walkers(s, B, seed=4), dtype=dtype, device="cuda")
     g = torch.Generator().manual_seed(1)
     kw = dict(gauss1=torch.randn(NS, B, 3 * N, generator=g, dtype=torch.float64),
