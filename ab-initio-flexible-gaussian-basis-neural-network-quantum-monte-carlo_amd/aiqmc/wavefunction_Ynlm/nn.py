@@ -71,9 +71,40 @@ def tree_flatten(tree):
     return [np.asarray(tree, dtype=np.float64)]
 
 
+def tree_leaves(tree):
+    """The leaves themselves (tensors / arrays / scalars), in tree_flatten order."""
+    if isinstance(tree, dict):
+        return [x for k in sorted(tree.keys()) for x in tree_leaves(tree[k])]
+    if isinstance(tree, (list, tuple)):
+        return [x for v in tree for x in tree_leaves(v)]
+    return [tree]
+
+
+def _flatten_leaves(leaves) -> np.ndarray:
+    """Concatenated float64 copy of the leaves; tensor leaves on one device are gathered there and
+    copied to the host once (a device->host copy per leaf synchronises once per leaf)."""
+    if not leaves:
+        return np.zeros(0)
+    if all(isinstance(l, torch.Tensor) for l in leaves) and len({l.device for l in leaves}) == 1:
+        return torch.cat([l.detach().reshape(-1).to(torch.float64) for l in leaves]).cpu().numpy()
+    return np.concatenate([l.reshape(-1) for l in tree_flatten(leaves)])
+
+
 def flatten_params(params) -> np.ndarray:
-    leaves = tree_flatten(params)
-    return np.concatenate([l.reshape(-1) for l in leaves]) if leaves else np.zeros(0)
+    return _flatten_leaves(tree_leaves(params))
+
+
+def _leaf_key(leaves):
+    """Identity + in-place version of every tensor leaf (no device sync); None when a leaf is not a
+    tensor (its value must then be compared)."""
+    if not all(isinstance(l, torch.Tensor) for l in leaves):
+        return None
+    return [(l, l._version) for l in leaves]
+
+
+def _same_leaves(key, leaves) -> bool:
+    return key is not None and len(key) == len(leaves) and all(
+        t is l and v == l._version for (t, v), l in zip(key, leaves))
 
 
 def _first(x):
@@ -114,7 +145,7 @@ class AINet:
         self.natoms = int(natoms)
         self.nelectrons = int(nelectrons)
         self._ctx: Dict[Tuple, _lib.Context] = {}
-        self._loaded: Dict[Tuple, str] = {}
+        self._loaded: Dict[int, tuple] = {}   # id(ctx) -> (leaf key, digest) of the last upload
 
     # -- init (nn.py:203-278, 370-407; network_blocks.py:63-102) --------------
     def init(self, key) -> Dict[str, Any]:
@@ -165,14 +196,23 @@ class AINet:
         return ctx
 
     def bind(self, params, atoms, dtype=torch.float32, device: Optional[int] = None) -> _lib.Context:
-        """Context with `params` uploaded (re-uploads only when the values changed)."""
+        """Context with `params` uploaded (re-uploads only when the values changed).
+
+        The same tensor leaves at the same in-place versions as the last upload are taken as
+        unchanged without looking at their values (no device->host copy, no sync: the drop-in
+        drivers call apply / local_energy / mc_step several times per step with one params
+        tree); otherwise the leaves are gathered with one copy and compared by digest."""
         ctx = self.context(atoms, dtype, device)
-        flat = flatten_params(params)
-        digest = hashlib.sha1(flat.tobytes()).hexdigest()
+        leaves = tree_leaves(params)
         k = id(ctx)
-        if self._loaded.get(k) != digest:
+        prev = self._loaded.get(k)
+        if prev is not None and _same_leaves(prev[0], leaves):
+            return ctx
+        flat = _flatten_leaves(leaves)
+        digest = hashlib.sha1(flat.tobytes()).hexdigest()
+        if prev is None or prev[1] != digest:
             ctx.set_params(flat)
-            self._loaded[k] = digest
+        self._loaded[k] = (_leaf_key(leaves), digest)
         return ctx
 
     # -- apply (nn.py:545-551) --------------------------------------------------
