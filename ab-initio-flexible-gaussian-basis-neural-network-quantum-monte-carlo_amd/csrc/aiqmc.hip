@@ -221,46 +221,53 @@ __global__ __launch_bounds__(256) void k_dmc_weights(int B, int N, const T* __re
   w[i] = (T)(exp(tau * td * (0.5 * sn + 0.5 * so)) * (double)w[i]);
 }
 
-// Stochastic comb (DMC/branch.py:10-33), one block: cumulative weights in a fixed (sequential)
-// order, then newinds[j] = searchsorted_left(cumsum, (u wtot + j wtot / n) mod wtot);
-// wout[0] = wtot / n.  The running sum is carried by one thread through chunks of the weights
-// staged in LDS (its loads are LDS hits, not dependent global round trips: 196 -> ~15 us at
-// n = 4096); the searches run over the LDS copy when the whole cumsum fits.
+// Stochastic comb (DMC/branch.py:10-33), one block: cumulative weights in a fixed order, then
+// newinds[j] = searchsorted_left(cumsum, (u wtot + j wtot / n) mod wtot); wout[0] = wtot / n.
+// The cumulative sum is a blocked scan: thread t sums its contiguous chunk of ceil(n / 1024)
+// weights, the 1024 chunk sums are scanned in a fixed tree (Hillis-Steele over LDS), and each
+// thread re-walks its chunk from its prefix.  Deterministic; it equals the sequential sum up to
+// fp64 rounding.  (A single thread carrying the running sum took 196 us at n = 4096 from global
+// memory and 69 us through LDS.)  The searches read an LDS copy when the cumsum fits.
+constexpr int COMB_LDS = 4096;
 template <typename T>
 __global__ __launch_bounds__(1024) void k_dmc_branch(int n, const T* __restrict__ w, double u, double* __restrict__ csum,
                                                      int32_t* __restrict__ newinds, T* __restrict__ wout) {
-  constexpr int COMB_CH = sizeof(T) == 4 ? 4096 : 2048;   // 48 KB of LDS either way
-  __shared__ T ws[COMB_CH];
-  __shared__ double cs[COMB_CH];
-  double a = 0.0;   // thread 0's running sum
-  for (int c0 = 0; c0 < n; c0 += COMB_CH) {
-    const int m = n - c0 < COMB_CH ? n - c0 : COMB_CH;
-    for (int i = threadIdx.x; i < m; i += 1024) ws[i] = w[c0 + i];
+  __shared__ double sc[1024];
+  __shared__ double cl[COMB_LDS];
+  const int t = threadIdx.x;
+  const int ch = (n + 1023) / 1024;
+  const int i0 = t * ch < n ? t * ch : n, i1 = i0 + ch < n ? i0 + ch : n;
+  double s = 0.0;
+  for (int i = i0; i < i1; ++i) s += (double)w[i];
+  sc[t] = s;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {   // inclusive scan of the chunk sums
+    const double v = t >= d ? sc[t - d] : 0.0;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int i = 0; i < m; ++i) {
-        a += (double)ws[i];
-        cs[i] = a;
-      }
-    }
-    __syncthreads();
-    if (n > COMB_CH)
-      for (int i = threadIdx.x; i < m; i += 1024) csum[c0 + i] = cs[i];
+    sc[t] += v;
     __syncthreads();
   }
-  const double* cp = n > COMB_CH ? csum : cs;
+  double a = t > 0 ? sc[t - 1] : 0.0;
+  const bool lds = n <= COMB_LDS;
+  for (int i = i0; i < i1; ++i) {
+    a += (double)w[i];
+    if (lds) cl[i] = a;
+    else csum[i] = a;
+  }
+  __syncthreads();   // (block-scope fence: the global cumsum of the other threads is visible)
+  const double* cp = lds ? cl : csum;
   const double wtot = cp[n - 1];
-  for (int j = threadIdx.x; j < n; j += 1024) {
-    const double t = fmod(u * wtot + (double)j * (wtot / (double)n), wtot);
+  for (int j = t; j < n; j += 1024) {
+    const double tt = fmod(u * wtot + (double)j * (wtot / (double)n), wtot);
     int lo = 0, hi = n;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      if (cp[mid] < t) lo = mid + 1;
+      if (cp[mid] < tt) lo = mid + 1;
       else hi = mid;
     }
     newinds[j] = lo;
   }
-  if (threadIdx.x == 0) wout[0] = (T)(wtot / (double)n);
+  if (t == 0) wout[0] = (T)(wtot / (double)n);
 }
 
 // ============================================================================ host side
