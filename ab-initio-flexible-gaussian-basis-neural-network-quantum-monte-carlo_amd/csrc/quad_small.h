@@ -39,40 +39,58 @@ template <typename T> __device__ __forceinline__ T row_class4_sum(T x) {
   return x;
 }
 
-// per-row (configuration) LDS block
+// configurations per wave: 4 (one 16-lane row each) for N <= 4, 2 (one 32-lane half each) for
+// N <= 8; NI = SW / 4 electron slots per configuration
+template <int N> struct QSlot {
+  static constexpr int SW = N <= 4 ? 16 : 32;
+  static constexpr int NI = SW / 4;
+  static constexpr int NSL = 64 / SW;
+};
+// sum over the SW lanes of this configuration's slot
+template <int SW, typename T> __device__ __forceinline__ T slot_sum(T x) {
+  x = row16_sum(x);
+  if constexpr (SW == 32) x += __shfl_xor(x, 16);
+  return x;
+}
+// sum over the slot's lanes 4i + f with equal f (over electrons i, per unit f)
+template <int SW, typename T> __device__ __forceinline__ T slot_class4_sum(T x) {
+  x = row_class4_sum(x);
+  if constexpr (SW == 32) x += __shfl_xor(x, 16);
+  return x;
+}
+
+// per-slot (configuration) LDS block
 template <typename T, int N, int A>
 struct SmemQ {
   static constexpr int D0 = 4 * A;
+  static constexpr int NI = QSlot<N>::NI, SW = QSlot<N>::SW;
   static constexpr int xs = 0;                    // [3N]      positions, the moved electron at its new place
-  static constexpr int xo = xs + 12;              // [3]       old position of the moved electron
+  static constexpr int xo = xs + 3 * NI;          // [3]       old position of the moved electron
   static constexpr int yv = xo + 4;               // [N][N]    Yt
-  static constexpr int hl = yv + 16;              // [N][D0]   ae features
-  static constexpr int g2 = hl + 4 * D0;          // [3][2][N][4] pair column means
-  static constexpr int S = g2 + 3 * 2 * 4 * 4;    // [16][12]  pair values of the patch
-  static constexpr int h3 = S + 16 * 12;          // [N][4]    h-stream output
-  static constexpr int size = h3 + 16;
+  static constexpr int hl = yv + NI * NI;         // [N][D0]   ae features
+  static constexpr int g2 = hl + NI * D0;         // [3][2][N][4] pair column means
+  static constexpr int S = g2 + 3 * 2 * NI * 4;   // [SW][12]  pair values of the patch
+  static constexpr int h3 = S + SW * 12;          // [N][4]    h-stream output
+  static constexpr int size = h3 + NI * 4;
 };
 
-// waves per workgroup (independent; the launch pays per workgroup, see walker_rev.h AQ_PROP_WPB)
-constexpr int QUAD_WPB = 1;   // 4 measured 0.354 vs 0.346 ms (C atom): per-workgroup cost is not the limit here
-
 template <typename T, int N, int A>
-__global__ __launch_bounds__(64 * QUAD_WPB) void k_quad_value(KArgs ka) {
-  static_assert(N <= 4, "four configurations per wave need N <= 4");
+__global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
+  static_assert(N <= 8, "several configurations per wave need N <= 8");
   using Ly = Lay<N, A>;
   using WC = WCache<N, A>;
   using EC = ECache<N, A>;
   using SQ = SmemQ<T, N, A>;
   constexpr int D0 = 4 * A;
+  constexpr int SW = QSlot<N>::SW, NI = QSlot<N>::NI, NSL = QSlot<N>::NSL;
   const cptr<T> P = param_ptr<T>(ka.prm);
-  __shared__ T smq[QUAD_WPB * 4 * SQ::size];
-  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int lane = threadIdx.x & 63;
-  const int slot = lane >> 4, sl = lane & 15;
-  const int c0 = (xcd_major(blockIdx.x, gridDim.x) * QUAD_WPB + wv) * 4 + slot;
+  __shared__ T smq[NSL * SQ::size];
+  const int lane = threadIdx.x;
+  const int slot = lane / SW, sl = lane % SW;
+  const int c0 = xcd_major(blockIdx.x, gridDim.x) * NSL + slot;
   const bool act = c0 < ka.nconf;
   const int conf = act ? c0 : ka.nconf - 1;
-  T* sm = smq + (wv * 4 + slot) * SQ::size;
+  T* sm = smq + slot * SQ::size;
   T* xs = sm + SQ::xs;
   T* Yv = sm + SQ::yv;
   T* hl = sm + SQ::hl;
@@ -88,29 +106,29 @@ __global__ __launch_bounds__(64 * QUAD_WPB) void k_quad_value(KArgs ka) {
   const T* Eq = (const T*)ka.ecache + (size_t)conf * EC::size;
 
   // ---------------------------------------------------------------- F1 cached stage of walker pb
-  if (sl < 3 * N) {
-    const T x0 = ((const T*)ka.pos)[(size_t)pb * 3 * N + sl];
-    const bool mv = sl / 3 == pi;
-    if (mv) sm[SQ::xo + sl - 3 * pi] = x0;
-    xs[sl] = mv ? Eq[EC::xp + sl - 3 * pi] : x0;
+  for (int idx = sl; idx < 3 * N; idx += SW) {
+    const T x0 = ((const T*)ka.pos)[(size_t)pb * 3 * N + idx];
+    const bool mv = idx / 3 == pi;
+    if (mv) sm[SQ::xo + idx - 3 * pi] = x0;
+    xs[idx] = mv ? Eq[EC::xp + idx - 3 * pi] : x0;
   }
-  if (sl < N * N) {
-    const int r = sl / N;
-    Yv[sl] = r == pi ? Eq[EC::yv + sl - r * N] : Wc[WC::yv + sl];
+  for (int idx = sl; idx < N * N; idx += SW) {
+    const int r = idx / N;
+    Yv[idx] = r == pi ? Eq[EC::yv + idx - r * N] : Wc[WC::yv + idx];
   }
-  for (int idx = sl; idx < N * D0; idx += 16) {
+  for (int idx = sl; idx < N * D0; idx += SW) {
     const int e = idx / D0;
     hl[idx] = e == pi ? Eq[EC::h0 + idx - e * D0] : Wc[WC::h0 + idx];
   }
-  for (int idx = sl; idx < 3 * 2 * N * 4; idx += 16) g2[idx] = Wc[WC::g2 + idx];
+  for (int idx = sl; idx < 3 * 2 * N * 4; idx += SW) g2[idx] = Wc[WC::g2 + idx];
   T jsum = sl < N ? (sl == pi ? Eq[EC::jv] : Wc[WC::jaev + sl]) : T(0);
   if (sl == 0) jsum += Wc[WC::jee];
   wave_sync();
 
   // ---------------------------------------------------------------- F2 pairs of the moved electron
-  // lane 4 part + o: part 0/1 pair (pi, o) at the new/old x_pi (column o), part 2/3 pair (o, pi)
+  // lane NI part + o: part 0/1 pair (pi, o) at the new/old x_pi (column o), part 2/3 pair (o, pi)
   {
-    const int part = sl >> 2, o = sl & 3;
+    const int part = sl / NI, o = sl % NI;
     const int os = o < N ? o : N - 1;
     const T* xp = (part & 1) ? sm + SQ::xo : xs + pi * 3;
     T d[3];
@@ -136,24 +154,24 @@ __global__ __launch_bounds__(64 * QUAD_WPB) void k_quad_value(KArgs ka) {
     for (int l = 0; l < 3; ++l)
 #pragma unroll
       for (int f = 0; f < 4; ++f)
-        g2[((l * 2 + Gp) * N + sl) * 4 + f] += (S[sl * 12 + l * 4 + f] - S[(4 + sl) * 12 + l * 4 + f]) * gw;
+        g2[((l * 2 + Gp) * N + sl) * 4 + f] += (S[sl * 12 + l * 4 + f] - S[(NI + sl) * 12 + l * 4 + f]) * gw;
   }
 #pragma unroll
-  for (int t0 = 0; t0 < 24; t0 += 16) {
+  for (int t0 = 0; t0 < 24; t0 += SW) {
     const int t = t0 + sl;
     if (t < 24) {
       const int l = t >> 3, G = (t >> 2) & 1, f = t & 3;
       const int k0 = G ? nup : 0, k1 = G ? N : nup;
       T acc = T(0);
       for (int k = k0; k < k1; ++k)
-        if (k != pi) acc += S[(8 + k) * 12 + l * 4 + f] - S[(12 + k) * 12 + l * 4 + f];
+        if (k != pi) acc += S[(2 * NI + k) * 12 + l * 4 + f] - S[(3 * NI + k) * 12 + l * 4 + f];
       g2[((l * 2 + G) * N + pi) * 4 + f] += acc * (G ? ginv1 : ginv0);
     }
   }
   wave_sync();
 
   // ---------------------------------------------------------------- F4 h-stream layers
-  // (the arithmetic of k_walker_rev's F4, lane 4i + f inside the row)
+  // (the arithmetic of k_walker_rev's F4, lane 4i + f inside the slot)
   const int fi = sl >> 2, ff = sl & 3;
   const bool ilive = fi < N;
   const int ic = ilive ? fi : N - 1;
@@ -178,8 +196,8 @@ __global__ __launch_bounds__(64 * QUAD_WPB) void k_quad_value(KArgs ka) {
     for (int t = 0; t < D0 / 4; ++t) {
       if (t < T4) {
         const T x = ilive ? hown[t] : T(0);
-        gown[0][t] = row_class4_sum(inG1 ? T(0) : x) * ginv0;
-        gown[1][t] = row_class4_sum(inG1 ? x : T(0)) * ginv1;
+        gown[0][t] = slot_class4_sum<SW>(inG1 ? T(0) : x) * ginv0;
+        gown[1][t] = slot_class4_sum<SW>(inG1 ? x : T(0)) * ginv1;
       }
     }
     T zc[QM];
@@ -228,15 +246,16 @@ __global__ __launch_bounds__(64 * QUAD_WPB) void k_quad_value(KArgs ka) {
   if (ilive) H3[ic * 4 + ff] = hreg;
   wave_sync();
 
-  // ---------------------------------------------------------------- F5 log det(Phi (x) Yt), LU in a quad
+  // ---------------------------------------------------------------- F5 log det(Phi (x) Yt), LU in a row
+  // lane c < NI of the slot's first 16-lane row holds column c; column k comes by DPP row_newbcast
   T lsum = T(0), ur = T(1), ui = T(0);
   int inv = 0;
-  if (sl < 4) {
+  if (sl < NI) {
     const int c = sl;
     const int* rowsrc = ka.rowsrc;
-    T ar[4], ai[4];
+    T ar[NI], ai[NI];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < NI; ++r) {
       T a = T(0), b = T(0);
       if (r < N && c < N) {
         const int src = rowsrc[r];
@@ -258,12 +277,11 @@ __global__ __launch_bounds__(64 * QUAD_WPB) void k_quad_value(KArgs ka) {
     unsigned used = 0;
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-      // column k of every row, from lane k of the quad
-      T kr[4], ki[4];
+      T kr[NI], ki[NI];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        kr[r] = k == 0 ? quad_bcast<0>(ar[r]) : (k == 1 ? quad_bcast<1>(ar[r]) : (k == 2 ? quad_bcast<2>(ar[r]) : quad_bcast<3>(ar[r])));
-        ki[r] = k == 0 ? quad_bcast<0>(ai[r]) : (k == 1 ? quad_bcast<1>(ai[r]) : (k == 2 ? quad_bcast<2>(ai[r]) : quad_bcast<3>(ai[r])));
+      for (int r = 0; r < NI; ++r) {
+        kr[r] = row_bcast(ar[r], k);
+        ki[r] = row_bcast(ai[r], k);
       }
       // pivot: first unused row with the largest |re| + |im| (izamax)
       int p = 0;
@@ -307,14 +325,13 @@ __global__ __launch_bounds__(64 * QUAD_WPB) void k_quad_value(KArgs ka) {
       }
     }
   }
-  const T jt = row16_sum(jsum);
+  const T jt = slot_sum<SW>(jsum);
   if (act && sl == 0) {
     const T sg = (inv & 1) ? T(-1) : T(1);
     if (ka.logabs) ((T*)ka.logabs)[conf] = T(0.5) * lsum + jt;
     if (ka.phase) ((T*)ka.phase)[conf] = f_atan2(ui * sg, ur * sg);
   }
 }
-
 
 // ============================================================================================
 // k_quad_grad: the Metropolis proposals of N <= 4 electrons (Be, the C atom's pseudo-valence

@@ -241,15 +241,25 @@ static int set_lds_impl() {
 
 // MODE_GRAD -> reverse-mode value+gradient kernel (walker_rev.h); MODE_LAP -> forward
 // Laplacian kernel (walker_kernel.h); MODE_GRAD_FWD -> forward-mode gradient (diagnostics).
-// single-electron-moved configurations from the walker cache, N <= 4: four configurations per
-// wave (quad_small.h): value only (pp quadrature) or value + gradient (Metropolis proposals)
+// proposal-launch grid: ceil(nconf / wpb) workgroups, padded to a multiple of the 8 XCDs so that
+// xcd_major keeps each walker's proposals on one XCD (the padding workgroups exit at once)
+static inline unsigned prop_blocks(int nconf, int wpb) {
+  const unsigned nb = (unsigned)((nconf + wpb - 1) / wpb);
+  return wpb > 1 ? (nb + 7u) & ~7u : nb;
+}
+
+// single-electron-moved configurations from the walker cache (quad_small.h): value only (pp
+// quadrature, N <= 8) or value + gradient (Metropolis proposals and walker launches, N <= 4),
+// several configurations per wave
 template <typename T, int N, int A>
 static bool quad_small(const KArgs& ka, int nconf, hipStream_t s) {
-  if constexpr (N <= 4) {
+  if constexpr (N <= 8) {   // pp quadrature: 4 (N <= 4) or 2 (N <= 8) configurations per wave
     if (ka.proposal && ka.ecache && ka.value_only && !ka.orb) {
-      k_quad_value<T, N, A><<<dim3((nconf + 4 * QUAD_WPB - 1) / (4 * QUAD_WPB)), dim3(64 * QUAD_WPB), 0, s>>>(ka);
+      k_quad_value<T, N, A><<<dim3(prop_blocks(nconf, QSlot<N>::NSL)), dim3(64), 0, s>>>(ka);
       return true;
     }
+  }
+  if constexpr (N <= 4) {
     if (ka.proposal && ka.ecache && !ka.value_only && !ka.orb && !ka.ablate) {   // Metropolis proposals
       k_quad_grad<T, N, A><<<dim3((nconf + 3) / 4), dim3(64), 0, s>>>(ka);
       return true;
@@ -260,13 +270,6 @@ static bool quad_small(const KArgs& ka, int nconf, hipStream_t s) {
     }
   }
   return false;
-}
-
-// proposal-launch grid: ceil(nconf / wpb) workgroups, padded to a multiple of the 8 XCDs so that
-// xcd_major keeps each walker's proposals on one XCD (the padding workgroups exit at once)
-static inline unsigned prop_blocks(int nconf, int wpb) {
-  const unsigned nb = (unsigned)((nconf + wpb - 1) / wpb);
-  return wpb > 1 ? (nb + 7u) & ~7u : nb;
 }
 
 template <int N, int A>

@@ -112,17 +112,18 @@ def cpu_baseline(name, params, atoms, charges, nsteps_unused, tstep, sample_walk
     }
 
 
-def ecp_side_bench(dtype, device, walkers, steps, cpu_baseline_on):
+def ecp_side_bench(dtype, device, walkers, steps, cpu_baseline_on, name="C_ecp"):
     """BASELINE.json config 'C atom with ccECP pseudopotential, 4096 walkers, 1xMI355X': complex
-    pp local energy (pphamiltonian.py:177-188) of the whole batch, Philox grid rotations."""
+    pp local energy (pphamiltonian.py:177-188) of the whole batch, Philox grid rotations.
+    name="C2_ecp": the reference's example/C2 (8 pseudo-valence electrons, two atoms)."""
     from aiqmc import _lib, systems
     from aiqmc.initial_electrons_positions.init import init_electrons
     from aiqmc.wavefunction_Ynlm.nn import flatten_params
-    s = systems.make_system("C_ecp")
+    s = systems.make_system(name)
     ctx = s.context(dtype=dtype, device=device.index)
     params = s.make_network().init(1)
     ctx.set_params(flatten_params(params))
-    e = systems.ccecp_tables("C_ecp")
+    e = systems.ccecp_tables(name)
     ctx.set_ecp(e.rn_local, e.local_coes, e.local_exps, e.rn_non_local, e.non_local_coes, e.non_local_exps, e.list_l)
     pos, _ = init_electrons(77, None, s.atoms, s.charges, s.spins, walkers, 1.0)
     pos = pos.to(device, dtype).contiguous()
@@ -138,11 +139,13 @@ def ecp_side_bench(dtype, device, walkers, steps, cpu_baseline_on):
     ctx.profile(False)
     q_ms, q_n = ctx.profile_read(_lib.PROF_ECP_QUAD)
     nq = walkers * s.nelectrons * s.natoms * _lib.ECP_NQ
-    res = {"config": "C atom ccECP (Z_eff=4, 4 e-, list_l=2), complex E_L incl. 50-point nonlocal quadrature",
+    cfg = ("C atom ccECP (Z_eff=4, 4 e-, list_l=2)" if name == "C_ecp" else
+           f"{name}: {s.nelectrons} e-, {s.natoms} atoms, ccECP") + ", complex E_L incl. 50-point nonlocal quadrature"
+    res = {"config": cfg,
            "walkers": walkers, "local_energy_evals_per_s": walkers * steps / dt, "ms_per_eval_batch": 1e3 * dt / steps,
            "quadrature_configs_per_launch": nq, "quadrature_launch_avg_ms": q_ms / max(q_n, 1),
            "mean_energy_re": float(out.real.mean()), "finite": bool(torch.isfinite(out.real).all())}
-    if cpu_baseline_on:
+    if cpu_baseline_on and name == "C_ecp":
         sys.path.insert(0, ROOT)
         from oracle import network as onet, pphamiltonian as opp, system as osys
         net = onet.Network(osys.make_system("C_ecp"))
@@ -457,6 +460,10 @@ def main():
                 out["ecp_c_atom"] = ecp_side_bench(dtype, dev, 4096, 5, not args.no_cpu_baseline)
             except Exception as e:  # a side measurement, never a failure of the headline bench
                 out["ecp_c_atom"] = {"error": repr(e)}
+            try:
+                out["ecp_c2"] = ecp_side_bench(dtype, dev, 4096, 3, False, name="C2_ecp")
+            except Exception as e:  # a side measurement, never a failure of the headline bench
+                out["ecp_c2"] = {"error": repr(e)}
         if world == 1 and not args.no_adam:
             try:
                 out["adam_be_atom"] = adam_side_bench(dtype, dev, 4096, 5)
