@@ -1,23 +1,27 @@
-// quad_small.h -- value-only log|psi| and phase of single-electron-moved configurations for
-// N <= 4 electrons, FOUR configurations per wavefront (one 16-lane row each).
+// quad_small.h -- single-electron-moved configurations and walkers of small systems, several
+// configurations per wavefront.
 //
-// These are the pseudopotential quadrature configurations of aiqmc_local_energy_ecp and
-// aiqmc_dmc_tmoves (Energy/pphamiltonian.py:130-190, DMC/Tmoves.py:32-225): electron i of
-// walker b moved to one of the N*A*50 rotated grid points.  k_walker_rev's value-only proposal
-// path evaluates one configuration per 64-lane wave in the N2-sized lane layout; for the C atom
-// (N = 4) that leaves 3/4 of the lanes of every phase idle (838 VALU instructions per
-// configuration, 1.1 ms for the 819,200 configurations of a 4096-walker batch).  Here a 16-lane
-// row holds one configuration:
+// k_quad_value: value-only log|psi| and phase of the pseudopotential quadrature configurations of
+// aiqmc_local_energy_ecp and aiqmc_dmc_tmoves (Energy/pphamiltonian.py:130-190,
+// DMC/Tmoves.py:32-225): electron i of walker b moved to one of the N*A*50 rotated grid points.
+// k_walker_rev's value-only proposal path evaluates one configuration per 64-lane wave in the
+// N2-sized lane layout; for the C atom (N = 4) that leaves 3/4 of the lanes of every phase idle
+// (838 VALU instructions per configuration, 1.1 ms for the 819,200 configurations of a
+// 4096-walker batch).  Here a slot of SW lanes holds one configuration (SW = 16 for N <= 4: four
+// per wave; SW = 32 for N <= 8: two per wave):
 //   F1 walker b's cached stage (WCache: Yt, ae features, pair column sums, J) with electron i's
-//      entries from k_moved_electron's record (ECache), as the proposal path;
+//      entries from the moved-electron record (ECache), as the proposal path;
 //   F2 the pair column sums patched with the 2(N-1) pairs of the moved electron
-//      (lane 4 part + o: new/old x row/column, part 0..3);
+//      (lane NI part + o: new/old x row/column, part 0..3);
 //   F4 the three h-stream layers, lane 4i + f; the spin-group means are class sums inside the
-//      16-lane row (DPP row_ror 4, 8), the conv quads as in k_walker_rev;
+//      slot (DPP row_ror 4, 8, and a lane swizzle across the two rows of a 32-lane slot), the
+//      conv quads as in k_walker_rev;
 //   F5 Phi (x) Yt and its determinant by LU with partial pivoting (LAPACK izamax rule, virtual
-//      row exchanges) inside one quad: lane c of the row's first quad holds column c, column k
-//      is broadcast by DPP quad_perm.  No inverse is needed for values, so no fixed pivot order
-//      and no fallback.
+//      row exchanges): lane c of the slot's first row holds column c, column k is broadcast by
+//      DPP row_newbcast.  No inverse is needed for values, so no fixed pivot order and no
+//      fallback.
+// k_quad_grad (N <= 4, four per wave): the Metropolis proposals (value + gradient) and, WALK,
+// the walker launches -- see its own header below.
 // log|psi| = log|det| + J_ae + J_ee (the Jastrows multiply the matrix, nn.py:504, Q11).
 #pragma once
 #include "walker_rev.h"
@@ -373,7 +377,7 @@ struct SmemQG {
 // (WCache, including the pair tanh's and the pivot record the one-wave proposal path reads).
 template <typename T, int N, int A, bool WALK = false>
 __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
-  static_assert(N <= 4, "four configurations per wave need N <= 4");
+  static_assert(N <= 4, "k_quad_grad: four configurations per wave need N <= 4");
   using Ly = Lay<N, A>;
   using WC = WCache<N, A>;
   using EC = ECache<N, A>;

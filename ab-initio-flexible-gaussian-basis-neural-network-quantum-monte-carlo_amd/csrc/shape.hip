@@ -324,6 +324,14 @@ static void lap_impl(int dtype, const KArgs& k1, const KArgs& k2, int nconf, int
 
 template <int N, int A>
 static void moved_impl(int dtype, const KArgs& ka, hipStream_t s) {
+  if (ka.value_only && ka.xnew) {   // pp quadrature: values only, one configuration per lane
+    const int nv = (ka.nconf + 63) / 64;
+    if (dtype == AIQMC_F32)
+      k_moved_value<float, N, A><<<dim3(prop_blocks(nv, MOVED_WPB)), dim3(64 * MOVED_WPB), 0, s>>>(ka);
+    else
+      k_moved_value<double, N, A><<<dim3(prop_blocks(nv, MOVED_WPB)), dim3(64 * MOVED_WPB), 0, s>>>(ka);
+    return;
+  }
   const int nb = (ka.nconf + 15) / 16;
   if (dtype == AIQMC_F32)
     k_moved_electron<float, N, A><<<dim3(prop_blocks(nb, MOVED_WPB)), dim3(64 * MOVED_WPB), 0, s>>>(ka);

@@ -247,6 +247,42 @@ __global__ __launch_bounds__(64 * MOVED_WPB) void k_moved_electron(KArgs ka) {
   }
 }
 
+// Value-only records for the pp quadrature configurations (ka.value_only): their consumers
+// (k_quad_value, the value-only proposal path) read the Yt row, the ae features, J_ae and the
+// position only, so one configuration per lane (the value row of electron_stage) instead of one
+// per 16-lane direction row: a quarter of the waves.
+template <typename T, int N, int A>
+__global__ __launch_bounds__(64 * MOVED_WPB) void k_moved_value(KArgs ka) {
+  using Ly = Lay<N, A>;
+  using EC = ECache<N, A>;
+  constexpr int D0 = 4 * A;
+  const cptr<T> P = param_ptr<T>(ka.prm);
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  const int q0 = (xcd_major(blockIdx.x, gridDim.x) * MOVED_WPB + wv) * 64 + lane;
+  if (q0 >= ka.nconf) return;
+  const int mper = ka.mper ? ka.mper : N, mdiv = ka.mdiv ? ka.mdiv : 1;
+  const int b = q0 / mper, i = (q0 - b * mper) / mdiv;
+  T xp[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) xp[c] = ((const T*)ka.xnew)[(size_t)q0 * 3 + c];
+  ElecOut<T, A> eo;
+  electron_stage<T, N, A>(P, xp, i, 3, eo);
+  T* E = (T*)ka.ecache + (size_t)q0 * EC::size;
+#pragma unroll
+  for (int col = 0; col < N; ++col) {
+    PJ<T> sy = P[Ly::wy + col] * eo.yst[0];
+#pragma unroll
+    for (int m = 1; m < NYW; ++m) sy = sy + P[Ly::wy + m * N + col] * eo.yst[m];
+    E[EC::yv + col] = (eo.env * sy).v;
+  }
+#pragma unroll
+  for (int m = 0; m < D0; ++m) E[EC::h0 + m] = eo.hf[m].v;
+  E[EC::jv] = eo.jae.v;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) E[EC::xp + c] = xp[c];
+}
+
 // Occupancy hint per instantiation: fp32 N2 (14, 2) lands one VGPR above the
 // 4-waves/SIMD budget (128) without it and fits it without spilling with it.
 // PREP (the adjoint pass of the local energy, walker_lap.h) asks for 2.
