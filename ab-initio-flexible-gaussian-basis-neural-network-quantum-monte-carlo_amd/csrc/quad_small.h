@@ -254,7 +254,69 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
   // lane c < NI of the slot's first 16-lane row holds column c; column k comes by DPP row_newbcast
   T lsum = T(0), ur = T(1), ui = T(0);
   int inv = 0;
-  if (sl < NI) {
+  if constexpr (SW == 16) {
+    // N <= 4: one element per lane, lane 4r + c of the row holds A[r][c].  The pivot row of
+    // column k is the max of packed keys over the column's four lanes (bits of |re| + |im| with
+    // the low two bits replaced by 3 - r: the first maximal row, the izamax rule up to the two
+    // dropped mantissa bits, as gj.h), two DPP row rotations; the pivot comes by row_newbcast,
+    // the pivot row's entry of this lane's column by one lane permute.
+    const int r = sl >> 2, c = sl & 3;
+    const bool rl = r < N;
+    T a = T(0), b = T(0);
+    if (rl && c < N) {
+      const int src = ka.rowsrc[r];
+      const int sp = r < nup ? 0 : 1;
+      T re = P[Ly::orb_b + (sp * N + c) * 2 + 0], im = P[Ly::orb_b + (sp * N + c) * 2 + 1];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const T hv = H3[src * 4 + f];
+        re += hv * P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 0];
+        im += hv * P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 1];
+      }
+      const T y = Yv[r * N + c];
+      a = re * y;
+      b = im * y;
+    }
+    const int rowbase = lane & ~15;
+    unsigned used = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const T akr = k == 0 ? quad_bcast<0>(a) : (k == 1 ? quad_bcast<1>(a) : (k == 2 ? quad_bcast<2>(a) : quad_bcast<3>(a)));
+      const T aki = k == 0 ? quad_bcast<0>(b) : (k == 1 ? quad_bcast<1>(b) : (k == 2 ? quad_bcast<2>(b) : quad_bcast<3>(b)));
+      const bool open = rl && !((used >> r) & 1u);
+      unsigned key = open ? ((key_bits(f_abs(akr) + f_abs(aki)) & ~3u) | (unsigned)(3 - r)) : 0u;
+      {
+        const unsigned k4 = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x124, 0xF, 0xF, true);
+        key = key > k4 ? key : k4;
+        const unsigned k8 = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x128, 0xF, 0xF, true);
+        key = key > k8 ? key : k8;
+      }
+      const int p = 3 - (int)(key & 3u);
+      const T p0r = row_bcast(a, k), p1r = row_bcast(a, 4 + k), p2r = row_bcast(a, 8 + k), p3r = row_bcast(a, 12 + k);
+      const T p0i = row_bcast(b, k), p1i = row_bcast(b, 4 + k), p2i = row_bcast(b, 8 + k), p3i = row_bcast(b, 12 + k);
+      const T pr = p == 0 ? p0r : (p == 1 ? p1r : (p == 2 ? p2r : p3r));
+      const T pim = p == 0 ? p0i : (p == 1 ? p1i : (p == 2 ? p2i : p3i));
+      const T er = __shfl(a, rowbase + 4 * p + c), ei = __shfl(b, rowbase + 4 * p + c);   // A[p][c]
+      inv += __builtin_popcount(used >> p);
+      used |= 1u << p;
+      const T den = pr * pr + pim * pim;
+      const T rden = f_rcp(den);
+      lsum += f_log(den);
+      {
+        const T rm = f_sqrt(rden);
+        const T xr = pr * rm, xi = pim * rm;
+        const T nr = ur * xr - ui * xi, ni = ur * xi + ui * xr;
+        ur = nr;
+        ui = ni;
+      }
+      const T ipr = pr * rden, ipi = -pim * rden;   // 1 / pivot
+      if (rl && !((used >> r) & 1u)) {   // rows still open: A[r][:] -= (A[r][k] / pivot) A[p][:]
+        const T mr = akr * ipr - aki * ipi, mi = akr * ipi + aki * ipr;
+        a -= mr * er - mi * ei;
+        b -= mr * ei + mi * er;
+      }
+    }
+  } else if (sl < NI) {
     const int c = sl;
     const int* rowsrc = ka.rowsrc;
     T ar[NI], ai[NI];
