@@ -735,65 +735,56 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
   wave_sync();
 
   // ---------------------------------------------------------------- F5 Phi, A = Phi (x) Yt, B = A^{-1}
+  // one matrix element per lane (lane 4r + c of the row holds A[r][c]); in-place Gauss-Jordan with
+  // virtual partial pivoting (gj_inverse's steps): after step k the pivot row p_k holds
+  // q = row / pivot (q_k = 1 / pivot), every other row r has a[r][c] - a[r][k] q_c (column k:
+  // -a[r][k] q_k); then B[k][p_c] = X[p_k][c].  The pivot row of column k is the max of packed keys
+  // (|re| + |im| bits, low bits 3 - r) over the column's lanes by two DPP row rotations among the
+  // rows not used yet.
   T lsum = T(0), ur = T(1), ui = T(0);
   int inv = 0;
-  if (sl < 4) {
-    const int c = sl;
-    T ar[4], ai[4];
+  {
+    const int r = sl >> 2, c = sl & 3;
+    const bool rl = r < N;
+    T a = T(0), b = T(0);
+    if (rl && c < N) {
+      const int src = rowsrc[r];
+      const int sp = r < nup ? 0 : 1;
+      T re = P[Ly::orb_b + (sp * N + c) * 2 + 0], im = P[Ly::orb_b + (sp * N + c) * 2 + 1];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      T a = T(0), b = T(0);
-      if (r < N && c < N) {
-        const int src = rowsrc[r];
-        const int sp = r < nup ? 0 : 1;
-        T re = P[Ly::orb_b + (sp * N + c) * 2 + 0], im = P[Ly::orb_b + (sp * N + c) * 2 + 1];
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-          const T hv = H3[src * 4 + f];
-          re += hv * P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 0];
-          im += hv * P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 1];
-        }
-        Ph[(r * N + c) * 2 + 0] = re;
-        Ph[(r * N + c) * 2 + 1] = im;
-        const T y = Yv[r * N + c];
-        a = re * y;
-        b = im * y;
+      for (int f = 0; f < 4; ++f) {
+        const T hv = H3[src * 4 + f];
+        re += hv * P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 0];
+        im += hv * P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 1];
       }
-      ar[r] = a;
-      ai[r] = b;
+      Ph[(r * N + c) * 2 + 0] = re;
+      Ph[(r * N + c) * 2 + 1] = im;
+      const T y = Yv[r * N + c];
+      a = re * y;
+      b = im * y;
     }
-    // in-place Gauss-Jordan with virtual partial pivoting (gj_inverse's steps): after step k the
-    // pivot row p_k holds q = row / pivot (q_k = 1 / pivot), every other row r has
-    // a[r][c] - a[r][k] q_c (column k: -a[r][k] q_k); then B[k][p_c] = X[p_k][c]
+    const int rowbase = lane & ~15;
     unsigned used = 0;
-    int stepk[4] = {0, 0, 0, 0};
-    int myp = 0;
+    int stepk = 0;   // the step at which this lane's row was the pivot row
+    int pc = 0;      // the pivot row of step c (this lane's column)
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-      T kr[4], ki[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        kr[r] = k == 0 ? quad_bcast<0>(ar[r]) : (k == 1 ? quad_bcast<1>(ar[r]) : (k == 2 ? quad_bcast<2>(ar[r]) : quad_bcast<3>(ar[r])));
-        ki[r] = k == 0 ? quad_bcast<0>(ai[r]) : (k == 1 ? quad_bcast<1>(ai[r]) : (k == 2 ? quad_bcast<2>(ai[r]) : quad_bcast<3>(ai[r])));
+      const T akr = k == 0 ? quad_bcast<0>(a) : (k == 1 ? quad_bcast<1>(a) : (k == 2 ? quad_bcast<2>(a) : quad_bcast<3>(a)));
+      const T aki = k == 0 ? quad_bcast<0>(b) : (k == 1 ? quad_bcast<1>(b) : (k == 2 ? quad_bcast<2>(b) : quad_bcast<3>(b)));
+      const bool open = rl && !((used >> r) & 1u);
+      unsigned key = open ? ((key_bits(f_abs(akr) + f_abs(aki)) & ~3u) | (unsigned)(3 - r)) : 0u;
+      {
+        const unsigned k4 = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x124, 0xF, 0xF, true);
+        key = key > k4 ? key : k4;
+        const unsigned k8 = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x128, 0xF, 0xF, true);
+        key = key > k8 ? key : k8;
       }
-      int p = 0;
-      T best = T(-1);
-#pragma unroll
-      for (int r = 0; r < N; ++r) {
-        const T m = f_abs(kr[r]) + f_abs(ki[r]);
-        const bool take = !((used >> r) & 1u) && m > best;
-        best = take ? m : best;
-        p = take ? r : p;
-      }
-      T pr = T(0), pim = T(0), spr = T(0), spi = T(0);
-#pragma unroll
-      for (int r = 0; r < N; ++r)
-        if (r == p) {
-          pr = kr[r];
-          pim = ki[r];
-          spr = ar[r];
-          spi = ai[r];
-        }
+      const int p = 3 - (int)(key & 3u);
+      const T p0r = row_bcast(a, k), p1r = row_bcast(a, 4 + k), p2r = row_bcast(a, 8 + k), p3r = row_bcast(a, 12 + k);
+      const T p0i = row_bcast(b, k), p1i = row_bcast(b, 4 + k), p2i = row_bcast(b, 8 + k), p3i = row_bcast(b, 12 + k);
+      const T pr = p == 0 ? p0r : (p == 1 ? p1r : (p == 2 ? p2r : p3r));
+      const T pim = p == 0 ? p0i : (p == 1 ? p1i : (p == 2 ? p2i : p3i));
+      const T spr = __shfl(a, rowbase + 4 * p + c), spi = __shfl(b, rowbase + 4 * p + c);   // A[p][c]
       inv += __builtin_popcount(used >> p);
       used |= 1u << p;
       const T den = pr * pr + pim * pim;
@@ -806,7 +797,7 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
         ur = nr;
         ui = ni;
       }
-      if (WALK && c == 0 && act) {   // pivot record (gj.h: row of step k, 1 / |pivot_k|)
+      if (WALK && sl == 0 && act) {   // pivot record (gj.h: row of step k, 1 / |pivot_k|)
         Wc[WC::pv + k] = T(p);
         Wc[WC::pv + N + k] = f_sqrt(rden);
       }
@@ -814,25 +805,19 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
       const bool ck = (c == k);
       const T qr = ck ? ir : spr * ir - spi * ii;
       const T qi = ck ? ii : spr * ii + spi * ir;
-#pragma unroll
-      for (int r = 0; r < N; ++r) {
-        const T br = ck ? T(0) : ar[r], bi = ck ? T(0) : ai[r];
-        const T nr = br - (kr[r] * qr - ki[r] * qi);
-        const T ni = bi - (kr[r] * qi + ki[r] * qr);
-        ar[r] = r == p ? qr : nr;
-        ai[r] = r == p ? qi : ni;
-        stepk[r] = r == p ? k : stepk[r];
-      }
-      myp = ck ? p : myp;
+      const T br = ck ? T(0) : a, bi = ck ? T(0) : b;
+      const T nr = br - (akr * qr - aki * qi);
+      const T ni = bi - (akr * qi + aki * qr);
+      a = r == p ? qr : nr;
+      b = r == p ? qi : ni;
+      stepk = r == p ? k : stepk;
+      pc = ck ? p : pc;
     }
-    if (c < N) {
-#pragma unroll
-      for (int r = 0; r < N; ++r) {
-        Mx[(stepk[r] * N + myp) * 2 + 0] = ar[r];
-        Mx[(stepk[r] * N + myp) * 2 + 1] = ai[r];
-      }
+    if (rl && c < N) {
+      Mx[(stepk * N + pc) * 2 + 0] = a;
+      Mx[(stepk * N + pc) * 2 + 1] = b;
     }
-    if (WALK && c == 0 && act) {
+    if (WALK && sl == 0 && act) {
       Wc[WC::pv + 2 * N] = T(inv & 1);
       Wc[WC::pv + 2 * N + 1] = T(0.5) * lsum;
     }
