@@ -5,9 +5,17 @@ dict, params, opt_state) via ``np.savez``; device tensors are copied to host num
 first, so a file written here holds plain numpy leaves.  ``restore`` returns
 ``(t + 1, AINetData, params, opt_state)`` as the reference does (:63-70).  Reading never
 unpickles: ``restore``/``find_last_checkpoint`` go through the weights-only interpreter of
-``utils.safe_npz`` (numpy/JAX arrays, numpy scalars, containers and optax state records;
-anything else in the file is refused), so the reference's own pickled-pytree checkpoints
-load without JAX and without executing anything from the file.
+``utils.safe_npz`` (numpy/JAX arrays, numpy scalars, containers, optax state records and
+kfac_jax optimizer states; anything else in the file is refused), so the reference's own
+pickled-pytree checkpoints -- e.g. ``AIQMCrelease3/example/C2/Save/qmcjax_ckpt_000009.npz``,
+whose ``opt_state`` is a ``kfac_jax.Optimizer.State`` -- load without JAX and without
+executing anything from the file.
+
+``find_last_checkpoint`` keeps the reference's "try the next file" rule for files that are
+truncated or corrupt (checkpoint.py:19-23), but a file the weights-only interpreter REFUSES
+(a global outside its vocabulary) raises :class:`UnsafeCheckpointError` naming the file and
+the global: silently starting from scratch next to a checkpoint that exists would hide it.
+``skip_refused=True`` restores the plain skip (logged at ERROR level).
 """
 from __future__ import annotations
 
@@ -36,8 +44,9 @@ def _host(tree: Any) -> Any:
     return tree
 
 
-def find_last_checkpoint(ckpt_path: Optional[str] = None) -> Optional[str]:
-    """checkpoint.py:13-24: newest loadable qmcjax_ckpt file, or None."""
+def find_last_checkpoint(ckpt_path: Optional[str] = None, skip_refused: bool = False) -> Optional[str]:
+    """checkpoint.py:13-24: newest loadable qmcjax_ckpt file, or None.  Corrupt files are
+    skipped as in the reference; a refused one raises unless ``skip_refused``."""
     if ckpt_path and os.path.exists(ckpt_path):
         files = [f for f in os.listdir(ckpt_path) if "qmcjax_ckpt" in f]
         for file in sorted(files, reverse=True):
@@ -46,7 +55,12 @@ def find_last_checkpoint(ckpt_path: Optional[str] = None) -> Optional[str]:
                 with open(fname, "rb") as f:
                     load_npz(f)
                 return fname
-            except (OSError, EOFError, zipfile.BadZipFile, ValueError, KeyError, UnsafeCheckpointError):
+            except UnsafeCheckpointError as e:
+                if not skip_refused:
+                    raise UnsafeCheckpointError(f"{fname}: {e}") from e
+                logging.error("Checkpoint %s refused by the weights-only reader (%s). Trying next checkpoint...",
+                              fname, e)
+            except (OSError, EOFError, zipfile.BadZipFile, ValueError, KeyError):
                 logging.info("Error loading checkpoint %s. Trying next checkpoint...", fname)
     return None
 

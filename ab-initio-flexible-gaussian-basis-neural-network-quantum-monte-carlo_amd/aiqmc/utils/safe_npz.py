@@ -15,9 +15,18 @@ result itself from a fixed vocabulary:
 * ``numpy.dtype(spec, align, copy)`` + BUILD(byte order), numpy ``scalar(dtype, bytes)``;
 * JAX ``_reconstruct_array`` -> the numpy array it wraps (device placement dropped);
 * ``collections.OrderedDict`` -> dict;
-* optax state NamedTuples (``RECORD_TYPES``) -> :class:`Record` (name + fields, tuple-like).
+* optax state NamedTuples (``RECORD_TYPES``) -> :class:`Record` (name + fields, tuple-like);
+* kfac_jax optimizer states (``main/main_pp.py`` checkpoints ``opt_state`` of
+  ``kfac_jax.Optimizer``; every release2/release3 checkpoint the reference ships holds one):
+  the stream names the state class as ``builtins.getattr(<class>, "State")`` and builds it by
+  ``NEWOBJ(cls, ())`` + ``BUILD(field dict)``.  ``getattr`` is accepted only as that exact
+  pattern -- a class marker from ``STATE_OWNERS`` and the literal attribute ``"State"`` --
+  and yields another marker, never an attribute lookup; the object becomes a
+  :class:`StateRecord` (class name + field dict) and nothing else.  ``STATE_TYPES`` lists
+  the dataclasses built directly (``WeightedMovingAverage``).
 
-Any other global, or an opcode outside the vocabulary, raises :class:`UnsafeCheckpointError`.
+Any other global, an opcode outside the vocabulary, or a self-referential container raises
+:class:`UnsafeCheckpointError`.
 """
 from __future__ import annotations
 
@@ -29,7 +38,8 @@ from typing import Any, Dict, List, Tuple
 import numpy as np
 from numpy.lib import format as npformat
 
-__all__ = ["UnsafeCheckpointError", "Record", "load_npz", "loads_pickle_stream", "RECORD_TYPES"]
+__all__ = ["UnsafeCheckpointError", "Record", "StateRecord", "load_npz", "loads_pickle_stream", "RECORD_TYPES",
+           "STATE_OWNERS", "STATE_TYPES"]
 
 
 class UnsafeCheckpointError(ValueError):
@@ -48,6 +58,24 @@ class Record(tuple):
         return f"Record({self.type_name}, {tuple(self)!r})"
 
 
+class StateRecord(dict):
+    """A dataclass state from the stream (kfac_jax): field dict + the original class name.
+    Fields read as items or attributes (``rec["velocities"]`` / ``rec.velocities``)."""
+
+    def __init__(self, name: str, fields: Dict[str, Any]):
+        super().__init__(fields)
+        self.type_name = name
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError:
+            raise AttributeError(k) from None
+
+    def __repr__(self):
+        return f"StateRecord({self.type_name}, {dict.__repr__(self)})"
+
+
 # NamedTuple classes of the optimizer states the drivers checkpoint (optax chain of
 # scale_by_adam / scale_by_schedule / scale, main_all_electrons_adam_muti_GPU.py:152-158).
 RECORD_TYPES = {
@@ -57,6 +85,24 @@ RECORD_TYPES = {
     "optax._src.base EmptyState",
     "optax._src.transform ScaleByRmsState",
     "optax._src.transform TraceState",
+}
+# Classes whose nested ``State`` dataclass may be named through getattr(<class>, "State")
+# (kfac_jax 0.0.x: optimizer, curvature estimator and the curvature blocks the network's
+# layers map to; the reference's KFAC driver registers dense and scale-and-shift blocks,
+# Optimizer/curvature_tags_and_blocks.py).
+STATE_OWNERS = {
+    "kfac_jax._src.optimizer Optimizer",
+    "kfac_jax._src.curvature_estimator BlockDiagonalCurvature",
+    "kfac_jax._src.curvature_blocks Diagonal",
+    "kfac_jax._src.curvature_blocks Full",
+    "kfac_jax._src.curvature_blocks KroneckerFactored",
+    "kfac_jax._src.curvature_blocks TwoKroneckerFactored",
+    "kfac_jax._src.curvature_blocks ScaleAndShiftDiagonal",
+    "kfac_jax._src.curvature_blocks ScaleAndShiftFull",
+}
+# Dataclasses built directly by NEWOBJ(cls, ()) + BUILD(fields).
+STATE_TYPES = {
+    "kfac_jax._src.utils.accumulators WeightedMovingAverage",
 }
 _NUMPY_MODULES = ("numpy.core.multiarray", "numpy._core.multiarray")
 
@@ -79,6 +125,24 @@ class _DType:
         if isinstance(state, tuple) and len(state) >= 2 and state[1] in ("<", ">", "|", "=") \
                 and self.dtype.kind not in ("O", "V"):
             self.dtype = self.dtype.newbyteorder(state[1]) if state[1] in "<>" else self.dtype
+
+
+class _Object:
+    """A STATE_TYPES / <owner>.State object under construction: BUILD fills its fields."""
+
+    def __init__(self, name: str):
+        self.name = name
+        self.fields: Dict[str, Any] = {}
+
+    def build(self, state):
+        # object.__reduce_ex__ state: the instance dict, or (dict | None, slots dict | None).
+        parts = state if isinstance(state, tuple) and len(state) == 2 else (state,)
+        for part in parts:
+            if part is None:
+                continue
+            if not isinstance(part, dict) or not all(isinstance(k, str) for k in part):
+                raise UnsafeCheckpointError(f"unexpected state of {self.name}")
+            self.fields.update(part)
 
 
 class _Array:
@@ -124,6 +188,12 @@ def _global(module: str, name: str):
         return _Marker("odict")
     if full in RECORD_TYPES:
         return _Marker("record:" + full)
+    if module == "builtins" and name == "getattr":
+        return _Marker("getattr")
+    if full in STATE_OWNERS:
+        return _Marker("owner:" + full)
+    if full in STATE_TYPES:
+        return _Marker("state:" + full)
     raise UnsafeCheckpointError(f"refusing global {module}.{name}")
 
 
@@ -158,15 +228,51 @@ def _call(fn, args: tuple):
         return d
     if k.startswith("record:"):
         return Record(k[len("record:"):].split(" ")[1], args)
+    if k == "getattr":
+        if not (len(args) == 2 and isinstance(args[0], _Marker) and args[0].name.startswith("owner:")
+                and args[1] == "State"):
+            raise UnsafeCheckpointError("getattr outside the <kfac class>.State pattern")
+        return _Marker("state:" + args[0].name[len("owner:"):] + ".State")
     raise UnsafeCheckpointError(f"cannot call {k}")
 
 
+def _newobj(cls, args: tuple):
+    """NEWOBJ: namedtuple records (cls(*fields)) or an empty state object filled by BUILD."""
+    if isinstance(cls, _Marker) and cls.name.startswith("state:"):
+        if args:
+            raise UnsafeCheckpointError(f"unexpected constructor arguments for {cls.name}")
+        mod_cls = cls.name[len("state:"):].split(" ", 1)[1]
+        return _Object(mod_cls)
+    return _call(cls, args)
+
+
+_IN_PROGRESS = object()
+
+
 def _resolve(obj, seen=None):
+    """Replace the construction helpers by their values.  Mutable containers are registered
+    before their children are visited (a memo reference back to them resolves to the same
+    object); an immutable one reached again while it is being resolved is a cycle that a
+    weights-only file never holds, and is refused."""
     if seen is None:
         seen = {}
     oid = id(obj)
     if oid in seen:
+        if seen[oid] is _IN_PROGRESS:
+            raise UnsafeCheckpointError("self-referential object in the stream")
         return seen[oid]
+    if isinstance(obj, dict) and not isinstance(obj, StateRecord):
+        out = {}
+        seen[oid] = out
+        for k, v in obj.items():
+            out[_resolve(k, seen)] = _resolve(v, seen)
+        return out
+    if isinstance(obj, list):
+        out = []
+        seen[oid] = out
+        out.extend(_resolve(v, seen) for v in obj)
+        return out
+    seen[oid] = _IN_PROGRESS
     if isinstance(obj, _Array):
         if obj.value is None:
             raise UnsafeCheckpointError("ndarray never built")
@@ -177,12 +283,10 @@ def _resolve(obj, seen=None):
                 flat[i] = _resolve(flat[i], seen)
     elif isinstance(obj, _DType):
         out = obj.dtype
+    elif isinstance(obj, _Object):
+        out = StateRecord(obj.name, {k: _resolve(v, seen) for k, v in obj.fields.items()})
     elif isinstance(obj, Record):
         out = Record(obj.type_name, [_resolve(v, seen) for v in obj])
-    elif isinstance(obj, dict):
-        out = {_resolve(k, seen): _resolve(v, seen) for k, v in obj.items()}
-    elif isinstance(obj, list):
-        out = [_resolve(v, seen) for v in obj]
     elif isinstance(obj, tuple):
         out = tuple(_resolve(v, seen) for v in obj)
     elif isinstance(obj, np.ndarray) and obj.dtype.hasobject:
@@ -224,7 +328,10 @@ def loads_pickle_stream(data: bytes):
         if n == "STOP":
             if len(stack) != 1:
                 raise UnsafeCheckpointError("malformed stream")
-            return _resolve(stack[0])
+            try:
+                return _resolve(stack[0])
+            except RecursionError as e:
+                raise UnsafeCheckpointError("object nesting too deep") from e
         if n in _PUSH_CONST:
             stack.append(_PUSH_CONST[n])
         elif n in _PUSH_ARG:
@@ -295,11 +402,11 @@ def loads_pickle_stream(data: bytes):
         elif n == "NEWOBJ":
             args = stack.pop()
             cls = stack.pop()
-            stack.append(_call(cls, tuple(args)))
+            stack.append(_newobj(cls, tuple(args)))
         elif n == "BUILD":
             state = stack.pop()
             obj = stack[-1]
-            if isinstance(obj, (_Array, _DType)):
+            if isinstance(obj, (_Array, _DType, _Object)):
                 obj.build(state)
             elif isinstance(obj, dict) and isinstance(state, dict):
                 obj.update(state)

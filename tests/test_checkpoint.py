@@ -149,3 +149,132 @@ def test_safe_loader_refuses_foreign_globals(tmp_path):
     with pytest.raises(UnsafeCheckpointError):
         load_npz(io.BytesIO(buf.getvalue()))
     assert not marker.exists()
+
+
+_REF_C2 = "/root/reference/AIQMCrelease3/example/C2/Save"
+
+
+def test_restore_reference_release3_kfac_checkpoint():
+    """The reference's own release3 checkpoint (example/C2/Save, written by the KFAC
+    driver): opt_state pickles kfac_jax.Optimizer.State through builtins.getattr.  Read from
+    /root/reference as data only (never executed); skipped where the reference is absent."""
+    import pytest
+    if not os.path.isdir(_REF_C2):
+        pytest.skip("reference tree absent (GPU box)")
+    import sys
+    from aiqmc import checkpoint
+    from aiqmc.utils.safe_npz import StateRecord
+    last = checkpoint.find_last_checkpoint(_REF_C2)
+    assert os.path.basename(last) == "qmcjax_ckpt_000009.npz"
+    t, data, params, opt = checkpoint.restore(last)
+    assert t == 10                                  # saved at t = 9, resumes at t + 1 (checkpoint.py:67)
+    # pmapped layout [ndev=1, B=4, 3N=24] (C2 ECP: 8 valence electrons, 2 atoms)
+    assert data.positions.shape == (1, 4, 24) and data.positions.dtype == np.float32
+    assert data.atoms.shape == (1, 4, 2, 3) and data.charges.shape == (1, 4, 2)
+    assert data.spins.shape == (1, 4, 8)
+    # release2-style network tree (SURVEY F7): envelope[k] = {pi, sigma}, no convolutional layer
+    assert sorted(params) == ["envelope", "jastrow_ee", "layers", "orbitals", "y"]
+    assert len(params["envelope"]) == 2 and sorted(params["envelope"][0]) == ["pi", "sigma"]
+    assert params["envelope"][0]["pi"].shape == (1, 2, 8)
+    assert [sorted(s) for s in params["layers"]["streams"]] == [["double", "single"]] * 2 + [["single"]]
+    assert params["orbitals"][0]["w"].shape == (1, 4, 16)
+    assert params["jastrow_ee"]["ee_par"].shape == (1, 12) and params["jastrow_ee"]["ee_anti"].shape == (1, 16)
+    for leaf in (params["y"][0]["w"], params["layers"]["streams"][2]["single"]["w"]):
+        assert np.all(np.isfinite(leaf))
+    # kfac_jax optimizer state: a StateRecord tree, the velocities mirroring params
+    assert isinstance(opt, StateRecord) and opt.type_name == "Optimizer.State"
+    assert sorted(opt) == ["damping", "data_seen", "estimator_state", "step_counter", "velocities"]
+    assert int(np.asarray(opt.step_counter).reshape(-1)[0]) == 10
+    assert int(np.asarray(opt.data_seen).reshape(-1)[0]) == 40         # 10 steps x 4 walkers
+    assert sorted(opt.velocities) == sorted(params)
+    assert opt.velocities["orbitals"][0]["w"].shape == params["orbitals"][0]["w"].shape
+    est = opt.estimator_state
+    assert est.type_name == "BlockDiagonalCurvature.State"
+    names = {b.type_name for b in est.blocks_states}
+    assert names <= {"Diagonal.State", "KroneckerFactored.State"} and "KroneckerFactored.State" in names
+    assert "jax" not in sys.modules and "kfac_jax" not in sys.modules
+
+
+def test_every_reference_checkpoint_loads():
+    """All 45 qmcjax_ckpt files the reference ships (release2 H2/C2/CO2/..., release3 C2) go
+    through the weights-only reader."""
+    import glob
+    import pytest
+    files = sorted(glob.glob("/root/reference/**/qmcjax_ckpt_*.npz", recursive=True))
+    if not files:
+        pytest.skip("reference tree absent (GPU box)")
+    from aiqmc.utils.safe_npz import load_npz
+    for f in files:
+        ck = load_npz(f)
+        assert set(ck) == {"t", "data", "params", "opt_state"}, f
+        assert ck["data"].item()["positions"].dtype.kind == "f", f
+
+
+def _npz_with_stream(path, stream, name="params.npy"):
+    import zipfile
+    hdr = io_mod().BytesIO()
+    np.lib.format.write_array_header_1_0(hdr, {"descr": "|O", "fortran_order": False, "shape": ()})
+    with zipfile.ZipFile(path, "w") as z:
+        z.writestr("t.npy", _npy_int(9))
+        z.writestr(name, b"\x93NUMPY\x01\x00" + hdr.getvalue()[8:] + stream)
+
+
+def io_mod():
+    import io
+    return io
+
+
+def _npy_int(v):
+    b = io_mod().BytesIO()
+    np.save(b, np.int64(v))
+    return b.getvalue()
+
+
+def test_getattr_only_in_the_kfac_state_pattern():
+    import pytest
+    from aiqmc.utils.safe_npz import StateRecord, UnsafeCheckpointError, loads_pickle_stream
+    # getattr(kfac_jax._src.optimizer.Optimizer, "State")() + BUILD({"step_counter": 3})
+    good = (b"\x80\x03cbuiltins\ngetattr\nckfac_jax._src.optimizer\nOptimizer\nX\x05\x00\x00\x00State"
+            b"\x86R)\x81}X\x0c\x00\x00\x00step_counterK\x03sb.")
+    rec = loads_pickle_stream(good)
+    assert isinstance(rec, StateRecord) and rec.type_name == "Optimizer.State" and rec.step_counter == 3
+    # any other attribute, or getattr on a class outside the allowlist, is refused
+    for bad in (good.replace(b"State", b"__new"),
+                b"\x80\x03cbuiltins\ngetattr\ncos\nsystem\nX\x05\x00\x00\x00State\x86R.",
+                b"\x80\x03cbuiltins\ngetattr\nckfac_jax._src.optimizer\nOptimizer\nX\x05\x00\x00\x00State"
+                b"\x86R.",                                             # dangling class marker
+                b"\x80\x03cbuiltins\ngetattr\nckfac_jax._src.optimizer\nOptimizer\nX\x05\x00\x00\x00State"
+                b"\x86R)\x81K\x01b."):                                 # BUILD with a non-dict state
+        with pytest.raises(UnsafeCheckpointError):
+            loads_pickle_stream(bad)
+
+
+def test_self_referential_stream_is_refused_not_recursed():
+    import pytest
+    from aiqmc.utils.safe_npz import UnsafeCheckpointError, loads_pickle_stream
+    # memo references back to a list resolve to the same object instead of recursing
+    # (ADVICE r2: the seen-entry is made before descending): L = [L] and L = [(L,)]
+    lst = loads_pickle_stream(b"\x80\x03]q\x00h\x00a.")
+    assert lst[0] is lst
+    lst = loads_pickle_stream(b"\x80\x03]q\x00h\x00\x85q\x01a.")
+    assert isinstance(lst[0], tuple) and lst[0][0] is lst
+    # deep nesting is refused instead of escaping as a RecursionError
+    deep = b"\x80\x03" + b"]" * 5000 + b"a" * 4999 + b"."
+    with pytest.raises(UnsafeCheckpointError):
+        loads_pickle_stream(deep)
+
+
+def test_find_last_checkpoint_refused_vs_corrupt(tmp_path):
+    import logging
+    import pytest
+    from aiqmc import checkpoint
+    from aiqmc.utils.safe_npz import UnsafeCheckpointError
+    d = tmp_path / "Save"
+    d.mkdir()
+    _npz_with_stream(d / "qmcjax_ckpt_000002.npz", b"\x80\x03]q\x00.")          # loadable
+    (d / "qmcjax_ckpt_000003.npz").write_bytes(b"PK\x03\x04 truncated")        # corrupt: skipped
+    assert checkpoint.find_last_checkpoint(str(d)) == str(d / "qmcjax_ckpt_000002.npz")
+    _npz_with_stream(d / "qmcjax_ckpt_000004.npz", b"\x80\x03cos\nsystem\n)R.")  # refused: raises
+    with pytest.raises(UnsafeCheckpointError, match="os.system"):
+        checkpoint.find_last_checkpoint(str(d))
+    assert checkpoint.find_last_checkpoint(str(d), skip_refused=True) == str(d / "qmcjax_ckpt_000002.npz")
