@@ -20,7 +20,9 @@ batch_size / world walkers.  Kept from the reference:
 * the block estimate is the weighted average over all blocks so far and all devices (:190);
 * e_trial feedback uses jnp.mean over the per-device comb weights (:237): all-reduced here.
 Multi-rank housekeeping: rank 0 alone writes the checkpoint and the CSV, with the positions
-of all ranks gathered (the reference's arrays are global).  Deviations (documented in
+of all ranks gathered (the reference's arrays are global).  Whether a block checkpoints is
+decided by rank 0's clock and broadcast (``make_checkpoint_hook``): every rank enters the
+gather together, so the collectives never pair up across different call sites.  Deviations (documented in
 DESIGN.md): the Philox key offset advances every step (the reference passes the same
 ``subkeys`` to every step, :162); the re-indexing pads each device block to its own walker
 count (the reference compares the unique count with the GLOBAL batch_size, which only
@@ -71,8 +73,48 @@ def _gather_walkers(x: torch.Tensor, world: int) -> torch.Tensor:
     return torch.cat(parts, dim=0)
 
 
+def _rank0_decides(flag: bool, world: int, device) -> bool:
+    """Rank 0's flag on every rank (one MAX all-reduce of rank 0's value; other ranks add 0)."""
+    if world == 1:
+        return flag
+    rank = dist.get_rank()
+    if dist.get_backend() == "nccl" and device.type != "cuda":
+        device = torch.device("cuda", torch.cuda.current_device())
+    t = torch.tensor([1 if (flag and rank == 0) else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return bool(t.item())
+
+
+def make_checkpoint_hook(out_dir: str, params, opt_state, save_frequency: float, clock=time.time):
+    """on_block hook of main_dmc.py:195-200: a checkpoint when more than ``save_frequency``
+    minutes passed since the last one.  Rank 0's clock decides for all ranks (the reference
+    runs one process, so it has one clock); then every rank joins the gather of the walkers and
+    rank 0 writes.  ``clock`` is injectable for the multi-rank test."""
+    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    rank = dist.get_rank() if world > 1 else 0
+    last = [clock()]
+    saved = []
+
+    def on_block(block, e_est, data):
+        del e_est
+        due = _rank0_decides(clock() - last[0] > save_frequency * 60, world, data.positions.device)
+        if not due:
+            return
+        all_pos = _gather_walkers(data.positions, world)
+        if rank == 0:
+            saved.append(checkpoint.save(out_dir, block, nn.AINetData(positions=all_pos, spins=data.spins,
+                                                                      atoms=data.atoms, charges=data.charges),
+                                         params, opt_state))
+        if world > 1:
+            dist.barrier()
+        last[0] = clock()
+
+    on_block.saved = saved
+    return on_block
+
+
 def dmc_blocks(run, ctx, params, data, e_l0, variance0, nblocks: int, iterations: int, feedback: float,
-               step_key, block_draws, t_init: int = 0, on_block=None, writer=None):
+               step_key, block_draws, t_init: int = 0, on_block=None, writer=None, trace: bool = False):
     """The block loop of main_dmc.py:113-244 over this rank's walkers.
 
     run: dmc_propagate_run; ctx: the bound HIP context (comb); e_l0 [B] / variance0: total_e of
@@ -80,8 +122,10 @@ def dmc_blocks(run, ctx, params, data, e_l0, variance0, nblocks: int, iterations
     sqrt(variance0) = jnp.std(e_est), :113-118); step_key(step) -> the key of one
     dmc_propagate_run call (PhiloxKey or HostDmcDraws); block_draws(block) -> (u, extra) with
     u the comb's uniform (branch.py:17) and extra [B,3N] the re-indexing noise (:222).
-    Returns (block estimates, data, weights, trace) -- trace holds per-step energies / weights
-    and per-block comb indices for the parity tests."""
+    Returns (block estimates, data, weights, trace).  With ``trace=True`` (the parity tests)
+    trace holds device copies of every step's energies / weights / positions and every block's
+    comb indices; otherwise it is None and nothing per step is kept beyond the reference's own
+    [nblocks, iterations, B] energy and weight arrays."""
     world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
     B = data.positions.shape[0]
     dev = data.positions.device
@@ -94,7 +138,8 @@ def dmc_blocks(run, ctx, params, data, e_l0, variance0, nblocks: int, iterations
     energy_data = torch.zeros(nblocks, iterations, B, dtype=torch.float64, device=dev)
     weights_data = torch.zeros_like(energy_data)
     estimates = []
-    trace = {"energy": [], "weights": [], "positions": [], "newinds": [], "comb_weight": [], "e_trial": []}
+    tr = {"energy": [], "weights": [], "positions": [], "newinds": [], "comb_weight": [], "e_trial": []} \
+        if trace else None
     step = 0
     for block in range(nblocks):
         for t in range(t_init, t_init + iterations):
@@ -103,9 +148,10 @@ def dmc_blocks(run, ctx, params, data, e_l0, variance0, nblocks: int, iterations
             step += 1
             energy_data[block, t - t_init] = energy.real.to(torch.float64)
             weights_data[block, t - t_init] = weights.to(torch.float64)
-            trace["energy"].append(energy.detach().clone())
-            trace["weights"].append(weights.detach().clone())
-            trace["positions"].append(data.positions.detach().clone())
+            if tr is not None:
+                tr["energy"].append(energy.detach().clone())
+                tr["weights"].append(weights.detach().clone())
+                tr["positions"].append(data.positions.detach().clone())
         # :190 jnp.average over the global [nblocks, iterations, batch] arrays
         v = torch.stack([(energy_data * weights_data).sum(), weights_data.sum()])
         if world > 1:
@@ -125,13 +171,14 @@ def dmc_blocks(run, ctx, params, data, e_l0, variance0, nblocks: int, iterations
             wmean /= world
         e_trial = complex(e_est.real - feedback * float(torch.log(wmean).item()), 0.0)
         estimates.append(e_est.real)
-        trace["newinds"].append(newinds.detach().clone())
-        trace["comb_weight"].append(float(wn.item()))
-        trace["e_trial"].append(e_trial.real)
+        if tr is not None:
+            tr["newinds"].append(newinds.detach().clone())
+            tr["comb_weight"].append(float(wn.item()))
+            tr["e_trial"].append(e_trial.real)
         all_x2 = _gather_walkers(x2, world)
         if writer is not None:
             writer.write(block, block=block, energy=e_est.real, positions=np.asarray(all_x2.cpu()))
-    return estimates, data, weights, trace
+    return estimates, data, weights, tr
 
 
 def main(atoms, charges, spins, tstep: float, nelectrons: int, nsteps: int, natoms: int, ndim: int,
@@ -182,17 +229,7 @@ def main(atoms, charges, spins, tstep: float, nelectrons: int, nsteps: int, nato
     ctx = network.apply._aiqmc_network.bind(params, data.atoms, dtype)
     rng = np.random.default_rng(seed + rank)
     out_dir = ckpt_restore_path or ckpt_save_path
-    last_ckpt = [time.time()]
-
-    def on_block(block, e_est, data):
-        if time.time() - last_ckpt[0] > save_frequency * 60:
-            all_pos = _gather_walkers(data.positions, world)
-            if rank == 0:
-                checkpoint.save(out_dir, block, nn.AINetData(positions=all_pos, spins=data.spins, atoms=data.atoms,
-                                                             charges=data.charges), params, opt_state)
-            if world > 1:
-                dist.barrier()
-            last_ckpt[0] = time.time()
+    on_block = make_checkpoint_hook(out_dir, params, opt_state, save_frequency)
 
     writer = writers.Writer(name='DMC_states', schema=['block', 'energy', 'positions'], directory=out_dir,
                             iteration_key=None, log=False) if rank == 0 else contextlib.nullcontext()

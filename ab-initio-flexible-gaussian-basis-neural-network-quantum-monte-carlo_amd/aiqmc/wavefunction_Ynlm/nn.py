@@ -99,12 +99,12 @@ def _leaf_key(leaves):
     tensor (its value must then be compared)."""
     if not all(isinstance(l, torch.Tensor) for l in leaves):
         return None
-    return [(l, l._version) for l in leaves]
+    return [(l, l._version, l.data_ptr()) for l in leaves]
 
 
 def _same_leaves(key, leaves) -> bool:
     return key is not None and len(key) == len(leaves) and all(
-        t is l and v == l._version for (t, v), l in zip(key, leaves))
+        t is l and v == l._version and p == l.data_ptr() for (t, v, p), l in zip(key, leaves))
 
 
 def _first(x):
@@ -195,22 +195,29 @@ class AINet:
             self._ctx[key] = ctx
         return ctx
 
-    def bind(self, params, atoms, dtype=torch.float32, device: Optional[int] = None) -> _lib.Context:
+    def bind(self, params, atoms, dtype=torch.float32, device: Optional[int] = None,
+             force: bool = False) -> _lib.Context:
         """Context with `params` uploaded (re-uploads only when the values changed).
 
-        The same tensor leaves at the same in-place versions as the last upload are taken as
-        unchanged without looking at their values (no device->host copy, no sync: the drop-in
-        drivers call apply / local_energy / mc_step several times per step with one params
-        tree); otherwise the leaves are gathered with one copy and compared by digest."""
+        The same tensor leaves at the same in-place versions and storage pointers as the last
+        upload are taken as unchanged without looking at their values (no device->host copy, no
+        sync: the drop-in drivers call apply / local_energy / mc_step several times per step with
+        one params tree); otherwise the leaves are gathered with one copy and compared by digest.
+
+        Contract: a parameter leaf changed in place must bump its autograd version (every torch
+        in-place op does: ``w.add_(..)``, ``w.copy_(..)``, ``w[...] = ..``).  Writes that bypass it
+        -- through ``w.data``, a NumPy or DLPack view, or a raw device pointer -- are NOT seen;
+        after such a write pass ``force=True`` (or a new tensor).  The repo's optimizers return
+        new tensors, so this concerns only outside writers."""
         ctx = self.context(atoms, dtype, device)
         leaves = tree_leaves(params)
         k = id(ctx)
         prev = self._loaded.get(k)
-        if prev is not None and _same_leaves(prev[0], leaves):
+        if not force and prev is not None and _same_leaves(prev[0], leaves):
             return ctx
         flat = _flatten_leaves(leaves)
         digest = hashlib.sha1(flat.tobytes()).hexdigest()
-        if prev is None or prev[1] != digest:
+        if force or prev is None or prev[1] != digest:
             ctx.set_params(flat)
         self._loaded[k] = (_leaf_key(leaves), digest)
         return ctx

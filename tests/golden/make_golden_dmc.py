@@ -11,6 +11,8 @@ ECP coefficients (what "Ne + DMC" maps to), B = 4, 1 block x 2 iterat
 C_dmc_attractive_2dev.npz: the "attractive" table with the 8 walkers split over 2 devices
 (oracle.dmc.dmc_blocks_devices: per-device T-moves / drift-diffusion / comb, global cut, estimate
 and feedback), 2 blocks x 2 iterations; u_comb [2, 2], extra [2, 2, 4, 12] per (block, device).
+Ne_dmc_ne_allelectron_2dev.npz: all-electron Ne (BASELINE config 5, the multi-GPU DMC one) the
+same way, 4 walkers over 2 devices, 2 blocks x 2 iterations.
 Arrays: params_flat, x0 [B,12], e_l0_re/_im [B] (pp energies of x0 with rot0), rot0;
 per step k (6): rot_tm, u_sel, u_acc, gauss1 [B,12], gauss2 [B,4,12], u [B,4], rot_old, rot_new;
 per block (2): u_comb, extra [B,12]; outputs: energy_re/_im [6,B], weights [6,B],
@@ -42,12 +44,13 @@ TABLES = {
 TSTEP, FEEDBACK = 0.05, 1.0
 
 
-def make_2dev(out_dir: str):
-    """The multi-device driver (main_dmc.py pmapped over 2 devices) on the attractive table."""
-    s = system.make_system("C_ecp")
+def make_2dev(out_dir: str, name: str = "attractive"):
+    """The multi-device driver (main_dmc.py pmapped over 2 devices) on one table."""
+    sysname = "Ne" if name == "ne_allelectron" else "C_ecp"
+    s = system.make_system(sysname)
     N = s.nelectrons
-    B, NDEV, NBLOCKS, ITERS = 8, 2, 2, 2
-    rng = np.random.default_rng(54)
+    B, NDEV, NBLOCKS, ITERS = (4 if sysname == "Ne" else 8), 2, 2, 2
+    rng = np.random.default_rng({"attractive": 54, "ne_allelectron": 55}[name])
     params = system.init_params(rng, s, randomize_aux=True)
     x0 = system.init_electrons(rng, s.atoms, s.charges, B, 1.0)
     rot0 = pp.haar_rotations(rng, B)
@@ -61,7 +64,7 @@ def make_2dev(out_dir: str):
     extra = rng.uniform(size=(NBLOCKS, NDEV, B // NDEV, 3 * N))
     net = network.Network(s)
     pt = network.to_torch(params)
-    ecp = TABLES["attractive"]
+    ecp = TABLES[name]
     e_l0 = pp.batch_local_energy_pp(net, pt, ecp, torch.tensor(x0), rot0)[0].detach().numpy()
     trace, x, w = dmc.dmc_blocks_devices(net, pt, ecp, x0, e_l0, NBLOCKS, ITERS, TSTEP, FEEDBACK,
                                          lambda k: steps[k],
@@ -75,8 +78,8 @@ def make_2dev(out_dir: str):
                tstep=np.float64(TSTEP), feedback=np.float64(FEEDBACK))
     for key in steps[0]:
         out[key] = np.stack([st[key] for st in steps])
-    np.savez_compressed(os.path.join(out_dir, "C_dmc_attractive_2dev.npz"), **out)
-    print("2dev e_est", trace["e_est"], "comb weights", trace["comb_weight"], "newinds", trace["newinds"])
+    np.savez_compressed(os.path.join(out_dir, f"{'Ne' if sysname == 'Ne' else 'C'}_dmc_{name}_2dev.npz"), **out)
+    print(name, "2dev e_est", trace["e_est"], "comb weights", trace["comb_weight"], "newinds", trace["newinds"])
 
 
 def make(out_dir: str, name: str):
@@ -120,8 +123,8 @@ def make(out_dir: str, name: str):
 
 
 if __name__ == "__main__":
-    for n in sys.argv[1:] or list(TABLES) + ["attractive_2dev"]:
-        if n == "attractive_2dev":
-            make_2dev(os.path.dirname(os.path.abspath(__file__)))
+    for n in sys.argv[1:] or list(TABLES) + ["attractive_2dev", "ne_allelectron_2dev"]:
+        if n.endswith("_2dev"):
+            make_2dev(os.path.dirname(os.path.abspath(__file__)), n[:-len("_2dev")])
         else:
             make(os.path.dirname(os.path.abspath(__file__)), n)

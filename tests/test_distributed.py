@@ -117,3 +117,70 @@ def test_clipping_and_gradient_pmean_match_global(world):
         assert abs(r[1] - e_all.mean()) < 1e-12 and abs(r[2] - center) < 1e-12
         np.testing.assert_allclose(r[3], diff[64 * r[0]:64 * (r[0] + 1)], rtol=1e-12, atol=1e-12)
         np.testing.assert_allclose(r[4], np.full(7, (world - 1) / 2.0))
+
+
+def _ckpt_worker(rank, world, port, out_dir, q):
+    """DMC checkpoint cadence on world ranks whose clocks disagree (each rank used
+    its own wall clock, so one rank could enter the gather + barrier while another skipped it)."""
+    import sys
+    from conftest import PKG
+    sys.path.insert(0, PKG)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from aiqmc.DMC import main_dmc
+    from aiqmc.wavefunction_Ynlm.nn import AINetData
+    # per-rank fake clocks in seconds (save_frequency 1 min): rank 0 is first due at block 1,
+    # rank 1 already at block 0
+    clock_vals = [0, 0, 100, 100, 200, 200, 300, 300, 400, 400] if rank == 0 else \
+        [0, 100, 100, 200, 200, 300, 300, 400, 400, 500]
+    calls = [0]
+
+    def clock():
+        v = clock_vals[min(calls[0], len(clock_vals) - 1)]
+        calls[0] += 1
+        return float(v)
+
+    hook = main_dmc.make_checkpoint_hook(out_dir, {"w": np.ones(2)}, {"count": np.int64(0)},
+                                         save_frequency=1.0, clock=clock)
+    after = []
+    for block in range(4):
+        pos = torch.full((3, 6), float(10 * rank + block), dtype=torch.float64)
+        data = AINetData(positions=pos, spins=np.ones(2), atoms=np.zeros((1, 3)), charges=np.ones(1))
+        hook(block, complex(-1.0), data)
+        # the next collective of the driver: must pair with the same call on every rank
+        x = torch.tensor([float(block)])
+        dist.all_reduce(x)
+        after.append(float(x))
+    q.put((rank, [os.path.basename(f) for f in hook.saved], after))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dmc_checkpoint_cadence_is_collective(tmp_path):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ckpt_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # rank 0's clock decides (due at blocks 1, 2, 3; rank 1's clock alone would say 0, 1, 2, 3)
+    saved0 = res[0][1]
+    assert saved0 == [f"qmcjax_ckpt_{b:06d}.npz" for b in (1, 2, 3)] and res[1][1] == []
+    for r in res:
+        assert r[2] == [float(world * b) for b in range(4)]          # collectives stayed paired
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+    from aiqmc import checkpoint
+    for f in saved0:
+        t, data, _, _ = checkpoint.restore(str(tmp_path / f))
+        block = t - 1
+        pos = np.asarray(data.positions)
+        assert pos.shape == (6, 6)                                   # both ranks' walkers, rank-major
+        np.testing.assert_array_equal(pos[:3], block)
+        np.testing.assert_array_equal(pos[3:], 10 + block)

@@ -94,6 +94,17 @@ def test_comput_S_dropin_matches_oracle():
     v2 = rng.standard_normal((40, 12)) ** 2
     got = comput_S(-5.1, -5.0, 0.7, torch.tensor(v2), 0.02, torch.tensor(eloc), 4).numpy()
     np.testing.assert_allclose(got, odmc.comput_S(-5.1, -5.0, 0.7, v2, 0.02, eloc, 4), rtol=1e-14)
+    # first DMC block (main_dmc.py:115-124): per-walker e_trial = e_est = total_e energies (complex,
+    # as total_e returns them) and a per-walker branch cut 10 * esigma
+    e0 = eloc + rng.normal(0, 0.3, 40) + 1j * rng.normal(0, 0.1, 40)
+    bc = np.full(40, 10.0) * 0.05
+    got = comput_S(torch.tensor(e0), torch.tensor(e0), torch.tensor(bc), torch.tensor(v2), 0.02,
+                   torch.tensor(eloc + 0j), 4).numpy()
+    want = odmc.comput_S(e0, e0, bc, v2, 0.02, eloc, 4)
+    assert want.shape == (40,)
+    np.testing.assert_allclose(got, want, rtol=1e-14)
+    got = comput_S(e0, e0, bc, torch.tensor(v2), 0.02, torch.tensor(eloc), 4).numpy()   # numpy arrays
+    np.testing.assert_allclose(got, want, rtol=1e-14)
 
 
 @pytest.mark.gpu
@@ -453,7 +464,7 @@ def test_dmc_trajectory_matches_oracle(golden_dir, name):
                                           T(g["rot_old"][k]), T(g["rot_new"][k]))
     block_draws = lambda b: (float(g["u_comb"][b]), T(g["extra"][b]))
     est, data, w, trace = main_dmc.dmc_blocks(run, ctx, params, data, e_l0, var0, nblocks, iters, float(g["feedback"]),
-                                              step_key, block_draws)
+                                              step_key, block_draws, trace=True)
     torch.cuda.synchronize()
     for k in range(nblocks * iters):
         np.testing.assert_allclose(trace["positions"][k].cpu().numpy(), g["positions"][k], rtol=1e-9, atol=1e-9)

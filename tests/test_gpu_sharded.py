@@ -144,13 +144,18 @@ def _dmc_rank(rank, world, fixture):
     from aiqmc.VMC.VMCmcstep import HostDraws
     from aiqmc.wavefunction_Ynlm import nn
     g = dict(np.load(fixture))
-    s = systems.make_system("C_ecp")
+    sysname = "Ne" if os.path.basename(fixture).startswith("Ne_") else "C_ecp"
+    s = systems.make_system(sysname)
     N, A = s.nelectrons, s.natoms
     network = s.make_network()
-    params = system.unflatten_params(system.init_params(np.random.default_rng(0), system.make_system("C_ecp")),
+    params = system.unflatten_params(system.init_params(np.random.default_rng(0), system.make_system(sysname)),
                                      g["params_flat"])
     from oracle import pphamiltonian as opp
-    e = opp.ECP([[1.0]], [[0.0]], [[1.0]], [[[2.0], [1.0]]], [[[-3.0], [-5.0]]], [[[0.7], [0.4]]], 1)
+    if sysname == "Ne":      # all-electron Ne through the pp-only DMC step (make_golden_dmc.TABLES)
+        e = opp.ECP([[1.0]], [[0.0]], [[1.0]], [[[2.0], [2.0], [2.0]]], [[[0.0], [0.0], [0.0]]],
+                    [[[1.0], [1.0], [1.0]]], 2)
+    else:
+        e = opp.ECP([[1.0]], [[0.0]], [[1.0]], [[[2.0], [1.0]]], [[[-3.0], [-5.0]]], [[[0.7], [0.4]]], 1)
     B = g["x0"].shape[0]
     Bd = B // world
     sl = slice(rank * Bd, (rank + 1) * Bd)
@@ -172,7 +177,7 @@ def _dmc_rank(rank, world, fixture):
         torch.tensor(g["rot_old"][k][sl]), torch.tensor(g["rot_new"][k][sl]))
     block_draws = lambda b: (float(g["u_comb"][b, rank]), torch.tensor(g["extra"][b, rank]))
     est, data, w, trace = main_dmc.dmc_blocks(run, ctx, params, data, e_l0, var0, nblocks, iters, float(g["feedback"]),
-                                              step_key, block_draws)
+                                              step_key, block_draws, trace=True)
     torch.cuda.synchronize()
     return dict(positions=np.stack([p.cpu().numpy() for p in trace["positions"]]),
                 energy=np.stack([x.real.cpu().numpy() for x in trace["energy"]]),
@@ -182,14 +187,16 @@ def _dmc_rank(rank, world, fixture):
                 x_final=data.positions.cpu().numpy())
 
 
-def test_two_rank_dmc_driver_matches_two_device_oracle(tmp_path, golden_dir):
+@pytest.mark.parametrize("fixture_name", ["C_dmc_attractive_2dev.npz", "Ne_dmc_ne_allelectron_2dev.npz"])
+def test_two_rank_dmc_driver_matches_two_device_oracle(tmp_path, golden_dir, fixture_name):
     """main_dmc.dmc_blocks on two ranks (gloo, one GPU), 4 walkers each, every draw injected, vs
     the oracle's two-device driver (oracle.dmc.dmc_blocks_devices, C_dmc_attractive_2dev.npz):
     per-rank T-moves / drift-diffusion / comb, the comput_S cut as ONE minimum over both ranks
     (MIN all-reduce), the global block estimate and the e_trial feedback from the mean of the two
-    ranks' comb weights.  Positions 1e-9, weights 1e-12 relative, comb indices exact."""
+    ranks' comb weights.  Positions 1e-9, weights 1e-12 relative, comb indices exact.  Also
+    all-electron Ne (BASELINE config 5, Ne_dmc_ne_allelectron_2dev.npz), 2 walkers per rank."""
     world = 2
-    fixture = os.path.join(golden_dir, "C_dmc_attractive_2dev.npz")
+    fixture = os.path.join(golden_dir, fixture_name)
     port = _free_port()
     procs = []
     for r in range(world):
