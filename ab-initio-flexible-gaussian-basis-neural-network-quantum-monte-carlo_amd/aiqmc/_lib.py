@@ -79,6 +79,21 @@ class AiqmcEcp(ctypes.Structure):
 _lib: Optional[ctypes.CDLL] = None
 
 
+def library_sha16(path: Optional[str] = None) -> Optional[str]:
+    """First 16 hex digits of the SHA-256 of the shared library file (default: the one this
+    module loads).  PMC summaries under profiles/ carry it, and bench.py reports their counters
+    only when it matches the library it is running (stale counters are set to null)."""
+    import hashlib
+    f = path or LIB_PATH
+    if not os.path.exists(f):
+        return None
+    h = hashlib.sha256()
+    with open(f, "rb") as fh:
+        for chunk in iter(lambda: fh.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()[:16]
+
+
 def load() -> ctypes.CDLL:
     """Load the HIP library (raises if it has not been built)."""
     global _lib

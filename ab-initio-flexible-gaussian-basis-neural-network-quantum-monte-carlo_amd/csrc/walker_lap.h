@@ -201,6 +201,85 @@ __device__ __forceinline__ void lap_layer(cptr<T> P, const T* xs, T* hb, const T
   }
 }
 
+// E4's determinant term ss = Re sum_{r,s} S_rs S_sr, S_rs = sum_f U_rf Q_f[r,s], on the matrix
+// cores.  ss = u^T K u with u = U[(r,f)] (this direction's column of dh/dx of electron
+// rowsrc[r], hb) and
+//   K[(r,f),(s,g)] = Re(Q_f[r,s] Q_g[s,r])          (4N x 4N, symmetric, the same for every direction),
+// so V = K U for all 3N directions at once is one (4N x 4N) x (4N x 48) product:
+// v_mfma_{f32,f64}_16x16x4 with K-step s = electron s (k = unit g = lane >> 4), M-tiles over
+// rows (r, f), N-tile c = coordinate (column e = lane & 15 of tile c is direction lane 16c + e,
+// the hb column).  The A fragment (one K entry per lane) is formed from two LDS reads of Q_f;
+// the B fragment is read from hb as it stands.  Then ss = sum_i U[i] V[i] per direction: a
+// lane-local sum over the accumulator rows and a sum over the four lane groups.  Multi-wave
+// mode: wave wv takes the K-steps s = wv, wv + W, ... (ss is linear in V).  Replaces ~1,650
+// VALU FMAs and ~1,100 broadcast LDS reads per wave (the double loop over r < s) by 12 N MFMAs.
+// Opt-in (-DAQ_LAP_MFMA_SS): measured SLOWER on N2 / 4096 walkers (local-energy pair 240.8 /
+// 241.2 us against 234.0 / 234.6 us with the VALU loop, two interleaved runs, same box;
+// profiles/r03_s1_lap_mfma_ab.txt).  The quadratic form does 4x the FLOPs of the S_rs S_sr
+// loop (K is 4N x 4N dense, S is rank-structured), and f32 MFMA runs at the f32 VALU rate on
+// gfx950, so the matrix cores only pay where they overlap VALU work of the other wave.
+template <typename T> struct MfmaTile;
+template <> struct MfmaTile<float> {
+  typedef float v4 __attribute__((ext_vector_type(4)));
+  static __device__ __forceinline__ v4 mma(float a, float b, v4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  // accumulator register v of lane group q holds row 4q + v (column = lane & 15)
+  static constexpr __device__ int row(int q, int v) { return 4 * q + v; }
+};
+template <> struct MfmaTile<double> {
+  typedef double v4 __attribute__((ext_vector_type(4)));
+  static __device__ __forceinline__ v4 mma(double a, double b, v4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+  }
+  static constexpr __device__ int row(int q, int v) { return q + 4 * v; }   // f64 C/D map
+};
+
+template <typename T, int N>
+__device__ __forceinline__ T ss_mfma(const T* Qs, const T* hb, const int* rowsrc, int lane, int wv, int W) {
+  static_assert(NH == 4, "K-step = one electron's 4 units");
+  using MT = MfmaTile<T>;
+  using V4 = typename MT::v4;
+  constexpr int NM = (4 * N + 15) / 16;   // M-tiles over the rows (r, f)
+  const int q = lane >> 4, e = lane & 15;
+  T out = T(0);
+  // one N-tile (coordinate c) at a time: 4 NM accumulator registers live instead of 12 NM
+#pragma unroll 1
+  for (int c = 0; c < 3; ++c) {
+    V4 acc[NM];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) acc[m] = V4{T(0), T(0), T(0), T(0)};
+#pragma unroll 2
+    for (int s = wv; s < N; s += W) {
+      const T bop = hb[(rowsrc[s] * NH + q) * 49 + 16 * c + e];
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        const int i = 16 * m + e;            // A row (r, f); A column k = unit q of electron s
+        const int r = i >> 2, f = i & 3;
+        const int rc = r < N ? r : N - 1;
+        const T* a = Qs + ((rc * N + s) * NH + f) * 2;
+        const T* b = Qs + ((s * N + rc) * NH + q) * 2;
+        T kv = a[0] * b[0] - a[1] * b[1];
+        if (4 * N % 16 != 0 && m == NM - 1) kv = r < N ? kv : T(0);
+        acc[m] = MT::mma(kv, bop, acc[m]);
+      }
+    }
+    T p = T(0);
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int i = 16 * m + MT::row(q, v);
+        const int r = i >> 2, f = i & 3;
+        if (16 * (m + 1) <= 4 * N || r < N) p += hb[(rowsrc[r < N ? r : N - 1] * NH + f) * 49 + 16 * c + e] * acc[m][v];
+      }
+    p += __shfl_xor(p, 16);
+    p += __shfl_xor(p, 32);
+    out = (q == c) ? p : out;
+  }
+  return out;
+}
+
 // One workgroup of W = blockDim.x / 64 waves per walker (W = 1, 2 or 4; aiqmc.hip picks W so
 // that small batches still fill the chip): every wave evaluates the per-electron stage of all
 // electrons (its lanes are the 3N directions), the h-stream columns i = wv, wv + W, ... of each
@@ -357,15 +436,20 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
       zr += br * wr[col] - bi * wi[col];
       zi += br * wi[col] + bi * wr[col];
     }
-    T sr = T(0), si = T(0), dr = T(0), di = T(0);
+    T sr = T(0), si = T(0);
 #pragma unroll
     for (int f = 0; f < NH; ++f) {
       sr += ur[f] * Qs[((r * N + le) * NH + f) * 2];
       si += ur[f] * Qs[((r * N + le) * NH + f) * 2 + 1];
+    }
+    cross += zr * sr - zi * si;
+#ifndef AQ_LAP_MFMA_SS
+    T dr = T(0), di = T(0);
+#pragma unroll
+    for (int f = 0; f < NH; ++f) {
       dr += ur[f] * Qs[((r * N + r) * NH + f) * 2];
       di += ur[f] * Qs[((r * N + r) * NH + f) * 2 + 1];
     }
-    cross += zr * sr - zi * si;
     ss += dr * dr - di * di;
 #pragma unroll 1
     for (int s = r + 1; s < N; ++s) {
@@ -380,7 +464,12 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
       }
       ss += T(2) * (ar * br - ai * bi);
     }
+#endif
   }
+#ifdef AQ_LAP_MFMA_SS
+  __builtin_amdgcn_sched_barrier(0);
+  ss = ss_mfma<T, N>(Qs, hb, rowsrc, lane, wv, W);
+#endif
 #undef UH
   T lap = (w0 ? t2 : T(0)) - (ss + T(2) * cross + (w0 ? wbr * wbr - wbi * wbi : T(0))) + jd2 + acc;
   if (W > 1) {

@@ -800,7 +800,13 @@ k_walker_rev(KArgs ka) {
 #ifdef AQ_PHASE_PROF
       if (lane == 0) atomicAdd(&aq_phase_cycles[15], 1ull);   // fallback count (diagnostics build)
 #endif
+#ifdef AQ_PHASE_MARK
+      AQ_PH(10);   // tools/isa_phases.py: the rarely taken pivoted fallback, counted apart
+#endif
       gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi);
+#ifdef AQ_PHASE_MARK
+      AQ_PH(11);
+#endif
     }
   } else {
     gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi, (!PREP && !isprop) ? Wc + WC::pv : nullptr);

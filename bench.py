@@ -6,8 +6,12 @@ loop (main_all_electrons_adam_muti_GPU.py:177-197 / VMC/VMCmain.py:83-91):
   mc_step with nsteps drift-diffusion Metropolis sweeps (VMCmcstep.py:121-140),
   local energy of every walker (hamiltonian.local_energy, complex_output=False),
   energy statistics pmean (loss.py:206-208) as ONE all-reduce over RCCL.
-Walkers are sharded: each rank owns --walkers walkers (weak scaling); only the
-statistics cross ranks.
+Walkers are sharded in contiguous blocks; only the statistics cross ranks.  With N > 1 ranks
+the headline is SURVEY 8(d)'s strong-scaling curve: 4096 walkers IN TOTAL (512 per GPU at
+N = 8); a weak-scaling run at 4096 walkers per GPU is reported beside it (``weak_scaling``).
+``--weak`` makes the weak run the headline.  With N = 1 both are the same 4096-walker run, and
+``strong_scaling_per_rank`` times the per-rank workloads of N = 2, 4, 8 (2048/1024/512
+walkers) on the one GPU.
 
 Usage: python bench.py [--gpus N --steps K --warmup W]; for N>1 launch with
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
@@ -46,15 +50,19 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--walkers", type=int, default=4096, help="walkers per GPU (weak scaling, the default)")
-    ap.add_argument("--global-walkers", type=int, default=0,
+    ap.add_argument("--walkers", type=int, default=4096, help="walkers per GPU of a weak-scaling run")
+    ap.add_argument("--global-walkers", type=int, default=4096,
                     help="strong scaling: this many walkers in total, split over the ranks (SURVEY 8(d): 4096)")
+    ap.add_argument("--weak", action="store_true",
+                    help="headline = weak scaling (--walkers per GPU) instead of SURVEY 8(d)'s 4096 in total")
+    ap.add_argument("--no-per-rank", action="store_true",
+                    help="N=1: skip timing the 2048/1024/512-walker per-rank workloads of N=2/4/8")
     ap.add_argument("--nsteps", type=int, default=10, help="Metropolis sweeps per iteration")
     ap.add_argument("--tstep", type=float, default=0.05)
     ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
     ap.add_argument("--system", default="N2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-walkers", type=int, default=64)
+    ap.add_argument("--cpu-sample-walkers", type=int, default=256, help="SURVEY 8(d): 256 walkers")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     ap.add_argument("--no-ecp", action="store_true", help="skip the C-atom ccECP local-energy side measurement")
     ap.add_argument("--no-adam", action="store_true", help="skip the Be-atom Adam training-step side measurement")
@@ -72,11 +80,42 @@ def build(name, dtype, device):
     return s.atoms, s.charges, s.spins, network, params, ctx
 
 
+def host_cpu_info():
+    """The host this runs on: machine CPUs, the CPUs this process may use (affinity and cgroup
+    quota), and the CPU model from /proc/cpuinfo."""
+    machine = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = machine
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = min(affinity, quota) if quota else affinity
+    return {"machine_cpus": machine, "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "usable_cpus": usable, "model": model}
+
+
 def cpu_baseline(name, params, atoms, charges, nsteps_unused, tstep, sample_walkers):
-    """Time the float64 oracle (reference algorithms) on host cores on a bounded sample."""
+    """Time the float64 oracle (reference algorithms) on host cores on a bounded sample, with
+    every CPU this process may use (affinity / cgroup quota: os.cpu_count() on the GPU box is
+    the whole machine, of which a one-GPU job gets a share)."""
     sys.path.insert(0, ROOT)
     from oracle import hamiltonian, mcstep, network, system
-    threads = min(16, os.cpu_count() or 1)
+    host = host_cpu_info()
+    threads = host["usable_cpus"]
     torch.set_num_threads(threads)
     s = system.make_system(name)
     net = network.Network(s)
@@ -88,15 +127,15 @@ def cpu_baseline(name, params, atoms, charges, nsteps_unused, tstep, sample_walk
     g1 = torch.tensor(rng.standard_normal((B, 3 * N)))
     g2 = torch.tensor(rng.standard_normal((B, N, 3 * N)))
     u = torch.tensor(rng.uniform(size=(B, N)))
-    # time-bounded sample (~10 s per leg): repeat until the leg has run for at least `target` s
-    target = 8.0
+    # time-bounded sample (~10 s per leg): whole sweeps of B walkers until the leg has run >= target s
+    target = 10.0
     t_mc, n_mc = 0.0, 0
     while t_mc < target:
         t0 = time.perf_counter()
         mcstep.walkers_update(net, pt, x, g1, g2, u, tstep)
         t_mc += time.perf_counter() - t0
         n_mc += B
-    be = 4
+    be = 8
     t_el, n_el = 0.0, 0
     while t_el < target:
         t0 = time.perf_counter()
@@ -105,10 +144,11 @@ def cpu_baseline(name, params, atoms, charges, nsteps_unused, tstep, sample_walk
         n_el += be
     return {
         "value": n_mc / t_mc, "unit": "walker*steps/s", "cores": threads, "kind": "port",
-        "local_energy_evals_per_s": n_el / t_el,
+        "local_energy_evals_per_s": n_el / t_el, "host": host, "torch_threads": torch.get_num_threads(),
         "sample": f"float64 oracle (torch CPU, jvp-of-grad Laplacian, per-electron-config MH) on {name}: "
                   f"{n_mc // B} Metropolis sweeps of {B} walkers ({t_mc:.1f}s) + local energy of {n_el} "
-                  f"walkers in batches of {be} ({t_el:.1f}s)",
+                  f"walkers in batches of {be} ({t_el:.1f}s); {threads} threads = the CPUs usable by this "
+                  f"process ({host['machine_cpus']} on the machine, model {host['model']})",
     }
 
 
@@ -317,6 +357,24 @@ def adam_side_bench(dtype, device, walkers, steps):
             "walker_steps_per_s": walkers * 10 / dt, "energy": float(loss_v), "finite": bool(math.isfinite(float(loss_v)))}
 
 
+def load_pmc(lib_sha):
+    """PMC-derived per-launch figures of the proposal kernel (rocprofv3 --pmc passes, one counter
+    group per run, corrected per MI355X_MICROARCH.md; tools/gpu_pmc3.sh -> profiles/pmc_r03.json).
+    They are used only if the file was taken on THIS library build (``lib_sha16`` equal to the
+    loaded .so's hash); otherwise every counter-derived field is null and the reason is given."""
+    f = os.path.join(ROOT, "profiles", "pmc_r03.json")
+    if not os.path.exists(f):
+        return {}, "no PMC summary committed (profiles/pmc_r03.json)"
+    try:
+        pmc = json.load(open(f))
+    except Exception as e:
+        return {}, f"unreadable PMC summary: {e!r}"
+    if pmc.get("lib_sha16") != lib_sha:
+        return {}, (f"PMC summary taken on library {pmc.get('lib_sha16')}, this run loads {lib_sha}: "
+                    "counters not reported for a different build")
+    return pmc, None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -336,93 +394,150 @@ def main():
 
     atoms, charges, spins, network, params, ctx = build(args.system, dtype, local_dev)
     N = int(charges.sum())
-    strong = args.global_walkers > 0
-    if strong and args.global_walkers % world:
+    if args.global_walkers % world:
         raise SystemExit("--global-walkers must be divisible by the number of ranks")
-    B = args.global_walkers // world if strong else args.walkers
-    if strong:   # contiguous blocks of one global batch (main_all_electrons_adam_muti_GPU.py:86-97)
-        pos0, _ = init_electrons(1000, None, atoms, charges, spins, args.global_walkers, 1.0)
-        pos0 = pos0[rank * B:(rank + 1) * B]
-    else:
-        pos0, _ = init_electrons(1000 + rank, None, atoms, charges, spins, B, 1.0)
-    pos = pos0.to(dev, dtype).contiguous()
-    el = torch.empty(B, dtype=dtype, device=dev)
-    seed = 12345 + rank
-    offset = 0
 
-    def iteration(record=None):
-        nonlocal offset
-        if record is not None:
-            record[0].record()
-        ctx.mc_step(pos, args.nsteps, args.tstep, seed=seed, offset=offset)
-        offset += args.nsteps
-        if record is not None:
-            record[1].record()
-        ctx.local_energy(pos, out=el)
-        if record is not None:
-            record[2].record()
-        return constants.pmean_stats(el)
+    def walkers_of(strong):
+        if strong:   # contiguous blocks of one global batch (main_all_electrons_adam_muti_GPU.py:86-97)
+            B = args.global_walkers // world
+            pos0, _ = init_electrons(1000, None, atoms, charges, spins, args.global_walkers, 1.0)
+            return B, pos0[rank * B:(rank + 1) * B]
+        pos0, _ = init_electrons(1000 + rank, None, atoms, charges, spins, args.walkers, 1.0)
+        return args.walkers, pos0
 
-    for _ in range(args.warmup):
-        iteration()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ctx.profile(True)
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    stats = None
-    for k in range(args.steps):
-        stats = iteration(evs[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_local = time.perf_counter() - t0
-    ctx.profile(False)
-    mc_ms = sum(e[0].elapsed_time(e[1]) for e in evs)
-    el_ms = sum(e[1].elapsed_time(e[2]) for e in evs)
-    prop_ms, prop_n = ctx.profile_read(_lib.PROF_MC_PROPOSAL)
-    walk_ms, walk_n = ctx.profile_read(_lib.PROF_MC_WALKER)
-    lap_ms, lap_n = ctx.profile_read(_lib.PROF_LOCAL_ENERGY)
-    tt = torch.tensor([t_local, mc_ms, el_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    t_job, mc_ms_max, el_ms_max = tt.tolist()
-    mean_e, var_e = (float(stats[0]), float(stats[1]))
-    finite = bool(torch.isfinite(pos).all().item()) and math.isfinite(mean_e)
+    def measure(B, pos0, steps, warmup, tag):
+        """warmup + `steps` timed VMC iterations on this rank's B walkers; the job time is the max
+        over ranks (barrier + synchronize on both sides of the timed region)."""
+        pos = pos0.to(dev, dtype).contiguous()
+        el = torch.empty(B, dtype=dtype, device=dev)
+        seed = 12345 + rank + 7919 * tag
+        offset = [0]
+
+        def iteration(record=None):
+            if record is not None:
+                record[0].record()
+            ctx.mc_step(pos, args.nsteps, args.tstep, seed=seed, offset=offset[0])
+            offset[0] += args.nsteps
+            if record is not None:
+                record[1].record()
+            ctx.local_energy(pos, out=el)
+            if record is not None:
+                record[2].record()
+            return constants.pmean_stats(el)
+
+        for _ in range(warmup):
+            iteration()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ctx.profile(True)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+        t0 = time.perf_counter()
+        stats = None
+        for k in range(steps):
+            stats = iteration(evs[k])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_local = time.perf_counter() - t0
+        ctx.profile(False)
+        mc_ms = sum(e[0].elapsed_time(e[1]) for e in evs)
+        el_ms = sum(e[1].elapsed_time(e[2]) for e in evs)
+        prop_ms, prop_n = ctx.profile_read(_lib.PROF_MC_PROPOSAL)
+        walk_ms, walk_n = ctx.profile_read(_lib.PROF_MC_WALKER)
+        lap_ms, lap_n = ctx.profile_read(_lib.PROF_LOCAL_ENERGY)
+        tt = torch.tensor([t_local, mc_ms, el_ms], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_job, mc_ms_max, el_ms_max = tt.tolist()
+        mean_e, var_e = (float(stats[0]), float(stats[1]))
+        finite = bool(torch.isfinite(pos).all().item()) and math.isfinite(mean_e)
+        total = world * B
+        return {"B": B, "total_walkers": total, "t_job": t_job, "steps": steps,
+                "value": total * args.nsteps * steps / t_job, "ms_per_step": 1e3 * t_job / steps,
+                "local_energy_evals_per_s": total * steps / (el_ms_max * 1e-3),
+                "mc_walker_steps_per_s": total * args.nsteps * steps / (mc_ms_max * 1e-3),
+                "prop_avg_ms": prop_ms / max(prop_n, 1), "prop_n": prop_n,
+                "walk_avg_ms": walk_ms / max(walk_n, 1), "lap_avg_ms": lap_ms / max(lap_n, 1), "lap_n": lap_n,
+                "mean_e": mean_e, "var_e": var_e, "finite": finite}
+
+    peak = PEAK_FP32_TFLOPS if dtype == torch.float32 else PEAK_FP64_TFLOPS
+    lib_sha = _lib.library_sha16()
+    pmc, pmc_reason = load_pmc(lib_sha)
+
+    def rooflines(m):
+        B = m["B"]
+        flop_prop = B * N * F_VG_N2 if args.system == "N2" else None
+        achieved = (flop_prop / (m["prop_avg_ms"] * 1e-3) / 1e12) if flop_prop else None
+        achieved_el = (B * F_EL_N2 / (m["lap_avg_ms"] * 1e-3) / 1e12) if args.system == "N2" else None
+        # counters were taken at 4096 walkers per GPU; per-launch bytes scale with the launch size
+        use_pmc = pmc and B == pmc.get("walkers", 4096)
+        traffic = pmc.get("proposal_hbm_bytes_per_launch") if use_pmc else None
+        el_traffic = pmc.get("local_energy_hbm_bytes_per_pair") if use_pmc else None
+        why = pmc_reason if not pmc else (None if use_pmc else f"PMC passes were taken at {pmc.get('walkers', 4096)} "
+                                                                  f"walkers per GPU, this run has {B}")
+        prop = {
+            "kernel": "k_walker_rev<float,14,2,PROP> proposal launch (B*N value+gradient configs)",
+            # the bound is the fp32 vector ALU (157.3 TF = 64 FLOP/clk/SIMD, MI355X_MICROARCH.md): no
+            # MFMA on this path (SQ_INSTS_MFMA = 0 in the committed PMC pass), HBM at a few % of 8 TB/s
+            "bound": "valu", "compute_unit": "VALU fp32 (no MFMA on this path)",
+            "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+            "frac": (achieved / peak) if achieved else None, "traffic": traffic,
+            "hbm_gbs": (traffic / (m["prop_avg_ms"] * 1e-3) / 1e9) if traffic else None,
+            "hbm_frac": (traffic / (m["prop_avg_ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS) if traffic else None,
+            "mfma_util": pmc.get("proposal_mfma_util") if use_pmc else None,
+            "valu_insts_per_wave": pmc.get("proposal_valu_insts_per_wave") if use_pmc else None,
+            "nonfp_valu_insts_per_wave": pmc.get("proposal_nonfp_valu_insts_per_wave") if use_pmc else None,
+            "pmc_lib_sha16": pmc.get("lib_sha16") if pmc else None, "lib_sha16": lib_sha,
+            "pmc_null_reason": why,
+            "avg_launch_ms": m["prop_avg_ms"], "launches": m["prop_n"],
+            "flop_per_launch": flop_prop,
+            "flop_model": "B*N*3*F_fwd, F_fwd=4.9e4 (SURVEY 8d)"}
+        lap = {
+            "kernel": "k_walker_rev<float,14,2,PREP> + k_walker_lap<float,14,2> (local energy, 2 launches)",
+            "bound": "valu", "achieved": achieved_el, "peak": peak, "unit": "TFLOP/s",
+            "frac": (achieved_el / peak) if achieved_el else None, "avg_launch_ms": m["lap_avg_ms"],
+            "traffic": el_traffic,
+            "mfma_util": pmc.get("local_energy_mfma_util") if use_pmc else None,
+            "launches": m["lap_n"], "flop_model": "B*2.55e6 (SURVEY 8d)"}
+        return prop, lap
+
+    strong = not args.weak
+    B, pos0 = walkers_of(strong)
+    head = measure(B, pos0, args.steps, args.warmup, 0)
+    weak = None
+    if world > 1 and strong:
+        Bw, posw = walkers_of(False)
+        weak = measure(Bw, posw, args.steps, args.warmup, 1)
+    per_rank = {}
+    if world == 1 and not args.no_per_rank and args.system == "N2":
+        for n in (2, 4, 8):
+            Bn = args.global_walkers // n
+            pn, _ = init_electrons(1000, None, atoms, charges, spins, args.global_walkers, 1.0)
+            m = measure(Bn, pn[:Bn], max(args.steps, 5), max(args.warmup, 2), 10 + n)
+            pr, lr = rooflines(m)
+            per_rank[f"N={n}"] = {
+                "walkers": Bn, "ms_per_step": m["ms_per_step"],
+                "walker_steps_per_s_one_rank": m["value"],
+                "projected_job_walker_steps_per_s": n * m["value"],
+                "mc_walker_steps_per_s_one_rank": m["mc_walker_steps_per_s"],
+                "local_energy_evals_per_s_one_rank": m["local_energy_evals_per_s"],
+                "proposal_avg_ms": m["prop_avg_ms"], "walker_launch_avg_ms": m["walk_avg_ms"],
+                "local_energy_pair_avg_ms": m["lap_avg_ms"],
+                "roofline_frac": pr["frac"], "roofline_local_energy_frac": lr["frac"]}
 
     if rank == 0:
-        total_walkers = world * B
-        value = total_walkers * args.nsteps * args.steps / t_job
-        peak = PEAK_FP32_TFLOPS if dtype == torch.float32 else PEAK_FP64_TFLOPS
-        prop_avg_ms = prop_ms / max(prop_n, 1)
-        flop_prop = B * N * F_VG_N2 if args.system == "N2" else None
-        achieved = (flop_prop / (prop_avg_ms * 1e-3) / 1e12) if flop_prop else None
-        lap_avg_ms = lap_ms / max(lap_n, 1)
-        achieved_el = (B * F_EL_N2 / (lap_avg_ms * 1e-3) / 1e12) if args.system == "N2" else None
-        # PMC-derived per-launch figures of the proposal kernel, collected by profiles/pmc_passes.sh
-        # in separate rocprofv3 --pmc passes over this bench (corrected per MI355X_MICROARCH.md) and
-        # committed under profiles/; null when no pass has been committed for this build
-        pmc = {}
-        for fn in ("pmc_r02.json", "pmc_traffic.json"):
-            f = os.path.join(ROOT, "profiles", fn)
-            if os.path.exists(f):
-                try:
-                    pmc = json.load(open(f))
-                    break
-                except Exception:
-                    pmc = {}
-        traffic = pmc.get("proposal_hbm_bytes_per_launch", pmc.get("k_walker_grad_proposal_bytes_per_launch"))
+        prop, lap = rooflines(head)
         out = {
             "metric": METRIC,
-            "value": value,
+            "value": head["value"],
             "unit": "walker*steps/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": 1e3 * t_job / args.steps,
+            "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
@@ -430,31 +545,25 @@ def main():
             "data": "synthetic (init_electrons walkers, random-init network of the reference architecture)",
             "config": {"workload": f"{args.system} VMC iteration: {args.nsteps} Metropolis sweeps + local energy "
                                    f"+ energy-stat all-reduce", "system": args.system, "electrons": N,
-                       "walkers_per_gpu": B, "global_walkers": total_walkers, "nsteps": args.nsteps,
+                       "walkers_per_gpu": head["B"], "global_walkers": head["total_walkers"], "nsteps": args.nsteps,
                        "tstep": args.tstep, "parallelism": f"walker-sharded dp{world}"},
-            "local_energy_evals_per_s": total_walkers * args.steps / (el_ms_max * 1e-3),
-            "mc_walker_steps_per_s": total_walkers * args.nsteps * args.steps / (mc_ms_max * 1e-3),
-            "roofline": {
-                "kernel": "k_walker_rev<float,14,2,PROP> proposal launch (B*N value+gradient configs)",
-                # no MFMA on this path (SQ_INSTS_MFMA = 0 per the committed PMC pass): the bound is the
-                # fp32 vector ALU (157.3 TF = 64 FLOP/clk/SIMD, MI355X_MICROARCH.md), not HBM
-                "bound": "valu", "compute_unit": "VALU fp32 (no MFMA on this path)",
-                "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                "frac": (achieved / peak) if achieved else None, "traffic": traffic,
-                "hbm_gbs": (traffic / (prop_avg_ms * 1e-3) / 1e9) if traffic else None,
-                "hbm_frac": (traffic / (prop_avg_ms * 1e-3) / 1e9 / PEAK_HBM_GBS) if traffic else None,
-                "mfma_util": pmc.get("proposal_mfma_util"),
-                "valu_insts_per_wave": pmc.get("proposal_valu_insts_per_wave"),
-                "avg_launch_ms": prop_avg_ms, "launches": prop_n,
-                "flop_per_launch": flop_prop,
-                "flop_model": "B*N*3*F_fwd, F_fwd=4.9e4 (SURVEY 8d)"},
-            "roofline_local_energy": {
-                "kernel": "k_walker_rev<float,14,2,PREP> + k_walker_lap<float,14,2> (local energy, 2 launches)", "achieved": achieved_el, "peak": peak, "unit": "TFLOP/s",
-                "frac": (achieved_el / peak) if achieved_el else None, "avg_launch_ms": lap_avg_ms,
-                "launches": lap_n, "flop_model": "B*2.55e6 (SURVEY 8d)"},
-            "walker_grad_avg_ms": walk_ms / max(walk_n, 1),
-            "mean_energy": mean_e, "energy_variance": var_e, "finite": finite,
+            "local_energy_evals_per_s": head["local_energy_evals_per_s"],
+            "mc_walker_steps_per_s": head["mc_walker_steps_per_s"],
+            "roofline": prop,
+            "roofline_local_energy": lap,
+            "walker_grad_avg_ms": head["walk_avg_ms"],
+            "mean_energy": head["mean_e"], "energy_variance": head["var_e"], "finite": head["finite"],
         }
+        if weak is not None:
+            wp, wl = rooflines(weak)
+            out["weak_scaling"] = {"walkers_per_gpu": weak["B"], "global_walkers": weak["total_walkers"],
+                                   "value": weak["value"], "ms_per_step": weak["ms_per_step"],
+                                   "local_energy_evals_per_s": weak["local_energy_evals_per_s"],
+                                   "mc_walker_steps_per_s": weak["mc_walker_steps_per_s"],
+                                   "roofline_frac": wp["frac"], "roofline_local_energy_frac": wl["frac"],
+                                   "finite": weak["finite"]}
+        if per_rank:
+            out["strong_scaling_per_rank"] = per_rank
         if world == 1 and not args.no_ecp:
             try:
                 out["ecp_c_atom"] = ecp_side_bench(dtype, dev, 4096, 5, not args.no_cpu_baseline)

@@ -102,21 +102,35 @@ def test_two_rank_blocks_equal_single_process(tmp_path):
     assert abs(float(var) - np.mean(np.abs(e - e.mean()) ** 2)) <= 1e-9 * np.var(e)
 
 
-def test_bench_two_ranks_under_torchrun(tmp_path):
-    """The driver's multi-GPU launch line with two ranks on the one test GPU (gloo): one JSON
-    line from rank 0 with n_gpus = 2 and the whole-job walker count."""
+def _bench_two_ranks(tmp_path, extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
-           "2", "--warmup", "1", "--walkers", "512", "--no-cpu-baseline", "--no-ecp", "--no-adam", "--no-dmc",
-           "--dist-backend", "gloo"]
+           "2", "--warmup", "1", "--no-cpu-baseline", "--no-ecp", "--no-adam", "--no-dmc",
+           "--dist-backend", "gloo"] + extra
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
                          env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout
-    r = json.loads(lines[0])
-    assert r["n_gpus"] == 2 and r["config"]["global_walkers"] == 1024 and r["finite"]
-    assert r["value"] > 0
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_under_torchrun(tmp_path):
+    """The driver's multi-GPU launch line with two ranks on the one test GPU (gloo).  Default =
+    SURVEY 8(d)'s strong scaling: --global-walkers in total split over the ranks (here 1024 ->
+    512 per rank), with the weak-scaling run (--walkers per rank) beside it."""
+    r = _bench_two_ranks(tmp_path, ["--global-walkers", "1024", "--walkers", "256"])
+    assert r["n_gpus"] == 2 and r["scaling"] == "strong" and r["finite"]
+    assert r["config"]["global_walkers"] == 1024 and r["config"]["walkers_per_gpu"] == 512
+    assert r["value"] > 0 and r["roofline"]["avg_launch_ms"] > 0
+    w = r["weak_scaling"]
+    assert w["walkers_per_gpu"] == 256 and w["global_walkers"] == 512 and w["value"] > 0 and w["finite"]
+
+
+def test_bench_two_ranks_weak_headline(tmp_path):
+    r = _bench_two_ranks(tmp_path, ["--weak", "--walkers", "512"])
+    assert r["scaling"] == "weak" and r["config"]["global_walkers"] == 1024 and "weak_scaling" not in r
+    assert r["value"] > 0 and r["finite"]
 
 
 _DMC_WORKER = r'''
