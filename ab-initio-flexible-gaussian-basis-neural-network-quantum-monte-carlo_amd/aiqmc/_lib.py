@@ -33,6 +33,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
     "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves", "aiqmc_phase_param_grad",
     "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals", "aiqmc_debug_set_ablate", "aiqmc_debug_set_fuse_accept", "aiqmc_debug_set_lap_waves",
+    "aiqmc_debug_set_fuse_reduce",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -126,6 +127,8 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_debug_set_ablate.restype = ctypes.c_int
     lib.aiqmc_debug_set_fuse_accept.argtypes = [vp, i32]
     lib.aiqmc_debug_set_fuse_accept.restype = ctypes.c_int
+    lib.aiqmc_debug_set_fuse_reduce.argtypes = [vp, i32]
+    lib.aiqmc_debug_set_fuse_reduce.restype = ctypes.c_int
     lib.aiqmc_debug_set_lap_waves.argtypes = [vp, i32]
     lib.aiqmc_debug_set_lap_waves.restype = ctypes.c_int
     lib.aiqmc_debug_set_proposal_reuse.argtypes = [vp, i32]
@@ -317,6 +320,13 @@ class Context:
     def set_fuse_accept(self, on: bool):
         """Diagnostics: fused (default) or separate per-sweep acceptance launch in mc_step."""
         check(self._lib.aiqmc_debug_set_fuse_accept(self._h, int(bool(on))), "aiqmc_debug_set_fuse_accept")
+
+    def set_fuse_reduce(self, mode):
+        """Diagnostics: fp32 mc_step limdrift sums fused into the walker / proposal launches as
+        exact integer accumulations: 1 (default) for batches <= 1,024 walkers, 2 always,
+        0 never (k_taueff reduction launches).  True/False map to 2/0."""
+        m = 2 if mode is True else (0 if mode is False else int(mode))
+        check(self._lib.aiqmc_debug_set_fuse_reduce(self._h, m), "aiqmc_debug_set_fuse_reduce")
 
     def set_ablate(self, mask: int):
         """Development builds (-DAQ_ABLATE) only: skip proposal phases to time them."""

@@ -21,6 +21,10 @@
 
 using namespace aq;
 
+// fp32 mc_step sums its limdrift reductions in the walker / proposal launches up to this many
+// walkers per call (aiqmc_debug_set_fuse_reduce: 1 = by batch size, 2 = always, 0 = never)
+constexpr int FUSE_REDUCE_MAX_B = 1024;
+
 // ============================================================================ small kernels
 
 // v2 = sum(x[0..n)) ; taueff = (sqrt(1 + 2 tau a v2) - 1)/(a v2), a = 0.25  (VMCmcstep.py:11-14)
@@ -336,6 +340,9 @@ static void free_ws(aiqmc_ctx* c) {
   c->d_g1 = c->d_g2 = c->d_u = nullptr;
   c->d_wc = c->d_ec = nullptr;
   c->d_taueff = nullptr;
+  if (c->d_tacc) (void)hipFree(c->d_tacc);
+  c->d_tacc = nullptr;
+  c->tacc_n = 0;
   c->ws_B = 0;
   c->ws_bytes = 0;
 }
@@ -707,10 +714,14 @@ int aiqmc_debug_local_energy_forward(aiqmc_ctx* c, const void* pos, int32_t B, v
 // launch and one inter-kernel gap fewer per sweep; same arithmetic, accept_one).
 // dmc (optional, device doubles [3]): DMC drift-diffusion extras (DMC/drift_diffusion.py:15-22):
 // dmc[0] = sum of the proposed coordinates, dmc[2] = tdamp = sum(x_new) / dmc[0]; never deferred.
+// tacc (optional, fp32 mc_step): this sweep's zeroed pair of fused limdrift accumulators
+// (walker_kernel.h TACC_SCALE); the two k_taueff launches are then skipped.
 static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double tstep, int rng_mode, const void* gauss1,
                     const void* gauss2, const void* u, int st, uint64_t seed, uint64_t step, int32_t* accept_out,
-                    double* dmc, hipStream_t s, AccArgs* pending = nullptr, bool defer = false) {
+                    double* dmc, hipStream_t s, AccArgs* pending = nullptr, bool defer = false,
+                    unsigned long long* tacc = nullptr) {
   const int N = c->N;
+  if (dmc) tacc = nullptr;
   const size_t es = c->dtype == AIQMC_F32 ? 4 : 8;
   double* dscr = dmc ? dmc_scratch(c) : nullptr;
   if (dmc && !dscr) return fail(AIQMC_EHIP, "hipMalloc: DMC scratch");
@@ -733,6 +744,7 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
   ka.logabs = c->d_lp;
   ka.grad = c->d_grad;
   ka.sumsq = c->d_sq;
+  ka.tacc = tacc;
   ka.wcache = c->d_wc;
   ka.tstep = tstep;
   ka.seed = seed;
@@ -747,11 +759,13 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
     pending->lpn = nullptr;
   }
   timed(c, 1, s, [&] { ops.walker(c->dtype, MODE_GRAD, ka, B, s); });
-  // (2) limdrift factor over the device batch (:60)
-  if (c->dtype == AIQMC_F32)
-    k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)c->d_sq, B, tstep, c->d_taueff);
-  else
-    k_taueff<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)c->d_sq, B, tstep, c->d_taueff);
+  // (2) limdrift factor over the device batch (:60) -- fused: summed by the walker launch
+  if (!tacc) {
+    if (c->dtype == AIQMC_F32)
+      k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)c->d_sq, B, tstep, c->d_taueff);
+    else
+      k_taueff<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)c->d_sq, B, tstep, c->d_taueff);
+  }
   // (3) single-electron proposals x^(i): value + gradient (:55-79, :95-97)
   KArgs kp = base_args(c);
   kp.nconf = B * N;
@@ -760,6 +774,7 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
   kp.pgrad = c->d_grad;
   kp.gauss1 = g1;
   kp.taueff = c->d_taueff;
+  kp.tacc = tacc;
   kp.tstep = tstep;
   kp.seed = seed;
   kp.step = step;
@@ -776,13 +791,16 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
     kp.wcache = c->d_wcp;   // per-proposal scratch of the same layout
   }
   timed(c, 0, s, [&] { ops.walker(c->dtype, MODE_GRAD, kp, B * N, s); });
-  // (4) limdrift factor of the proposal gradients over all B*N*3N entries (:80)
-  if (c->dtype == AIQMC_F32)
-    k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)c->d_sqn, B * N, tstep,
-                       c->d_taueff + 1);
-  else
-    k_taueff<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)c->d_sqn, B * N, tstep,
-                       c->d_taueff + 1);
+  // (4) limdrift factor of the proposal gradients over all B*N*3N entries (:80) -- fused:
+  // summed by the proposal launch
+  if (!tacc) {
+    if (c->dtype == AIQMC_F32)
+      k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)c->d_sqn, B * N, tstep,
+                         c->d_taueff + 1);
+    else
+      k_taueff<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)c->d_sqn, B * N, tstep,
+                         c->d_taueff + 1);
+  }
   if (dmc) {
     if (c->dtype == AIQMC_F32)
       k_dmc_sum_part<float><<<dim3(DMC_NB), dim3(256), 0, s>>>((const float*)pos, (const float*)c->d_grad,
@@ -802,6 +820,7 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
   a.gauss2 = g2;
   a.u = uu;
   a.taueff = c->d_taueff;
+  a.tacc = tacc;
   a.tstep = tstep;
   a.count = accept_out;
   if (defer && pending && !dmc) {
@@ -842,10 +861,28 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
     if (rc) return rc;
   }
   hipStream_t s = (hipStream_t)stream;
+  // fp32, small batches (the per-rank share of a strong-scaling run): the limdrift sums of every
+  // sweep accumulate in integer accumulators (walker_kernel.h; one set per sweep, zeroed once
+  // here) instead of two k_taueff launches per sweep.  N2, ms per VMC iteration, launches vs
+  // fused: 512 walkers 1.040 vs 1.000, 1024 walkers 1.399 vs 1.377, 4096 walkers 3.53 vs 3.56 --
+  // at 4096 the walker launch's wave-wide read of the accumulators before its fused acceptance
+  // and the proposals' atomics cost more than the two launches they replace.
+  unsigned long long* tacc = nullptr;
+  if (c->fuse_reduce && c->dtype == AIQMC_F32 && (c->fuse_reduce > 1 || B <= FUSE_REDUCE_MAX_B)) {
+    if (c->tacc_n < nsteps) {
+      if (c->d_tacc) (void)hipFree(c->d_tacc);
+      c->d_tacc = nullptr;
+      c->tacc_n = 0;
+      HIPCHK(hipMalloc((void**)&c->d_tacc, (size_t)2 * TACC_SLOTS * nsteps * sizeof(unsigned long long)));
+      c->tacc_n = nsteps;
+    }
+    tacc = c->d_tacc;
+    HIPCHK(hipMemsetAsync(tacc, 0, (size_t)2 * TACC_SLOTS * nsteps * sizeof(unsigned long long), s));
+  }
   AccArgs pending{};
   for (int st = 0; st < nsteps; ++st) {
     rc = mc_sweep(c, ops, pos, B, tstep, rng_mode, gauss1, gauss2, u, st, seed, offset + (uint64_t)st, accept_out,
-                  nullptr, s, &pending, c->fuse_accept && st + 1 < nsteps);
+                  nullptr, s, &pending, c->fuse_accept && st + 1 < nsteps, tacc ? tacc + 2 * TACC_SLOTS * st : nullptr);
     if (rc) return rc;
   }
   HIPCHK(hipGetLastError());
@@ -1353,6 +1390,13 @@ int aiqmc_debug_set_lap_waves(aiqmc_ctx* c, int32_t waves) {
 int aiqmc_debug_set_fuse_accept(aiqmc_ctx* c, int32_t on) {
   if (!c) return fail(AIQMC_EINVAL, "null context");
   c->fuse_accept = on != 0;
+  return AIQMC_OK;
+}
+
+int aiqmc_debug_set_fuse_reduce(aiqmc_ctx* c, int32_t on) {
+  if (!c) return fail(AIQMC_EINVAL, "null context");
+  if (on < 0 || on > 2) return fail(AIQMC_EINVAL, "fuse_reduce must be 0, 1 or 2");
+  c->fuse_reduce = on;
   return AIQMC_OK;
 }
 

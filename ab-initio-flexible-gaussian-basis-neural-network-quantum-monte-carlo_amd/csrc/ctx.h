@@ -44,6 +44,9 @@ struct aiqmc_ctx {
   bool reuse = true;                                        // proposals reuse the walker's cached stage
   int ablate = 0;                                           // AQ_ABLATE development builds (walker_rev.h)
   int fuse_accept = 1;                                      // acceptance fused into the next walker launch
+  int fuse_reduce = 1;                                      // fp32 mc_step: limdrift sums by integer atomics
+  unsigned long long* d_tacc = nullptr;                     // their per-sweep accumulators [tacc_n][2]
+  int tacc_n = 0;
   int lap_waves = 0;                                        // waves per walker of k_walker_lap (0: by batch)
   int ncu = 256;                                            // compute units of the device
   double* d_taueff = nullptr;

@@ -478,9 +478,11 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
   if constexpr (WALK) {
     // ---------------------------------------------------------------- F0 positions (+ acceptance)
     if (ka.acc.lpn) {
+      const T te1 = taueff_wave<T>(ka.acc.taueff, ka.acc.tacc, 0, ka.acc.tstep);
+      const T te2 = taueff_wave<T>(ka.acc.taueff, ka.acc.tacc, 1, ka.acc.tstep);
       if (sl < N) {   // the previous sweep's acceptance of this walker's N proposals
         T xn[3];
-        const bool acc = accept_one<T, N>(ka.acc, (const T*)ka.pos, conf, sl, xn);
+        const bool acc = accept_one<T, N>(ka.acc, (const T*)ka.pos, conf, sl, xn, te1, te2);
 #pragma unroll
         for (int c = 0; c < 3; ++c) xs[3 * sl + c] = xn[c];
         if (acc && act) {
@@ -1024,6 +1026,7 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
       if (ka.logabs) ((T*)ka.logabs)[conf] = T(0.5) * lsum0 + jt;
       if (ka.phase) ((T*)ka.phase)[conf] = f_atan2(ui0 * sg, ur0 * sg);
       if (ka.sumsq) ((T*)ka.sumsq)[conf] = sumsq;
+      if (ka.tacc) tacc_add(ka.tacc, WALK ? 0 : 1, conf, (double)sumsq);
     }
     if (WALK && ka.dg1 && sl < N) {   // the sweep's draws of walker conf (k_draws' arithmetic)
       const uint32_t t = (uint32_t)(conf * N + sl);

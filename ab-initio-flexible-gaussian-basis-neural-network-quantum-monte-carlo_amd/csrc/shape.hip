@@ -24,10 +24,12 @@ static int fail(int code, const std::string& m) { return aiqmc_fail(code, m); }
 template <typename T, int N>
 __global__ __launch_bounds__(256) void k_accept(T* __restrict__ pos, AccArgs a, int B) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  // limdrift factors: every lane of the (full, 256-thread) block's waves before any returns
+  const T te1 = taueff_wave<T>(a.taueff, a.tacc, 0, a.tstep), te2 = taueff_wave<T>(a.taueff, a.tacc, 1, a.tstep);
   if (t >= B * N) return;
   const int b = t / N, i = t - b * N;
   T xn[3];
-  if (accept_one<T, N>(a, pos, b, i, xn)) {
+  if (accept_one<T, N>(a, pos, b, i, xn, te1, te2)) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) pos[(size_t)b * 3 * N + 3 * i + c] = xn[c];
     if (a.count) atomicAdd(&a.count[b], 1);

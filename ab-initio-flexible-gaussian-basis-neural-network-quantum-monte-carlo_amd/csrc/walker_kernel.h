@@ -37,6 +37,45 @@ constexpr int MODE_GRAD_FWD = 3;   // forward-mode gradient (diagnostics / cross
 // the next sweep's walker launch (lpn != nullptr): the walkers' gradients, log|psi| and limdrift
 // factors at the start of that sweep, the proposals' log|psi| and own-electron gradients, and
 // the sweep's draws.
+// Fused limdrift reductions (VMCmcstep.py:11-14, quirk Q8), fp32 Metropolis sweeps: instead of a
+// reduction launch after the walker launch and after the proposal launch, every configuration's
+// wave adds its |grad|^2 to one of TACC_SLOTS 64-bit integer accumulators of the sweep (slot =
+// configuration mod 1024: one address for every wave of a launch serialises the atomics in L2,
+// measured 715 instead of 249 us per proposal launch, 64 slots still +9 us) in units of 2^-16
+// (TACC_SCALE).  Integer
+// addition is exact and associative, so the sums -- and the limdrift factor every consumer
+// derives from them -- are bit-for-bit the same in any arrival order.  The quantum is far below
+// the float rounding of v2 (>= ~1 per configuration); an accumulator holds up to 2.8e14.  Two
+// launches and two inter-kernel gaps fewer per sweep.
+constexpr double TACC_SCALE = 65536.0;
+constexpr int TACC_SLOTS = 1024;
+__device__ __forceinline__ unsigned long long tacc_fix(double x) {
+  return (unsigned long long)(x * TACC_SCALE + 0.5);
+}
+__device__ __forceinline__ void tacc_add(unsigned long long* acc, int kind, int conf, double v) {
+  atomicAdd(acc + kind * TACC_SLOTS + (conf & (TACC_SLOTS - 1)), tacc_fix(v));
+}
+// taueff = (sqrt(1 + 2 tau a v2) - 1) / (a v2), a = 0.25, in T (k_taueff's arithmetic)
+template <typename T> __device__ __forceinline__ T taueff_from_v2(double v2, double tstep) {
+  const double a = 0.25;
+  const T v2t = (T)v2;
+  return (sqrt((T)1 + (T)2 * (T)tstep * (T)a * v2t) - (T)1) / ((T)a * v2t);
+}
+// Limdrift factor k (0: walkers, 1: proposals) of the sweep: the sum of the fused accumulators
+// (one slot per lane, exact integer wave sum) or k_taueff's result.  Every lane of the wave must
+// be active (call it outside divergent code); the result is wave-uniform.
+template <typename T>
+__device__ __forceinline__ T taueff_wave(const double* te, const unsigned long long* acc, int k, double tstep) {
+  if (!acc) return (T)te[k];
+  const unsigned long long* a = acc + k * TACC_SLOTS + (int)(threadIdx.x & 63);
+  unsigned long long v = 0;
+#pragma unroll
+  for (int j = 0; j < TACC_SLOTS / 64; ++j) v += a[64 * j];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return taueff_from_v2<T>((double)v * (1.0 / TACC_SCALE), tstep);
+}
+
 struct AccArgs {
   const void* grad;       // [B][3N]
   const void* lp;         // [B]
@@ -46,6 +85,7 @@ struct AccArgs {
   const void* gauss2;     // [B][N][3]
   const void* u;          // [B][N]
   const double* taueff;   // [2]
+  const unsigned long long* tacc;   // [2][TACC_SLOTS] fused accumulators of the sweep (nullptr: taueff)
   double tstep;
   int32_t* count;         // [B] accepted moves (optional)
 };
@@ -53,10 +93,11 @@ struct AccArgs {
 // Electron i of walker b: t_pro (sum over xyz, Q6), acceptance |exp(lp_i - lp)|^2 t_pro > u.
 // Returns the electron's position after the step in xn (moved or not); pos itself is not written.
 template <typename T, int N>
-__device__ __forceinline__ bool accept_one(const AccArgs& a, const T* __restrict__ pos, int b, int i, T xn[3]) {
+// te1, te2: the sweep's limdrift factors (taueff_wave, computed by the caller outside divergent code).
+__device__ __forceinline__ bool accept_one(const AccArgs& a, const T* __restrict__ pos, int b, int i, T xn[3], T te1,
+                                           T te2) {
   const T tstep = (T)a.tstep;
   const T sq = sqrt(tstep);
-  const T te1 = (T)a.taueff[0], te2 = (T)a.taueff[1];
   const T* grad = (const T*)a.grad;
   const T* gown = (const T*)a.gown;
   const T* g1 = (const T*)a.gauss1;
@@ -100,6 +141,10 @@ struct KArgs {
   const void* pgrad;      // [B][3N] grad log|psi| at the walkers
   const void* gauss1;     // [B][3N] standard normals (host draws or k_draws output)
   const double* taueff;   // device scalar: limdrift factor of pgrad (VMCmcstep.py:11-14)
+  // fused limdrift accumulators of the sweep [2][TACC_SLOTS] (fp32 mc_step; nullptr elsewhere):
+  // walker launches add their |grad|^2 to kind 0, proposal launches to kind 1; readers of the
+  // walker factor (moved electron, proposals from scratch) sum kind 0 (taueff_wave)
+  unsigned long long* tacc;
   double tstep;
   uint64_t seed, step;
   // single-electron-move layout (proposal != 0, k_walker_rev / k_moved_electron): configuration
@@ -372,7 +417,7 @@ __global__ __launch_bounds__(64) void k_walker(KArgs ka) {
     T x = ((const T*)ka.pos)[(size_t)pb * 3 * N + lane];
     if (ka.proposal && lane / 3 == pi) {
       const T z = ((const T*)ka.gauss1)[(size_t)pb * 3 * N + lane];   // drawn by the host or k_draws
-      const T ge = ((const T*)ka.pgrad)[(size_t)pb * 3 * N + lane] * (T)(*ka.taueff);
+      const T ge = ((const T*)ka.pgrad)[(size_t)pb * 3 * N + lane] * (T)(*ka.taueff);   // never fused (not mc_step)
       x = x + (ge * tstep + f_sqrt(tstep) * z);
     }
     xs[lane] = x;

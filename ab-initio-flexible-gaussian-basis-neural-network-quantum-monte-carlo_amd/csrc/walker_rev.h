@@ -38,6 +38,16 @@ static __device__ unsigned long long aq_phase_cycles[32];
 #elif defined(AQ_PHASE_MARK)
 // ISA-inspection build: a marker comment in the assembly at each phase boundary
 #define AQ_PH(k) asm volatile(";AQMARK " #k)
+#elif defined(AQ_STOP_AFTER)
+// register-pressure probe (never a product build): the proposal path ends after phase k, its
+// live LDS state kept alive by one store, so the compiled VGPR count is the peak up to phase k
+#define AQ_PH(k)                                                                     \
+  do {                                                                               \
+    if constexpr (PROP && (k) == AQ_STOP_AFTER) {                                    \
+      if (ka.logabs) ((T*)ka.logabs)[conf * 64 + lane] = sm[lane] + sm[lane + 1024]; \
+      return;                                                                        \
+    }                                                                                \
+  } while (0)
 #else
 #define AQ_PH(k) \
   do {           \
@@ -208,7 +218,7 @@ __global__ __launch_bounds__(64 * MOVED_WPB) void k_moved_electron(KArgs ka) {
     for (int c = 0; c < 3; ++c) xp[c] = ((const T*)ka.xnew)[(size_t)q * 3 + c];
   } else {
     const T tstep = (T)ka.tstep;
-    const T te = (T)(*ka.taueff);
+    const T te = taueff_wave<T>(ka.taueff, ka.tacc, 0, ka.tstep);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const size_t o = (size_t)b * 3 * N + 3 * i + c;
@@ -368,11 +378,15 @@ k_walker_rev(KArgs ka) {
     pb = conf / mper;
     pi = (conf - pb * mper) / mdiv;
   }
+  // reuse-off proposals: the walker limdrift factor, read by the wave before the divergent F0
+  const T te_walk = (!PROP && isprop && !ka.xnew) ? taueff_wave<T>(ka.taueff, ka.tacc, 0, ka.tstep) : T(0);
   if (!PREP && !isprop && ka.acc.lpn) {
     // the previous sweep's acceptance of this walker's N proposals (k_accept's arithmetic)
+    const T te1 = taueff_wave<T>(ka.acc.taueff, ka.acc.tacc, 0, ka.acc.tstep);
+    const T te2 = taueff_wave<T>(ka.acc.taueff, ka.acc.tacc, 1, ka.acc.tstep);
     if (lane < N) {
       T xn[3];
-      const bool acc = accept_one<T, N>(ka.acc, (const T*)ka.pos, conf, lane, xn);
+      const bool acc = accept_one<T, N>(ka.acc, (const T*)ka.pos, conf, lane, xn, te1, te2);
 #pragma unroll
       for (int c = 0; c < 3; ++c) xs[3 * lane + c] = xn[c];
       if (acc) {
@@ -389,7 +403,7 @@ k_walker_rev(KArgs ka) {
         x = ((const T*)ka.xnew)[(size_t)conf * 3 + (lane - 3 * pi)];
       } else {
         const T z = ((const T*)ka.gauss1)[(size_t)pb * 3 * N + lane];   // drawn by the host or k_draws
-        const T ge = ((const T*)ka.pgrad)[(size_t)pb * 3 * N + lane] * (T)(*ka.taueff);
+        const T ge = ((const T*)ka.pgrad)[(size_t)pb * 3 * N + lane] * te_walk;
         x = x + (ge * tstep + f_sqrt(tstep) * z);
       }
     }
@@ -1253,6 +1267,7 @@ k_walker_rev(KArgs ka) {
     if (ka.logabs) ((T*)ka.logabs)[conf] = lpsi;
     if (ka.phase) ((T*)ka.phase)[conf] = f_atan2(phi, phr);
     if (ka.sumsq) ((T*)ka.sumsq)[conf] = sumsq;
+    if (ka.tacc) tacc_add(ka.tacc, isprop ? 1 : 0, conf, (double)sumsq);
   }
   if constexpr (!PREP) {
     if (ka.dg1 && !isprop && lane < N) {   // the sweep's draws of walker conf (k_draws)

@@ -261,6 +261,14 @@ int aiqmc_debug_set_lap_waves(aiqmc_ctx* ctx, int32_t waves);
  * sweep.  Both are bitwise identical (same arithmetic, same order). */
 int aiqmc_debug_set_fuse_accept(aiqmc_ctx* ctx, int32_t on);
 
+/* Diagnostics: in fp32, aiqmc_mc_step can sum the two limdrift reductions of each sweep
+ * (|grad|^2 over the walkers, over the proposals; VMCmcstep.py:11-14) inside the walker and
+ * proposal launches, as exact 64-bit integer sums of |grad|^2 in units of 2^-16: no reduction
+ * launches, and the same bits in any arrival order.  mode 1 (default) = for batches of at most
+ * 1,024 walkers (where it is faster), 2 = always, 0 = never (the k_taueff reduction launches;
+ * fp64 always uses them).  Results agree to the float rounding of v2. */
+int aiqmc_debug_set_fuse_reduce(aiqmc_ctx* ctx, int32_t on);
+
 /* Development builds (-DAQ_ABLATE) only: skip proposal-kernel phases (bit mask, walker_rev.h) to
  * time their marginal cost; results are meaningless.  No effect in product builds. */
 int aiqmc_debug_set_ablate(aiqmc_ctx* ctx, int32_t mask);

@@ -15,6 +15,8 @@ ctx = s.context(dtype=torch.float32)
 ctx.set_params(flatten_params(s.make_network().init(1)))
 if os.environ.get("AIQMC_NOFUSE"):
     ctx.set_fuse_accept(False)
+if os.environ.get("AIQMC_FUSE_REDUCE"):     # 0: k_taueff launches, 1: by batch size (default), 2: integer atomics
+    ctx.set_fuse_reduce(int(os.environ["AIQMC_FUSE_REDUCE"]))
 if os.environ.get("AIQMC_LAPW"):      # waves per walker of the local energy's second launch
     ctx.set_lap_waves(int(os.environ["AIQMC_LAPW"]))
 if os.environ.get("AIQMC_NOREUSE"):   # every proposal from scratch (PMC comparison of the two paths)

@@ -39,6 +39,17 @@ __global__ __launch_bounds__(64) void k_rate(float* out, unsigned long long* cyc
         x[k] += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x[k]), 0xB1, 0xF, 0xF, true));
       } else if constexpr (KIND == 5) {   // v_rcp_f32
         x[k] = __builtin_amdgcn_rcpf(x[k]);
+      } else if constexpr (KIND == 6) {   // v_cndmask_b32 (select on a lane-dependent compare)
+        x[k] = (x[k] > b) ? x[k] : x[(k + 3) % ILP];
+      } else if constexpr (KIND == 7) {   // v_mov_b32_dpp row_newbcast alone (result used by a plain add)
+        const float d = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x[(k + 1) % ILP]), 0x153, 0xF, 0xF, false));
+        x[k] = x[k] + d;
+      } else if constexpr (KIND == 8) {   // integer v_add_u32 + v_lshl_add_u32 (address-style arithmetic)
+        int v = __builtin_bit_cast(int, x[k]);
+        v = (v << 2) + (int)threadIdx.x;
+        x[k] = __builtin_bit_cast(float, v);
+      } else if constexpr (KIND == 9) {   // v_readlane_b32 to an SGPR and back into a VALU op
+        x[k] = x[k] + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x[(k + 1) % ILP]), k));
       }
     }
   }
@@ -72,7 +83,7 @@ static void run(const char* name, int waves_per_simd) {
   double avg = 0;
   for (auto v : h) avg += (double)v;
   avg /= nblk;
-  const double insts = (double)ITERS * ILP * ((KIND == 1 || KIND == 4) ? 2 : 1);
+  const double insts = (double)ITERS * ILP * ((KIND == 1 || KIND == 4 || KIND == 6 || KIND == 7 || KIND == 9) ? 2 : 1);
   printf("%-12s waves/SIMD=%d  wave cycles=%.0f  cyc/inst/SIMD=%.2f  wall=%.3f ms  clk=%.2f GHz\n", name,
          waves_per_simd, avg, avg / (waves_per_simd * insts), ms, avg / (ms * 1e6));
   hipFree(out);
@@ -87,6 +98,10 @@ int main() {
     run<2>("exp", w);
     run<5>("rcp", w);
     run<3>("pk_fma", w);
+    run<6>("cndmask", w);
+    run<7>("dppmov+add", w);
+    run<8>("int2", w);
+    run<9>("readlane+add", w);
   }
   return 0;
 }
