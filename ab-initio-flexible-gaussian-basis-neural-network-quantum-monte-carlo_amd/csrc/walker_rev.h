@@ -710,7 +710,15 @@ k_walker_rev(KArgs ka) {
     for (int s4 = 0; s4 < SM::QM / 4; ++s4) {
       if (s4 < QF) {
         const int q0 = 4 * s4;
+#ifndef AQ_F4_BRANCH_SELECT
+        // the four quad sums are complete before the selection: left to itself the compiler sinks
+        // their last DPP add into divergent branches (exec-mask save/restore per output lane)
+        T z0 = zc[q0], z1 = zc[q0 + 1], z2 = zc[q0 + 2], z3 = zc[q0 + 3];
+        asm volatile("" : "+v"(z0), "+v"(z1), "+v"(z2), "+v"(z3));
+        const T zs = (ff & 2) ? ((ff & 1) ? z3 : z2) : ((ff & 1) ? z1 : z0);
+#else
         const T zs = ff == 0 ? zc[q0] : (ff == 1 ? zc[q0 + 1] : (ff == 2 ? zc[q0 + 2] : zc[q0 + 3]));
+#endif
         const T c = f_tanh(zs * T(0.25) + convb[q0 + ff]);
         if (ilive) cqv[SM::cqo(l, ic) + q0 + ff] = c;
         cq[q0 + 0] = quad_bcast<0>(c);
