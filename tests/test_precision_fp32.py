@@ -99,3 +99,59 @@ def test_fp32_kernel_no_worse_than_fp32_reference_arithmetic(golden_dir):
     ref_g = np.abs(g["grad_32"] - g["grad_64"]).max(axis=1)
     _no_worse("grad (local-energy kernels)", np.abs(gr - g["grad_64"]).max(axis=1), ref_g, 1.1)
     _no_worse("grad (Metropolis kernels)", np.abs(ga - g["grad_64"]).max(axis=1), ref_g, 1.1)
+
+
+def _cancellation_scale(g):
+    """Per walker, the size of the terms that cancel in E_L = V - (lap + |grad|^2)/2 near a node:
+    S = |grad|^2 + |lap| + |V| from the float64 oracle (lap recovered from E_L, V and |grad|^2)."""
+    from oracle import system
+    s = system.make_system("N2")
+    pos = g["pos"].reshape(len(g["pos"]), -1, 3)
+    atoms, Z = np.asarray(s.atoms, dtype=np.float64), np.asarray(s.charges, dtype=np.float64)
+    ee = np.linalg.norm(pos[:, :, None, :] - pos[:, None, :, :], axis=-1)
+    iu = np.triu_indices(pos.shape[1], 1)
+    v = (1.0 / ee[:, iu[0], iu[1]]).sum(1)
+    v -= (Z[None, None, :] / np.linalg.norm(pos[:, :, None, :] - atoms[None, None], axis=-1)).sum((1, 2))
+    v += Z[0] * Z[1] / np.linalg.norm(atoms[0] - atoms[1])
+    g2 = (g["grad_64"] ** 2).sum(1)
+    lap = -2.0 * (g["e_l_64"] - v) - g2
+    return g2 + np.abs(lap) + np.abs(v)
+
+
+@pytest.mark.gpu
+def test_fp32_tail_no_worse_than_fp32_reference_arithmetic(golden_dir):
+    """The tail of the fp32 E_L error (the worst walker was 46 Ha off against 12 Ha for
+    the fp32 oracle).  Near a node E_L is a difference of terms ~ 1/d^2 (|grad|^2 ~ 1e6 on the
+    worst walker of this fixture) and both fp32 implementations lose digits in proportion to them,
+    so the per-walker error is compared RELATIVE to that cancellation scale S = |grad|^2 + |lap| +
+    |V| (float64 oracle).  Bounds (observed values printed): the p99.5 of |dE| within 1.25x of the
+    fp32 oracle's; the mean of the 5 worst normalised errors within 2x of the oracle's 5 worst;
+    the worst normalised error within 2x of the oracle's worst (1.1e-4, ~1,800 float32 ulps of
+    S: the cancellation scale does not capture the orbital matrix's own condition)."""
+    g = _fixture(golden_dir)
+    ctx = _ctx(torch.float32, g["params_flat"])
+    x = torch.tensor(g["pos"], dtype=torch.float32, device="cuda")
+    e, _, _ = ctx.local_energy(x)
+    torch.cuda.synchronize()
+    eh = np.abs(e.double().cpu().numpy() - g["e_l_64"])
+    er = np.abs(g["e_l_32"] - g["e_l_64"])
+    S = _cancellation_scale(g)
+    nh, nr = eh / S, er / S
+    top_h, top_r = np.sort(nh)[-5:], np.sort(nr)[-5:]
+    print("p99.5 |dE| hip", np.quantile(eh, 0.995), "fp32 oracle", np.quantile(er, 0.995))
+    print("5 worst |dE|/S hip", top_h, "fp32 oracle", top_r)
+    print("worst walker hip", int(nh.argmax()), eh[nh.argmax()], "S", S[nh.argmax()])
+    assert np.quantile(eh, 0.995) <= 1.25 * np.quantile(er, 0.995)
+    assert top_h.mean() <= 2.0 * top_r.mean(), (top_h, top_r)
+    assert nh.max() <= 2.0 * nr.max(), (nh.max(), nr.max())
+
+
+def test_cancellation_scale_of_the_fixture(golden_dir):
+    """CPU: the scale used above is large exactly where the fp32 oracle's errors are (its two
+    12 Ha walkers sit at S ~ 5e5-1.6e6) and the normalised oracle errors stay ~1e-4 at most."""
+    g = _fixture(golden_dir)
+    S = _cancellation_scale(g)
+    er = np.abs(g["e_l_32"] - g["e_l_64"])
+    worst = np.argsort(er)[-3:]
+    assert np.all(S[worst] > 1e4)
+    assert (er / S).max() < 2e-4
