@@ -56,7 +56,10 @@ def pmean_stats(e_l: torch.Tensor):
     n = float(e.numel())
     m = e.mean()
     m2 = ((e - m) * (e - m)).sum()
-    v = torch.stack([m2, n * m, n * m * m, torch.tensor(n, dtype=torch.float64, device=e.device)])
+    # the count as a device fill, not a host scalar copied in: torch.tensor(n, device=...) is a
+    # pageable host-to-device copy that waits for the stream (a drain per VMC iteration)
+    cnt = torch.full((), n, dtype=torch.float64, device=e.device)
+    v = torch.stack([m2, n * m, n * m * m, cnt])
     v = psum(v)
     mean = v[1] / v[3]
     between = torch.clamp(v[2] - v[3] * mean * mean, min=0.0)
