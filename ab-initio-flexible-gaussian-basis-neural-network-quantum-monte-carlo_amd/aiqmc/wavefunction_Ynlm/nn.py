@@ -248,10 +248,10 @@ def make_ai_net(nspins, charges, parallel_indices, antiparallel_indices, spin_up
                 n_parallel: int, n_antiparallel: int, ndim: int, natoms: int, nelectrons: int,
                 determinants: int = 1, bias_orbitals: bool = True, rescale_inputs: bool = False,
                 hidden_dims=DEFAULT_HIDDEN_DIMS, hidden_dims_Ynlm=DEFAULT_HIDDEN_DIMS_YNLM) -> Network:
-    """nn.py:511-553.  ``determinants`` is ignored exactly as in the reference (Q10)."""
-    del determinants
-    if not bias_orbitals:
-        raise NotImplementedError("bias_orbitals=False is not built (reference default True)")
+    """nn.py:511-553.  ``determinants`` is ignored exactly as in the reference (Q10), and so is
+    ``bias_orbitals``: the reference accepts it (nn.py:523) but never hands it to make_orbitals
+    (nn.py:531-539), whose orbital layer always carries its bias."""
+    del determinants, bias_orbitals
     if rescale_inputs:
         raise NotImplementedError("rescale_inputs=True is not built (reference default False)")
     if tuple(tuple(h) for h in hidden_dims) != DEFAULT_HIDDEN_DIMS or \

@@ -105,6 +105,9 @@ def test_unsupported_options_fail_loudly():
         nn.make_ai_net(rescale_inputs=True, **kw)
     with pytest.raises(NotImplementedError):
         nn.make_ai_net(hidden_dims=((8, 4),) * 3, **kw)
+    # bias_orbitals is accepted and ignored, as in the reference (nn.py:523 is never forwarded)
+    a, b = nn.make_ai_net(bias_orbitals=False, **kw), nn.make_ai_net(**kw)
+    np.testing.assert_array_equal(nn.flatten_params(a.init(0)), nn.flatten_params(b.init(0)))
 
 
 def test_spin_tables_product_equals_oracle():
