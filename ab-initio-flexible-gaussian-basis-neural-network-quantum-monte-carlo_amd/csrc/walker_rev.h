@@ -89,6 +89,12 @@ struct SmemRev {
   // the walker's pivot record [2N+2] (proposals) lives in the g2 region during F5: the g2
   // values are dead after F4 and their adjoints are written from B2 on
   static constexpr int pv = g2;
+  // proposals: F5's slot table after the pivot record, [4 RW slots][4] ints (Yt row offset, the
+  // h^3 row offset for each half of the spin-stacked orbital weights, flag), then a zero row
+  static constexpr int RW = (N + 3) / 4;
+  static constexpr int st = ((g2 + 2 * N + 2 + 3) / 4) * 4;
+  static constexpr int zr = st + (4 * RW * 4 * 4 + (int)sizeof(T) - 1) / (int)sizeof(T);
+  static_assert(zr + 4 <= g2 + 3 * 2 * N * 4, "slot table outside the g2 region");
   static constexpr int end = R + R_n;
   static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
   static constexpr int hoff(int l) { return l == 0 ? 0 : N * D0; }   // l = 0 or 3
@@ -161,6 +167,15 @@ __device__ __forceinline__ void pair_values(const T d[3], cptr<T> P, T out[3][4]
 template <typename T> __device__ __forceinline__ T class4_sum(T x) {
   x += dpp<0x124>(x);
   x += dpp<0x128>(x);
+#ifdef AQ_PERMLANE_SUM
+  if constexpr (sizeof(T) == 4) {
+    // across the rows on the VALU (gfx950 row swaps; the same additions as the xor shuffles)
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+  }
+#endif
   x += __shfl_xor(x, 16);
   x += __shfl_xor(x, 32);
   return x;
@@ -176,6 +191,16 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Kernel arguments read at the end of the kernel: through an opaque copy of the kernarg segment
+// pointer, so that their loads are issued where they are used instead of being hoisted into SGPRs
+// that live across the whole kernel (the proposal kernel spills SGPRs through VALU lane writes).
+// The kernels take one argument (KArgs), at kernarg offset 0.
+__device__ __forceinline__ const __attribute__((address_space(4))) KArgs* late_args() {
+  auto p = (const __attribute__((address_space(4))) KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
 }
 
 // Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2):
@@ -424,6 +449,7 @@ k_walker_rev(KArgs ka) {
   T* g2 = sm + SM::g2;
   T jv = T(0), jd1 = T(0), jve = T(0);
   T pvr = T(0);
+  int rsl = 0;   // PROP: rowsrc[lane]
   if (reuse) {
     // walker pb's cached stage and pair sums, electron pi's entries from k_moved_electron;
     // all loads issued before the first LDS store
@@ -439,22 +465,24 @@ k_walker_rev(KArgs ka) {
       const int l3 = lane < 3 * N ? lane : 3 * N - 1;
       x0 = ((const T*)ka.pos)[(size_t)pb * 3 * N + l3];
       xm = Eq[EC::xp + (mvl ? lane - 3 * pi : 0)];
+      rsl = rowsrc[lane < N ? lane : N - 1];   // F5's slot table (after F4)
     }
+    // unsigned offsets: the loads take the wave's base pointer in SGPRs plus a 32-bit lane offset
 #pragma unroll
     for (int t = 0; t < NY; ++t) {
-      const int idx = lane + 64 * t;
-      const int ix = idx < N * N ? idx : N * N - 1;
-      const int r = ix / N;
+      const unsigned idx = lane + 64 * t;
+      const unsigned ix = idx < N * N ? idx : N * N - 1;
+      const unsigned r = ix / N;
       const T a = Wc[WC::yv + ix], b = Eq[EC::yv + (ix - r * N)];
-      ry[t] = (r == pi) ? b : a;
+      ry[t] = ((int)r == pi) ? b : a;
     }
 #pragma unroll
     for (int t = 0; t < NHh; ++t) {
-      const int idx = lane + 64 * t;
-      const int ix = idx < N * D0 ? idx : N * D0 - 1;
-      const int e = ix / D0;
+      const unsigned idx = lane + 64 * t;
+      const unsigned ix = idx < N * D0 ? idx : N * D0 - 1;
+      const unsigned e = ix / D0;
       const T a = Wc[WC::h0 + ix], b = Eq[EC::h0 + (ix - e * D0)];
-      rh[t] = (e == pi) ? b : a;
+      rh[t] = ((int)e == pi) ? b : a;
     }
 #pragma unroll
     for (int t = 0; t < NG; ++t) {
@@ -656,6 +684,36 @@ k_walker_rev(KArgs ka) {
   const bool inG1 = ic >= nup;
   T hreg = T(0);
   if (!AQ_ABL(2)) {
+#ifndef AQ_F4_NO_PRELOAD
+  // this lane's layer weights (electron ic's conv weights and biases at unit ff, the single
+  // layer's column ff), layer l + 1's issued before layer l's arithmetic so that their latency
+  // overlaps it (left alone the compiler issues each layer's loads at their first use)
+  T wcv[3][SM::QM], wcb[3][SM::QM], wsw[3][SM::QM], wsb[3];
+  auto lw_load = [&](int l) {
+    const int d1 = l == 0 ? D0 : NH;
+    const int DF = 3 * d1 + 8;
+    const int Q = DF / 4;
+    const cptr<T> cw = P + (l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2)) + ic * DF;
+    const cptr<T> cb = P + (l == 0 ? Ly::conv_b0 : (l == 1 ? Ly::conv_b1 : Ly::conv_b2)) + ic * Q;
+    const cptr<T> sw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
+    const cptr<T> sb = P + (l == 0 ? Ly::sng_b0 : (l == 1 ? Ly::sng_b1 : Ly::sng_b2));
+#pragma unroll
+    for (int q = 0; q < SM::QM; ++q)
+      if (q < Q) {
+        wcv[l][q] = cw[4 * q + ff];
+        wsw[l][q] = sw[q * 4 + ff];
+      }
+    // conv biases: lane f's output of each full quad, then the Q mod 4 outputs every lane evaluates
+#pragma unroll
+    for (int s4 = 0; s4 < SM::QM / 4; ++s4)
+      if (s4 < Q / 4) wcb[l][s4] = cb[4 * s4 + ff];
+#pragma unroll
+    for (int q = 0; q < SM::QM; ++q)
+      if (q >= 4 * (Q / 4) && q < Q) wcb[l][q] = cb[q];
+    wsb[l] = sb[ff];
+  };
+  lw_load(0);
+#endif
 #pragma unroll
   for (int l = 0; l < 3; ++l) {
     const int d1 = l == 0 ? D0 : NH;
@@ -666,6 +724,21 @@ k_walker_rev(KArgs ka) {
     const cptr<T> convb = P + (l == 0 ? Ly::conv_b0 : (l == 1 ? Ly::conv_b1 : Ly::conv_b2)) + ic * Q;
     const cptr<T> sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
     const cptr<T> sngb = P + (l == 0 ? Ly::sng_b0 : (l == 1 ? Ly::sng_b1 : Ly::sng_b2));
+#ifndef AQ_F4_NO_PRELOAD
+    if (l + 1 < 3) lw_load(l + 1);
+    asm volatile("" ::: "memory");
+#define AQ_CW(q) wcv[l][q]
+#define AQ_CB(s4) wcb[l][s4]
+#define AQ_CR(q) wcb[l][q]
+#define AQ_SW(q) wsw[l][q]
+#define AQ_SB() wsb[l]
+#else
+#define AQ_CW(q) convw[4 * (q) + ff]
+#define AQ_CB(s4) convb[4 * (s4) + ff]
+#define AQ_CR(q) convb[q]
+#define AQ_SW(q) sngw[(q) * 4 + ff]
+#define AQ_SB() sngb[ff]
+#endif
     // conv output q = tanh(mean_4(f w) + b) over the input quad 4q..4q+3
     // (network_blocks.py:106-116): lane f of electron ic holds input 4q + f (h^l unit
     // 4t + f, a group mean of unit 4t + f, or a g2 unit f) and the quad adds the four
@@ -695,7 +768,7 @@ k_walker_rev(KArgs ka) {
         if (q < T4) F = hown[q];
         else if (q < 3 * T4) F = gown[(q - T4) / T4][(q - T4) % T4];
         else F = g2[((l * 2 + (q - 3 * T4)) * N + ic) * 4 + ff];
-        T z = F * convw[4 * q + ff];
+        T z = F * AQ_CW(q);
         z += dpp<0xB1>(z);
         z += dpp<0x4E>(z);
         zc[q] = z;
@@ -719,7 +792,7 @@ k_walker_rev(KArgs ka) {
 #else
         const T zs = ff == 0 ? zc[q0] : (ff == 1 ? zc[q0 + 1] : (ff == 2 ? zc[q0 + 2] : zc[q0 + 3]));
 #endif
-        const T c = f_tanh(zs * T(0.25) + convb[q0 + ff]);
+        const T c = f_tanh(zs * T(0.25) + AQ_CB(s4));
         if (ilive) cqv[SM::cqo(l, ic) + q0 + ff] = c;
         cq[q0 + 0] = quad_bcast<0>(c);
         cq[q0 + 1] = quad_bcast<1>(c);
@@ -730,27 +803,52 @@ k_walker_rev(KArgs ka) {
 #pragma unroll
     for (int q = 0; q < SM::QM; ++q) {
       if (q >= 4 * QF && q < Q) {
-        cq[q] = f_tanh(zc[q] * T(0.25) + convb[q]);
+        cq[q] = f_tanh(zc[q] * T(0.25) + AQ_CR(q));
         if (ilive && (q & 3) == ff) cqv[SM::cqo(l, ic) + q] = cq[q];
       }
     }
-    T z = sngb[ff], z1 = T(0);   // even / odd q: two independent chains
+    T z = AQ_SB(), z1 = T(0);   // even / odd q: two independent chains
 #pragma unroll
     for (int q = 0; q < SM::QM; ++q)
       if (q < Q) {
-        if (q & 1) z1 += cq[q] * sngw[q * 4 + ff];
-        else z += cq[q] * sngw[q * 4 + ff];
+        if (q & 1) z1 += cq[q] * AQ_SW(q);
+        else z += cq[q] * AQ_SW(q);
       }
     z += z1;
     const T sval = f_tanh(z);
     if (ilive) sv[(l * N + ic) * 4 + ff] = sval;
     const T hin = l == 0 ? hl[ic * D0 + ff] : hreg;
     hreg = (d1 == NH) ? (hin + sval) * RSQ2 : sval;
+#undef AQ_CW
+#undef AQ_CB
+#undef AQ_CR
+#undef AQ_SW
+#undef AQ_SB
   }
   }
   if (ilive) hl[SM::hoff(3) + ic * 4 + ff] = hreg;
   AQ_SYNC();
   if (reuse && lane < 2 * N + 2) sm[SM::pv + lane] = pvr;   // read by the Gauss-Jordan after the Phi barrier
+  if constexpr (PROP) {
+    // F5's slot table: slot k (pivot step k) holds row r = rec[k]; it records the offsets of
+    // that row's Yt row and of its h^3 row (electron rowsrc[r]) in the half of the
+    // spin-stacked orbital weights that applies (the other half reads the zero row), so that
+    // forming Phi needs no per-row spin selection and no row-table load
+    const int r = (int)pvr;
+    const int src = __shfl(rsl, lane < N ? r : 0);
+    if (lane < 4 * SM::RW) {
+      const bool ok = lane < N;
+      const bool up = r < nup;
+      const int h = SM::hl + SM::hoff(3) + src * 4;
+      int* stab = (int*)(sm + SM::st) + 4 * lane;
+      stab[0] = ok ? SM::yv + r * N : SM::yv;
+      stab[1] = (ok && up) ? h : SM::zr;
+      stab[2] = (ok && !up) ? h : SM::zr;
+      stab[3] = ok ? (up ? 0 : 1) : 2;
+    }
+    if (lane < 4) sm[SM::zr + lane] = T(0);
+    AQ_SYNC();
+  }
 
   AQ_PH(3);
   // ------------------------------------------------------------------ F5 Phi, A = Phi * Yt, Gauss-Jordan -> B = A^{-1}
@@ -788,29 +886,35 @@ k_walker_rev(KArgs ka) {
       using V2 = typename Pair<T>::type;
       const int cc = lane & 15, rg = lane >> 4;
       const T* rec = sm + SM::pv;
+      const int ccl = cc < N ? cc : N - 1;
+      // column ccl of the spin-stacked orbital weights [W_up; W_down] and both biases, loaded
+      // once at compile-time offsets from one lane base
+      V2 w[8], bsp[2];
+      const cptr<T> wcol = P + 2 * ccl;
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        w[s] = pair_make<T>(wcol[Ly::orb_w + s * N * 2], wcol[Ly::orb_w + s * N * 2 + 1]);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        bsp[s] = pair_make<T>(wcol[Ly::orb_b + s * N * 2], wcol[Ly::orb_b + s * N * 2 + 1]);
+      const int* stab = (const int*)(sm + SM::st) + 4 * RW * rg;
       V2 a2[RW];
 #pragma unroll
       for (int t = 0; t < RW; ++t) {
-        const int k = rg * RW + t;
-        T a = T(0), b = T(0);
-        if (k < N && cc < N) {
-          const int r = (int)rec[k];
-          const int src = rowsrc[r];
-          const int sp = r < nup ? 0 : 1;
-          T re = P[Ly::orb_b + (sp * N + cc) * 2 + 0], im = P[Ly::orb_b + (sp * N + cc) * 2 + 1];
+        const int yo = stab[4 * t], hu = stab[4 * t + 1], hd = stab[4 * t + 2], fl = stab[4 * t + 3];
+        V2 acc = fl == 1 ? bsp[1] : bsp[0];
 #pragma unroll
-          for (int f = 0; f < 4; ++f) {
-            const T hv = H3[src * 4 + f];
-            re += hv * P[Ly::orb_w + ((sp * 4 + f) * N + cc) * 2 + 0];
-            im += hv * P[Ly::orb_w + ((sp * 4 + f) * N + cc) * 2 + 1];
-          }
-          Ph[(r * N + cc) * 2 + 0] = re;
-          Ph[(r * N + cc) * 2 + 1] = im;
-          const T y = Yv[r * N + cc];
-          a = re * y;
-          b = im * y;
+        for (int f = 0; f < 4; ++f) acc = pair_fma<T>(sm[hu + f], w[f], acc);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) acc = pair_fma<T>(sm[hd + f], w[4 + f], acc);
+        const bool ok = fl != 2 && cc < N;
+        if (ok) {
+          const int e = yo - SM::yv + cc;   // r N + c
+          Ph[e * 2 + 0] = pair_re<T>(acc);
+          Ph[e * 2 + 1] = pair_im<T>(acc);
         }
-        a2[t] = pair_make<T>(a, b);
+        const T y = ok ? sm[yo + ccl] : T(0);
+        a2[t] = pair_make<T>(pair_re<T>(acc) * y, pair_im<T>(acc) * y);
       }
       if (!AQ_ABL(4)) gj_fixed_regs<T, N>(a2, Mx, lane, rec, logdet, phr, phi, bad);
     } else
@@ -919,6 +1023,27 @@ k_walker_rev(KArgs ka) {
   // lane map of F4: the adjoint of h^{l+1}[i][f] stays in a register.
   T* g2b = sm + SM::g2;    // forward g2 values are dead after F4: reuse for their adjoints
   if (!AQ_ABL(16)) {
+#ifdef AQ_B2_PRELOAD
+    // as in F4: this lane's layer weights (the single layer's rows of the conv outputs this lane
+    // forms, electron ic's conv weights at unit ff), layer l - 1's issued before layer l
+    T bsw[3][SM::QM / 4][4], bcw[3][SM::QM];
+    auto bw_load = [&](int l) {
+      const int d1 = l == 0 ? D0 : NH;
+      const int DF = 3 * d1 + 8;
+      const int Q = DF / 4;
+      const cptr<T> cw = P + (l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2)) + ic * DF;
+      const cptr<T> sw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
+#pragma unroll
+      for (int s4 = 0; s4 < SM::QM / 4; ++s4)
+        if (s4 < Q / 4)
+#pragma unroll
+          for (int m = 0; m < 4; ++m) bsw[l][s4][m] = sw[(4 * s4 + ff) * 4 + m];
+#pragma unroll
+      for (int q = 0; q < SM::QM; ++q)
+        if (q < Q) bcw[l][q] = cw[4 * q + ff];
+    };
+    bw_load(2);
+#endif
     T hb = hbar[SM::hoff(3) + ic * 4 + ff];
 #pragma unroll
     for (int l = 2; l >= 0; --l) {
@@ -928,6 +1053,10 @@ k_walker_rev(KArgs ka) {
       const int T4 = d1 / 4;
       const cptr<T> convw = P + (l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2)) + ic * DF;
       const cptr<T> sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
+#ifdef AQ_B2_PRELOAD
+      if (l > 0) bw_load(l - 1);
+      asm volatile("" ::: "memory");
+#endif
       // single: s = tanh(c Ws + b), h_out = res(h_in, s)
       const T sval = sv[(l * N + ic) * 4 + ff];
       const T sb = (d1 == NH) ? hb * RSQ2 : hb;
@@ -954,7 +1083,13 @@ k_walker_rev(KArgs ka) {
           const int qq = full ? q + ff : q;     // output this lane forms
           T cb = T(0);
 #pragma unroll
-          for (int m = 0; m < 4; ++m) cb += zq[m] * sngw[qq * 4 + m];
+          for (int m = 0; m < 4; ++m) {
+#ifdef AQ_B2_PRELOAD
+            cb += zq[m] * (full ? bsw[l][q / 4][m] : sngw[qq * 4 + m]);
+#else
+            cb += zq[m] * sngw[qq * 4 + m];
+#endif
+          }
           const T c = cqv[SM::cqo(l, ic) + qq];
           const T g = cb * (T(1) - c * c) * T(0.25);
           if constexpr (PREP) {
@@ -979,7 +1114,11 @@ k_walker_rev(KArgs ka) {
       T fb[SM::QM];
 #pragma unroll
       for (int q = 0; q < SM::QM; ++q)
+#ifdef AQ_B2_PRELOAD
+        if (q < Q) fb[q] = cg[q] * bcw[l][q];
+#else
         if (q < Q) fb[q] = cg[q] * convw[4 * q + ff];
+#endif
       // g2 adjoints (inputs 3 d1 + 4G + f), consumed by B3
       if (ilive) {   // pre-scaled by the group-mean weights 1/|G| of the pair sums
         g2b[((l * 2 + 0) * N + ic) * 4 + ff] = fb[3 * T4 + 0] * ginv0;
@@ -1121,37 +1260,49 @@ k_walker_rev(KArgs ka) {
   // from walker pb's cache, so iterations >= 1 skip the forward recompute.
   // one ordered pair (k, i): forward values (fresh) or the cached t1, t2 of walker pb, then the
   // adjoints back through the two double layers to d = x_i - x_k
-  auto pair_adjoint = [&](int k, int i, bool fresh, const T* tcache) {
+  // may_fresh (compile-time after unrolling): the pair may recompute its forward values; fresh
+  // selects them per lane without a branch (a divergent branch here turned the uniform weights
+  // into per-lane copies at the merge)
+  auto pair_adjoint = [&](int k, int i, bool may_fresh, bool fresh, const T* tcache) {
+    // the uniform layer weights are re-read per pair from the scalar cache (s_load) instead of
+    // being kept in SGPRs across the kernel (which spills them through VALU lane writes)
+    cptr<T> Pq = P;
+    asm volatile("" : "+s"(Pq));
     const int G = k >= nup ? 1 : 0;
     T d[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) d[c] = xs[i * 3 + c] - xs[k * 3 + c];
     const T r = f_sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
     T p0[4] = {r, d[0], d[1], d[2]};
-    T t1[4], p1[4], t2[4];
-    if (fresh) {
+    T t1[4], t2[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      t1[o] = tcache ? tcache[o] : T(0);
+      t2[o] = tcache ? tcache[4 + o] : T(0);
+    }
+    if (may_fresh) {
       // recompute the two double layers (values)
+      T f1[4], p1[4], f2[4];
 #pragma unroll
       for (int o = 0; o < 4; ++o) {
-        T s = P[Ly::dbl_b0 + o];
+        T s = Pq[Ly::dbl_b0 + o];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) s += p0[m] * P[Ly::dbl_w0 + m * 4 + o];
-        t1[o] = f_tanh(s);
+        for (int m = 0; m < 4; ++m) s += p0[m] * Pq[Ly::dbl_w0 + m * 4 + o];
+        f1[o] = f_tanh(s);
       }
 #pragma unroll
-      for (int o = 0; o < 4; ++o) p1[o] = (p0[o] + t1[o]) * RSQ2;
+      for (int o = 0; o < 4; ++o) p1[o] = (p0[o] + f1[o]) * RSQ2;
 #pragma unroll
       for (int o = 0; o < 4; ++o) {
-        T s = P[Ly::dbl_b1 + o];
+        T s = Pq[Ly::dbl_b1 + o];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) s += p1[m] * P[Ly::dbl_w1 + m * 4 + o];
-        t2[o] = f_tanh(s);
+        for (int m = 0; m < 4; ++m) s += p1[m] * Pq[Ly::dbl_w1 + m * 4 + o];
+        f2[o] = f_tanh(s);
       }
-    } else {
 #pragma unroll
       for (int o = 0; o < 4; ++o) {
-        t1[o] = tcache[o];
-        t2[o] = tcache[4 + o];
+        t1[o] = fresh ? f1[o] : t1[o];
+        t2[o] = fresh ? f2[o] : t2[o];
       }
     }
     // adjoints: output of layer l feeds g2[l][G][i] with weight 1/|G|
@@ -1165,7 +1316,7 @@ k_walker_rev(KArgs ka) {
     for (int m = 0; m < 4; ++m) {
       T s = g2b[((1 * 2 + G) * N + i) * 4 + m] + pb2[m] * RSQ2;
 #pragma unroll
-      for (int o = 0; o < 4; ++o) s += z2[o] * P[Ly::dbl_w1 + m * 4 + o];
+      for (int o = 0; o < 4; ++o) s += z2[o] * Pq[Ly::dbl_w1 + m * 4 + o];
       pb1[m] = s;
     }
     T z1[4];
@@ -1175,13 +1326,13 @@ k_walker_rev(KArgs ka) {
     for (int m = 0; m < 4; ++m) {
       T s = g2b[((0 * 2 + G) * N + i) * 4 + m] + pb1[m] * RSQ2;
 #pragma unroll
-      for (int o = 0; o < 4; ++o) s += z1[o] * P[Ly::dbl_w0 + m * 4 + o];
+      for (int o = 0; o < 4; ++o) s += z1[o] * Pq[Ly::dbl_w0 + m * 4 + o];
       pb0[m] = s;
     }
     // p0 = [r, d]; Pade e-e Jastrow once per unordered pair (k < i)
     T rb = pb0[0];
     if (k < i) {
-      const T cusp = P[Ly::jee_c + k * N + i], al = P[Ly::jee_a + k * N + i];
+      const T cusp = Pq[Ly::jee_c + k * N + i], al = Pq[Ly::jee_a + k * N + i];
       const T den = al * r + T(1);
       rb += cusp * f_rcp(den * den);
     }
@@ -1219,22 +1370,21 @@ k_walker_rev(KArgs ka) {
       }
       pk[u] = k;
       pi2[u] = i;
-      if (u > 0 || it >= M) {
-        const T* tp = Wc + WC::pt + (k * N + i) * 8;
+      // loaded on every lane (the fresh pairs of iteration 0 select their own values)
+      const T* tp = Wc + WC::pt + (k * N + i) * 8;
 #pragma unroll
-        for (int o = 0; o < 8; ++o) tc[u][o] = tp[o];
-      }
+      for (int o = 0; o < 8; ++o) tc[u][o] = tp[o];
     }
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
       const int it = lane + 64 * u;
-      if (it < NPR) pair_adjoint(pk[u], pi2[u], u == 0 && it < M, tc[u]);
+      if (it < NPR) pair_adjoint(pk[u], pi2[u], u == 0, u == 0 && it < M, tc[u]);
     }
   } else if (!reuse) {
     for (int it = lane; it < NPR; it += 64) {
       const int k = it / (N - 1);
       const int jj = it - k * (N - 1);
-      pair_adjoint(k, jj + (jj >= k ? 1 : 0), true, nullptr);
+      pair_adjoint(k, jj + (jj >= k ? 1 : 0), true, true, nullptr);
     }
   }
   AQ_SYNC();
@@ -1269,13 +1419,14 @@ k_walker_rev(KArgs ka) {
   const T gd = dir ? g : T(0);
   const T sumsq = wave_sum(gd * gd);
   const T lpsi = logdet + wave_sum(jv + jve);
-  if (ka.grad && dir) ((T*)ka.grad)[(size_t)conf * 3 * N + 3 * le + lc] = g;
-  if (ka.gown && dir && le == pi) ((T*)ka.gown)[(size_t)conf * 3 + lc] = g;
+  const auto* kl = late_args();
+  if (kl->grad && dir) ((T*)kl->grad)[(size_t)conf * 3 * N + 3 * le + lc] = g;
+  if (kl->gown && dir && le == pi) ((T*)kl->gown)[(size_t)conf * 3 + lc] = g;
   if (lane == 0) {
-    if (ka.logabs) ((T*)ka.logabs)[conf] = lpsi;
-    if (ka.phase) ((T*)ka.phase)[conf] = f_atan2(phi, phr);
-    if (ka.sumsq) ((T*)ka.sumsq)[conf] = sumsq;
-    if (ka.tacc) tacc_add(ka.tacc, isprop ? 1 : 0, conf, (double)sumsq);
+    if (kl->logabs) ((T*)kl->logabs)[conf] = lpsi;
+    if (kl->phase) ((T*)kl->phase)[conf] = f_atan2(phi, phr);
+    if (kl->sumsq) ((T*)kl->sumsq)[conf] = sumsq;
+    if (kl->tacc) tacc_add(kl->tacc, isprop ? 1 : 0, conf, (double)sumsq);
   }
   if constexpr (!PREP) {
     if (ka.dg1 && !isprop && lane < N) {   // the sweep's draws of walker conf (k_draws)
