@@ -203,6 +203,43 @@ __device__ __forceinline__ const __attribute__((address_space(4))) KArgs* late_a
   return p;
 }
 
+// Proposal B3's pair order (k, i) per moved electron pi and pair slot it = lane + 64 u: the
+// 2(N-1) pairs of pi first (it < M), then the others in row-major order; slots past N(N-1)
+// repeat the last pair.  Code = k | i << 4 | (k N + i) << 8 (the pair's walker-cache row).
+template <int N> struct PairTab {
+  static constexpr int M = 2 * (N - 1), NPR = N * (N - 1), NS = ((NPR + 63) / 64) * 64;
+  unsigned short v[N][NS];
+  constexpr PairTab() : v{} {
+    for (int pi = 0; pi < N; ++pi)
+      for (int it = 0; it < NS; ++it) {
+        int k = 0, i = 0;
+        if (it < M) {
+          const int j = it < N - 1 ? it : it - (N - 1);
+          const int o = j + (j >= pi ? 1 : 0);
+          k = it < N - 1 ? pi : o;
+          i = it < N - 1 ? o : pi;
+        } else if (N > 2) {
+          const int uu = (it < NPR ? it : NPR - 1) - M;
+          const int kk = uu / (N - 2);
+          const int jj = uu - kk * (N - 2);
+          const int ii = jj + (jj >= kk ? 1 : 0);
+          k = kk + (kk >= pi ? 1 : 0);
+          i = ii + (ii >= pi ? 1 : 0);
+        }
+        v[pi][it] = (unsigned short)(k | (i << 4) | ((k * N + i) << 8));
+      }
+  }
+};
+template <int N> __constant__ PairTab<N> pair_tab{};
+
+// c ? x : +0 as a bit mask (no select of a loaded value: see the F1 cache loads)
+__device__ __forceinline__ float and_zero(bool c, float x) {
+  return __builtin_bit_cast(float, __builtin_bit_cast(unsigned, x) & (c ? ~0u : 0u));
+}
+__device__ __forceinline__ double and_zero(bool c, double x) {
+  return __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, x) & (c ? ~0ull : 0ull));
+}
+
 // Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2):
 // give every XCD a contiguous range of configurations, so the N proposals of a
 // walker (and that walker's cache) land on one L2.
@@ -441,7 +478,10 @@ k_walker_rev(KArgs ka) {
   // Walker cache: read (proposal with reuse: this proposal's walker pb) or written (by conf).
   using WC = WCache<N, A>;
   using EC = ECache<N, A>;
-    const bool reuse = !PREP && isprop && (PROP || ka.ecache != nullptr);
+  // shape.hip launches every proposal that reads the walker cache with the PROP instantiation, so
+  // the cached path is compiled there only (the general one serves walker launches, reuse-off
+  // proposals and plain value+gradient calls)
+  const bool reuse = !PREP && PROP;
   T* Wc = (T*)ka.wcache + (size_t)(reuse ? pb : conf) * WC::size;
   T* Lw = PREP ? (T*)ka.lapcache + (size_t)conf * LCc::size : nullptr;
   const T* Eq = reuse ? (const T*)ka.ecache + (size_t)conf * EC::size : nullptr;
@@ -450,6 +490,40 @@ k_walker_rev(KArgs ka) {
   T jv = T(0), jd1 = T(0), jve = T(0);
   T pvr = T(0);
   int rsl = 0;   // PROP: rowsrc[lane]
+  T jvp = T(0);  // F2's Jastrow terms of the moved electron's pairs
+  // F2 of a proposal, first half: the 2(N-1) pairs of the moved electron pi, lane = 16 part + o:
+  // part 0/1: pair (pi, o) at the new/old x_pi (column o); part 2/3: pair (o, pi) (column pi);
+  // their stream values to S [64][12], the e-e Jastrow change to jvp
+  auto f2_pair_values = [&](T cusp, T al) {   // PROP: the pair's Jastrow parameters, loaded early
+    T* S = sm + SM::R + 4;
+    const T* xo = sm + SM::R;                       // old position of pi
+    const int o = lane & 15, part = lane >> 4;
+    const int os = o < N ? o : N - 1;
+    const T* xp = (part & 1) ? xo : xs + pi * 3;
+    T d[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) d[c] = (part < 2) ? xs[os * 3 + c] - xp[c] : xp[c] - xs[os * 3 + c];
+    T v[3][4];
+    pair_values<T, N, A>(d, P, v);
+#pragma unroll
+    for (int l = 0; l < 3; ++l)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) S[lane * 12 + l * 4 + f] = v[l][f];
+    if (part < 2 && o < N && o != pi) {
+      if constexpr (!PROP) {
+        cusp = P[Ly::jee_c + pi * N + o];
+        al = P[Ly::jee_a + pi * N + o];
+      }
+      const T je = f_div(cusp * v[0][0], al * v[0][0] + T(1));
+      jvp += part == 0 ? je : -je;
+    }
+  };
+  // the Jastrow parameters of pair (pi, o) of this lane (o = lane & 15, clamped)
+  auto jee_params = [&](T& cusp, T& al) {
+    const int os = (lane & 15) < N ? (lane & 15) : N - 1;
+    cusp = P[Ly::jee_c + pi * N + os];
+    al = P[Ly::jee_a + pi * N + os];
+  };
   if (reuse) {
     // walker pb's cached stage and pair sums, electron pi's entries from k_moved_electron;
     // all loads issued before the first LDS store
@@ -460,11 +534,12 @@ k_walker_rev(KArgs ka) {
     // Every load is issued unconditionally at a clamped, in-bounds index and the moved electron's
     // entries are selected afterwards: no divergent branch (exec-mask save/restore) per element.
     const bool mvl = lane < 3 * N && lane / 3 == pi;
-    T x0 = T(0), xm = T(0);
+    T x0 = T(0), xm = T(0), jc = T(0), ja = T(0);
     if constexpr (PROP) {
       const int l3 = lane < 3 * N ? lane : 3 * N - 1;
       x0 = ((const T*)ka.pos)[(size_t)pb * 3 * N + l3];
       xm = Eq[EC::xp + (mvl ? lane - 3 * pi : 0)];
+      jee_params(jc, ja);   // before the cache loads: F2's pair values wait for these only
       rsl = rowsrc[lane < N ? lane : N - 1];   // F5's slot table (after F4)
     }
     // unsigned offsets: the loads take the wave's base pointer in SGPRs plus a 32-bit lane offset
@@ -490,17 +565,32 @@ k_walker_rev(KArgs ka) {
       rg[t] = Wc[WC::g2 + (idx < 3 * 2 * N * 4 ? idx : 3 * 2 * N * 4 - 1)];
     }
     {
-      const T a = Wc[WC::jaev + le], b = Eq[EC::jv];
-      jv = (val && live) ? ((er == pi) ? b : a) : T(0);
-      const T a1 = Wc[WC::jaed + (lane < 48 ? lane : 47)], b1 = Eq[EC::jd + (lc < 3 ? lc : 0)];
-      jd1 = dir ? ((le == pi) ? b1 : a1) : T(0);
-      const T a2 = Wc[WC::jee];
-      jve = lane == 0 ? a2 : T(0);
+      // one load per value from a selected address, masked to +0 by a bit and: a select between
+      // two loaded values (or a loaded value and 0) is turned into a branch around the loads by
+      // the compiler, and the branch waits for every load issued so far
+      if constexpr (PROP) {
+        const T* js = (er == pi) ? Eq + EC::jv : Wc + WC::jaev + le;
+        jv = and_zero(val && live, *js);
+        const T* ds = (le == pi) ? Eq + EC::jd + (lc < 3 ? lc : 0) : Wc + WC::jaed + (lane < 48 ? lane : 47);
+        jd1 = and_zero(dir, *ds);
+        jve = and_zero(lane == 0, Wc[WC::jee]);
+      } else {
+        const T a = Wc[WC::jaev + le], b = Eq[EC::jv];
+        jv = (val && live) ? ((er == pi) ? b : a) : T(0);
+        const T a1 = Wc[WC::jaed + (lane < 48 ? lane : 47)], b1 = Eq[EC::jd + (lc < 3 ? lc : 0)];
+        jd1 = dir ? ((le == pi) ? b1 : a1) : T(0);
+        const T a2 = Wc[WC::jee];
+        jve = lane == 0 ? a2 : T(0);
+      }
       pvr = Wc[WC::pv + (lane < 2 * N + 2 ? lane : 2 * N + 1)];   // to LDS after F4 (SmemRev::pv)
     }
     if constexpr (PROP) {
       if (mvl) sm[SM::R + (lane - 3 * pi)] = x0;             // old position of the moved electron
       if (lane < 3 * N) xs[lane] = mvl ? xm : x0;
+      // F2's pair values of the moved electron need the positions only: computed while the
+      // cache loads above are still in flight (they are waited for at the LDS stores below)
+      AQ_SYNC();
+      f2_pair_values(jc, ja);
     }
 #pragma unroll
     for (int t = 0; t < NY; ++t)
@@ -551,27 +641,11 @@ k_walker_rev(KArgs ka) {
     // patch walker pb's sums with the 2(N-1) pairs of the moved electron pi. lane = 16*part + o:
     // part 0/1: pair (pi, o) at the new/old x_pi (column o); part 2/3: pair (o, pi) (column pi)
     T* S = sm + SM::R + 4;                          // [64][12] pair-stream values
-    const T* xo = sm + SM::R;                       // old position of pi
-    {
-      const int o = lane & 15, part = lane >> 4;
-      const int os = o < N ? o : N - 1;
-      const T* xp = (part & 1) ? xo : xs + pi * 3;
-      T d[3];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) d[c] = (part < 2) ? xs[os * 3 + c] - xp[c] : xp[c] - xs[os * 3 + c];
-      T v[3][4];
-      pair_values<T, N, A>(d, P, v);
-#pragma unroll
-      for (int l = 0; l < 3; ++l)
-#pragma unroll
-        for (int f = 0; f < 4; ++f) S[lane * 12 + l * 4 + f] = v[l][f];
-      if (part < 2 && o < N && o != pi) {
-        const T cusp = P[Ly::jee_c + pi * N + o], al = P[Ly::jee_a + pi * N + o];
-        const T je = f_div(cusp * v[0][0], al * v[0][0] + T(1));
-        jve += part == 0 ? je : -je;
-      }
+    if constexpr (!PROP) {                          // PROP: done during the cache loads (F1)
+      f2_pair_values(T(0), T(0));
+      AQ_SYNC();
     }
-    AQ_SYNC();
+    jve += jvp;
     if (lane < 16) {
       if (lane < N && lane != pi) {
         const int Gp = pi >= nup ? 1 : 0;
@@ -587,8 +661,13 @@ k_walker_rev(KArgs ka) {
       const int l = t >> 3, G = (t >> 2) & 1, f = t & 3;
       const int k0 = G ? nup : 0, k1 = G ? N : nup;
       T acc = T(0);
-      for (int k = k0; k < k1; ++k)
-        if (k != pi) acc += S[(32 + k) * 12 + l * 4 + f] - S[(48 + k) * 12 + l * 4 + f];
+      // unrolled over every k with the group and pi masked out (+0), so that the LDS reads are
+      // issued together instead of one dependent round trip per electron of the group
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        const T dv = S[(32 + k) * 12 + l * 4 + f] - S[(48 + k) * 12 + l * 4 + f];
+        acc += (k >= k0 && k < k1 && k != pi) ? dv : T(0);
+      }
       g2[((l * 2 + G) * N + pi) * 4 + f] += acc * (G ? ginv1 : ginv0);
     }
   } else if (!reuse) {
@@ -1353,25 +1432,13 @@ k_walker_rev(KArgs ka) {
     int pk[NIT], pi2[NIT];
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
-      const int it = lane + 64 * u;
-      int k = 0, i = 0;
-      if (it < M) {
-        const int j = it < N - 1 ? it : it - (N - 1);
-        const int o = j + (j >= pi ? 1 : 0);
-        k = it < N - 1 ? pi : o;
-        i = it < N - 1 ? o : pi;
-      } else if constexpr (N > 2) {
-        const int uu = (it < NPR ? it : NPR - 1) - M;
-        const int kk = uu / (N - 2);
-        const int jj = uu - kk * (N - 2);
-        const int ii = jj + (jj >= kk ? 1 : 0);
-        k = kk + (kk >= pi ? 1 : 0);
-        i = ii + (ii >= pi ? 1 : 0);
-      }
+      // pair (k, i) of this slot from the constant table (PairTab)
+      const unsigned code = pair_tab<N>.v[pi][lane + 64 * u];
+      const int k = code & 15, i = (code >> 4) & 15;
       pk[u] = k;
       pi2[u] = i;
       // loaded on every lane (the fresh pairs of iteration 0 select their own values)
-      const T* tp = Wc + WC::pt + (k * N + i) * 8;
+      const T* tp = Wc + WC::pt + (code >> 8) * 8;
 #pragma unroll
       for (int o = 0; o < 8; ++o) tc[u][o] = tp[o];
     }
