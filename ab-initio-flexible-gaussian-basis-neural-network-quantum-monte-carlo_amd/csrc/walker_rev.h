@@ -762,6 +762,18 @@ k_walker_rev(KArgs ka) {
   const int ic = ilive ? fi : N - 1;
   const bool inG1 = ic >= nup;
   T hreg = T(0);
+  // PROP: F5's orbital-weight column (lane column ccl of the spin-stacked [W_up; W_down] and both
+  // biases), issued during F4's last layer so that F5 finds it loaded
+  using V2o = typename Pair<T>::type;
+  V2o ow[8], obs[2];
+  auto orb_load = [&]() {
+    const int cl = (lane & 15) < N ? (lane & 15) : N - 1;
+    const cptr<T> wcol = P + 2 * cl;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) ow[s] = pair_make<T>(wcol[Ly::orb_w + s * N * 2], wcol[Ly::orb_w + s * N * 2 + 1]);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) obs[s] = pair_make<T>(wcol[Ly::orb_b + s * N * 2], wcol[Ly::orb_b + s * N * 2 + 1]);
+  };
   if (!AQ_ABL(2)) {
 #ifndef AQ_F4_NO_PRELOAD
   // this lane's layer weights (electron ic's conv weights and biases at unit ff, the single
@@ -805,6 +817,11 @@ k_walker_rev(KArgs ka) {
     const cptr<T> sngb = P + (l == 0 ? Ly::sng_b0 : (l == 1 ? Ly::sng_b1 : Ly::sng_b2));
 #ifndef AQ_F4_NO_PRELOAD
     if (l + 1 < 3) lw_load(l + 1);
+#ifndef AQ_F5_NO_PRELOAD
+    if constexpr (PROP) {
+      if (l == 2) orb_load();
+    }
+#endif
     asm volatile("" ::: "memory");
 #define AQ_CW(q) wcv[l][q]
 #define AQ_CB(s4) wcb[l][s4]
@@ -968,14 +985,11 @@ k_walker_rev(KArgs ka) {
       const int ccl = cc < N ? cc : N - 1;
       // column ccl of the spin-stacked orbital weights [W_up; W_down] and both biases, loaded
       // once at compile-time offsets from one lane base
-      V2 w[8], bsp[2];
-      const cptr<T> wcol = P + 2 * ccl;
-#pragma unroll
-      for (int s = 0; s < 8; ++s)
-        w[s] = pair_make<T>(wcol[Ly::orb_w + s * N * 2], wcol[Ly::orb_w + s * N * 2 + 1]);
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        bsp[s] = pair_make<T>(wcol[Ly::orb_b + s * N * 2], wcol[Ly::orb_b + s * N * 2 + 1]);
+#if defined(AQ_F5_NO_PRELOAD) || defined(AQ_F4_NO_PRELOAD)
+      orb_load();
+#endif
+      const V2* w = ow;
+      const V2* bsp = obs;
       const int* stab = (const int*)(sm + SM::st) + 4 * RW * rg;
       V2 a2[RW];
 #pragma unroll
