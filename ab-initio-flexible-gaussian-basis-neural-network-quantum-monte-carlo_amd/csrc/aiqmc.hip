@@ -68,6 +68,43 @@ __global__ __launch_bounds__(1024) void k_taueff(const T* __restrict__ x, int n,
   }
 }
 
+// fp32 limdrift reduction of an unfused sweep (batches above FUSE_REDUCE_MAX_B): TAUEFF_NB
+// workgroups, every element entering as tacc_fix(x) -- the fused accumulators' arithmetic, so the
+// factor is bit-for-bit the one the fused path derives, in any arrival order.  Each workgroup adds
+// its exact integer partial to acc[0]; the last one to finish (acc[1] counts them) forms taueff from
+// the total and clears acc for the next launch in stream order.  A single 1024-thread workgroup
+// (k_taueff) took 4.6 us for the N2 proposal batch.
+constexpr int TAUEFF_NB = 32;
+__global__ __launch_bounds__(256) void k_taueff_wide(const float* __restrict__ x, int n, double tstep, double* out,
+                                                     unsigned long long* acc) {
+  __shared__ unsigned long long ws[4];
+  unsigned long long v = 0;
+  const int stride = TAUEFF_NB * 256;
+  int i = blockIdx.x * 256 + (int)threadIdx.x;
+  for (; i + 7 * stride < n; i += 8 * stride) {
+    float t[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t[k] = x[i + k * stride];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v += tacc_fix((double)t[k]);
+  }
+  for (; i < n; i += stride) v += tacc_fix((double)x[i]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(acc, (ws[0] + ws[1]) + (ws[2] + ws[3]));
+    __threadfence();
+    if (atomicAdd(acc + 1, 1ull) == TAUEFF_NB - 1) {
+      const unsigned long long tot = atomicAdd(acc, 0ull);
+      *out = (double)taueff_from_v2<float>((double)tot * (1.0 / TACC_SCALE), tstep);
+      atomicExch(acc, 0ull);
+      atomicExch(acc + 1, 0ull);
+    }
+  }
+}
+
 // Per-sweep random draws (production mode), one thread per (walker b, electron i):
 // gauss1[b][3i..3i+2], gauss2[b][i][0..2] standard normals, u[b][i] in [0,1) --
 // the same buffers the caller supplies in AIQMC_RNG_HOST mode.
@@ -364,7 +401,9 @@ static int ensure_ws(aiqmc_ctx* c, int B) {
     HIPCHK(hipMalloc(ptrs[k], bytes[k]));
     tot += (int64_t)bytes[k];
   }
-  HIPCHK(hipMalloc((void**)&c->d_taueff, 2 * sizeof(double)));
+  // [2] limdrift factors, then k_taueff_wide's two (sum, count) accumulator pairs, zeroed once
+  HIPCHK(hipMalloc((void**)&c->d_taueff, 6 * sizeof(double)));
+  HIPCHK(hipMemset(c->d_taueff + 2, 0, 4 * sizeof(double)));
 
   c->ws_B = B;
   c->ws_bytes = tot + 16;
@@ -761,7 +800,10 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
   timed(c, 1, s, [&] { ops.walker(c->dtype, MODE_GRAD, ka, B, s); });
   // (2) limdrift factor over the device batch (:60) -- fused: summed by the walker launch
   if (!tacc) {
-    if (c->dtype == AIQMC_F32)
+    if (c->dtype == AIQMC_F32 && !dmc && c->wide_reduce)
+      k_taueff_wide<<<dim3(TAUEFF_NB), dim3(256), 0, s>>>((const float*)c->d_sq, B, tstep, c->d_taueff,
+                                                         (unsigned long long*)(c->d_taueff + 2));
+    else if (c->dtype == AIQMC_F32)
       k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)c->d_sq, B, tstep, c->d_taueff);
     else
       k_taueff<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)c->d_sq, B, tstep, c->d_taueff);
@@ -794,7 +836,10 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
   // (4) limdrift factor of the proposal gradients over all B*N*3N entries (:80) -- fused:
   // summed by the proposal launch
   if (!tacc) {
-    if (c->dtype == AIQMC_F32)
+    if (c->dtype == AIQMC_F32 && !dmc && c->wide_reduce)
+      k_taueff_wide<<<dim3(TAUEFF_NB), dim3(256), 0, s>>>((const float*)c->d_sqn, B * N, tstep, c->d_taueff + 1,
+                                                         (unsigned long long*)(c->d_taueff + 4));
+    else if (c->dtype == AIQMC_F32)
       k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)c->d_sqn, B * N, tstep,
                          c->d_taueff + 1);
     else
@@ -1395,8 +1440,9 @@ int aiqmc_debug_set_fuse_accept(aiqmc_ctx* c, int32_t on) {
 
 int aiqmc_debug_set_fuse_reduce(aiqmc_ctx* c, int32_t on) {
   if (!c) return fail(AIQMC_EINVAL, "null context");
-  if (on < 0 || on > 2) return fail(AIQMC_EINVAL, "fuse_reduce must be 0, 1 or 2");
-  c->fuse_reduce = on;
+  if (on < 0 || on > 3) return fail(AIQMC_EINVAL, "fuse_reduce must be 0, 1, 2 or 3");
+  c->fuse_reduce = on == 3 ? 0 : on;
+  c->wide_reduce = on == 3 ? 0 : 1;
   return AIQMC_OK;
 }
 

@@ -265,8 +265,10 @@ int aiqmc_debug_set_fuse_accept(aiqmc_ctx* ctx, int32_t on);
  * (|grad|^2 over the walkers, over the proposals; VMCmcstep.py:11-14) inside the walker and
  * proposal launches, as exact 64-bit integer sums of |grad|^2 in units of 2^-16: no reduction
  * launches, and the same bits in any arrival order.  mode 1 (default) = for batches of at most
- * 1,024 walkers (where it is faster), 2 = always, 0 = never (the k_taueff reduction launches;
- * fp64 always uses them).  Results agree to the float rounding of v2. */
+ * 1,024 walkers (where it is faster), 2 = always, 0 = never: reduction launches that sum the same
+ * integers in 32 workgroups (k_taueff_wide; the same bits as the fused sums), 3 = never, with the
+ * single-workgroup fp64 tree sum (k_taueff; fp64 always uses it; results agree with the integer
+ * sums to the float rounding of v2). */
 int aiqmc_debug_set_fuse_reduce(aiqmc_ctx* ctx, int32_t on);
 
 /* Development builds (-DAQ_ABLATE) only: skip proposal-kernel phases (bit mask, walker_rev.h) to

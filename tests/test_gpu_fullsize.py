@@ -278,11 +278,12 @@ def test_small_n_packed_proposals_match_one_wave_path(name, dtype):
 def test_fused_limdrift_reduction_matches_reduction_launches(name):
     """fp32 mc_step sums the two limdrift reductions of a sweep (VMCmcstep.py:11-14) inside the
     walker and proposal launches as exact integer accumulations (walker_kernel.h TACC_SCALE)
-    instead of two k_taueff launches.  The integer sum is order independent: repeated runs are
-    bitwise equal.  Against the reduction launches (fp64 tree sum) the limdrift factor differs
-    only in the float rounding of v2, so the positions agree to rounding, with at most a rare
-    acceptance flip (a ratio within ~1e-6 of its uniform).  Be runs the 4-configurations-per-wave
-    proposal kernel (quad_small.h), N2 k_walker_rev."""
+    instead of two reduction launches.  The integer sum is order independent: repeated runs are
+    bitwise equal, and so is the unfused path, whose reduction launches (k_taueff_wide) sum the
+    same integers.  Against the fp64 tree-sum launch (k_taueff, mode 3) the limdrift factor
+    differs only in the float rounding of v2, so the positions agree to rounding, with at most a
+    rare acceptance flip (a ratio within ~1e-6 of its uniform).  Be runs the
+    4-configurations-per-wave proposal kernel (quad_small.h), N2 k_walker_rev."""
     s, ctx = _ctx(name, torch.float32)
     B, NS, N = 4096, 4, s.nelectrons
     x0 = torch.tensor(_walkers(s, B, seed=21), dtype=torch.float32, device="cuda")
@@ -290,15 +291,18 @@ def test_fused_limdrift_reduction_matches_reduction_launches(name):
     kw = dict(gauss1=torch.randn(NS, B, 3 * N, generator=g, dtype=torch.float64),
               gauss2=torch.randn(NS, B, N, 3, generator=g, dtype=torch.float64),
               u=torch.rand(NS, B, N, generator=g, dtype=torch.float64))
-    a, a2, b = (x0.clone().contiguous() for _ in range(3))
+    a, a2, w, b = (x0.clone().contiguous() for _ in range(4))
     ctx.set_fuse_reduce(2)          # fused at any batch size (default: B <= 1,024 only)
     acc_a = ctx.mc_step(a, NS, 0.05, count_accepts=True, **kw)
     ctx.mc_step(a2, NS, 0.05, **kw)
-    ctx.set_fuse_reduce(0)
+    ctx.set_fuse_reduce(0)          # integer reduction launches
+    ctx.mc_step(w, NS, 0.05, **kw)
+    ctx.set_fuse_reduce(3)          # fp64 tree-sum launch
     acc_b = ctx.mc_step(b, NS, 0.05, count_accepts=True, **kw)
     ctx.set_fuse_reduce(1)
     torch.cuda.synchronize()
     assert torch.equal(a, a2)
+    assert torch.equal(a, w)
     d = (a - b).abs().reshape(B, -1).amax(1)
     flips = int((acc_a != acc_b).sum())
     assert flips <= B // 200, flips

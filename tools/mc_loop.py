@@ -15,7 +15,7 @@ ctx = s.context(dtype=torch.float32)
 ctx.set_params(flatten_params(s.make_network().init(1)))
 if os.environ.get("AIQMC_NOFUSE"):
     ctx.set_fuse_accept(False)
-if os.environ.get("AIQMC_FUSE_REDUCE"):     # 0: k_taueff launches, 1: by batch size (default), 2: integer atomics
+if os.environ.get("AIQMC_FUSE_REDUCE"):     # 0: integer reduction launches, 1: by batch size (default), 2: integer atomics, 3: fp64 k_taueff launches
     ctx.set_fuse_reduce(int(os.environ["AIQMC_FUSE_REDUCE"]))
 if os.environ.get("AIQMC_LAPW"):      # waves per walker of the local energy's second launch
     ctx.set_lap_waves(int(os.environ["AIQMC_LAPW"]))
