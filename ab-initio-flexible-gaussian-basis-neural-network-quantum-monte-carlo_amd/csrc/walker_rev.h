@@ -1462,10 +1462,23 @@ k_walker_rev(KArgs ka) {
       if (it < NPR) pair_adjoint(pk[u], pi2[u], u == 0, u == 0 && it < M, tc[u]);
     }
   } else if (!reuse) {
-    for (int it = lane; it < NPR; it += 64) {
-      const int k = it / (N - 1);
-      const int jj = it - k * (N - 1);
-      pair_adjoint(k, jj + (jj >= k ? 1 : 0), true, true, nullptr);
+    if (!PREP && !isprop && ka.wcache) {
+      // walker launch of a sweep: F2 has just written every pair's tanh outputs to the walker
+      // cache; read them back instead of recomputing the two double layers
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      for (int it = lane; it < NPR; it += 64) {
+        const int k = it / (N - 1);
+        const int jj = it - k * (N - 1);
+        const int i = jj + (jj >= k ? 1 : 0);
+        pair_adjoint(k, i, false, false, Wc + WC::pt + (k * N + i) * 8);
+      }
+    } else {
+      for (int it = lane; it < NPR; it += 64) {
+        const int k = it / (N - 1);
+        const int jj = it - k * (N - 1);
+        pair_adjoint(k, jj + (jj >= k ? 1 : 0), true, true, nullptr);
+      }
     }
   }
   AQ_SYNC();
@@ -1510,18 +1523,19 @@ k_walker_rev(KArgs ka) {
     if (kl->tacc) tacc_add(kl->tacc, isprop ? 1 : 0, conf, (double)sumsq);
   }
   if constexpr (!PREP) {
-    if (ka.dg1 && !isprop && lane < N) {   // the sweep's draws of walker conf (k_draws)
+    if (kl->dg1 && !isprop && lane < N) {   // the sweep's draws of walker conf (k_draws)
       const uint32_t t = (uint32_t)(conf * N + lane);
+      const uint64_t seed = kl->seed, step = kl->step;
       float a[3], b[3], c[4];
-      philox_normal3f(ka.seed, ka.step, t, 0u, a);
-      philox_normal3f(ka.seed, ka.step, t, 1u, b);
-      philox_u4(ka.seed, ka.step, t, 2u, c);
+      philox_normal3f(seed, step, t, 0u, a);
+      philox_normal3f(seed, step, t, 1u, b);
+      philox_u4(seed, step, t, 2u, c);
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        ((T*)ka.dg1)[(size_t)t * 3 + k] = (T)a[k];
-        ((T*)ka.dg2)[(size_t)t * 3 + k] = (T)b[k];
+        ((T*)kl->dg1)[(size_t)t * 3 + k] = (T)a[k];
+        ((T*)kl->dg2)[(size_t)t * 3 + k] = (T)b[k];
       }
-      ((T*)ka.du)[t] = (T)(c[0] - 5.9604644775390625e-08f);
+      ((T*)kl->du)[t] = (T)(c[0] - 5.9604644775390625e-08f);
     }
   }
   AQ_PH(9);
