@@ -1061,7 +1061,13 @@ k_walker_rev(KArgs ka) {
   // ------------------------------------------------------------------ B1 adjoints of H (= h^3) and Yt
   T* hbar = sm + SM::hbar;
   T* ybar = sm + SM::ybar;
-  if (lane < 4 * N && !AQ_ABL(8)) {
+#ifndef AQ_PREP_NO_MFMA
+  // fp32 adjoint pass of the local energy: Q_f on the matrix cores (below), B1 from its diagonal
+  constexpr bool q_mfma = PREP && sizeof(T) == 4 && NH == 4;
+#else
+  constexpr bool q_mfma = false;
+#endif
+  if (!q_mfma && lane < 4 * N && !AQ_ABL(8)) {
     const int r = lane >> 2, f = lane & 3;
     const int sp = r < nup ? 0 : 1;
     T q = T(0), q1 = T(0);   // even / odd c: two independent chains
@@ -1082,6 +1088,62 @@ k_walker_rev(KArgs ka) {
       Lw[LCc::bm + idx] = Mx[idx];
       Lw[LCc::ph + idx] = Ph[idx];
     }
+    if constexpr (q_mfma) {
+      // Q_f = U B, U[(r, f), c] = W_{s(r)}[f, c] Yt[r, c]: a (4N x N)(N x N) complex product on
+      // v_mfma_f32_16x16x4f32 (nn.py:449-485's orbital matmul): M-tiles over the rows (r, f),
+      // K-steps of four columns c, one N-tile s.  A fragment: lane (k = lane >> 4, row e =
+      // lane & 15); B fragment: lane (k, column e); accumulator v of lane group k: row 4k + v.
+      // Replaces a VALU loop of N^3 complex MACs with two global weight loads and an LDS read
+      // of Yt per MAC.  B1's H adjoint is Re Q_f[r, r] (the diagonal), written from here.
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      constexpr int NM = (4 * N + 15) / 16, NK = (N + 3) / 4;
+      const int kq = lane >> 4, e = lane & 15, fq = lane & 3;
+      float bre[NK], bim[NK], wr[2][NK], wi[2][NK];
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        const int c = 4 * kk + kq;
+        const bool bok = c < N && e < N;
+        const int cl = c < N ? c : N - 1, el = e < N ? e : N - 1;
+        bre[kk] = bok ? (float)BRE(cl, el) : 0.f;
+        bim[kk] = bok ? (float)BIM(cl, el) : 0.f;
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+          const float a = P[Ly::orb_w + ((sp * 4 + fq) * N + cl) * 2], b = P[Ly::orb_w + ((sp * 4 + fq) * N + cl) * 2 + 1];
+          wr[sp][kk] = c < N ? a : 0.f;
+          wi[sp][kk] = c < N ? b : 0.f;
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        const int r = 4 * m + (e >> 2);            // A row 16 m + e = (r, f = e & 3)
+        const bool rok = r < N;
+        const bool up = r < nup;
+        v4f qre = {0.f, 0.f, 0.f, 0.f}, qim = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+          const int c = 4 * kk + kq;
+          const float y = (rok && c < N) ? (float)Yv[(rok ? r : 0) * N + (c < N ? c : 0)] : 0.f;
+          const float ur = (up ? wr[0][kk] : wr[1][kk]) * y, ui = (up ? wi[0][kk] : wi[1][kk]) * y;
+          qre = __builtin_amdgcn_mfma_f32_16x16x4f32(ur, bre[kk], qre, 0, 0, 0);
+          qre = __builtin_amdgcn_mfma_f32_16x16x4f32(-ui, bim[kk], qre, 0, 0, 0);
+          qim = __builtin_amdgcn_mfma_f32_16x16x4f32(ur, bim[kk], qim, 0, 0, 0);
+          qim = __builtin_amdgcn_mfma_f32_16x16x4f32(ui, bre[kk], qim, 0, 0, 0);
+        }
+        const int rr = 4 * m + kq;                 // accumulator rows 4 kq + v: (rr, f = v), column s = e
+        if (rr < N && e < N) {
+          T* dst = Lw + LCc::qs + (rr * N + e) * 8;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            dst[2 * v] = qre[v];
+            dst[2 * v + 1] = qim[v];
+          }
+          if (e == rr && !AQ_ABL(8)) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) hbar[SM::hoff(3) + rowsrc[rr] * 4 + v] = qre[v];
+          }
+        }
+      }
+    } else {
     for (int idx = lane; idx < NH * N * N; idx += 64) {
       const int rs = idx >> 2, f = idx & 3;
       const int r = rs / N, s = rs - r * N;
@@ -1096,6 +1158,7 @@ k_walker_rev(KArgs ka) {
       }
       Lw[LCc::qs + idx * 2] = qr;
       Lw[LCc::qs + idx * 2 + 1] = qi;
+    }
     }
   }
   AQ_SYNC();   // ybar overwrites Yt
@@ -1356,7 +1419,7 @@ k_walker_rev(KArgs ka) {
   // may_fresh (compile-time after unrolling): the pair may recompute its forward values; fresh
   // selects them per lane without a branch (a divergent branch here turned the uniform weights
   // into per-lane copies at the merge)
-  auto pair_adjoint = [&](int k, int i, bool may_fresh, bool fresh, const T* tcache) {
+  auto pair_adjoint = [&](int k, int i, bool may_fresh, bool fresh, const T* tcache, T cusp, T al) {
     // the uniform layer weights are re-read per pair from the scalar cache (s_load) instead of
     // being kept in SGPRs across the kernel (which spills them through VALU lane writes)
     cptr<T> Pq = P;
@@ -1424,10 +1487,11 @@ k_walker_rev(KArgs ka) {
     }
     // p0 = [r, d]; Pade e-e Jastrow once per unordered pair (k < i)
     T rb = pb0[0];
-    if (k < i) {
-      const T cusp = Pq[Ly::jee_c + k * N + i], al = Pq[Ly::jee_a + k * N + i];
+    {
+      // the pair's Jastrow parameters come loaded on every lane and are masked here (a branch
+      // around their loads waited for every load in flight, the cached tanh's included)
       const T den = al * r + T(1);
-      rb += cusp * f_rcp(den * den);
+      rb += and_zero(k < i, cusp * f_rcp(den * den));
     }
     const T ir = f_rcp(r);
 #pragma unroll
@@ -1442,7 +1506,7 @@ k_walker_rev(KArgs ka) {
     // and the earlier iterations (instead of one exposed cache round trip per iteration).
     constexpr int M = 2 * (N - 1);
     constexpr int NIT = (NPR + 63) / 64;
-    T tc[NIT][8];
+    T tc[NIT][8], jc[NIT], ja[NIT];
     int pk[NIT], pi2[NIT];
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
@@ -1451,15 +1515,21 @@ k_walker_rev(KArgs ka) {
       const int k = code & 15, i = (code >> 4) & 15;
       pk[u] = k;
       pi2[u] = i;
+      jc[u] = P[Ly::jee_c + k * N + i];
+      ja[u] = P[Ly::jee_a + k * N + i];
+    }
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {
+      const int k = pk[u], i = pi2[u];
       // loaded on every lane (the fresh pairs of iteration 0 select their own values)
-      const T* tp = Wc + WC::pt + (code >> 8) * 8;
+      const T* tp = Wc + WC::pt + (k * N + i) * 8;
 #pragma unroll
       for (int o = 0; o < 8; ++o) tc[u][o] = tp[o];
     }
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
       const int it = lane + 64 * u;
-      if (it < NPR) pair_adjoint(pk[u], pi2[u], u == 0, u == 0 && it < M, tc[u]);
+      if (it < NPR) pair_adjoint(pk[u], pi2[u], u == 0, u == 0 && it < M, tc[u], jc[u], ja[u]);
     }
   } else if (!reuse) {
     if (!PREP && !isprop && ka.wcache) {
@@ -1471,13 +1541,14 @@ k_walker_rev(KArgs ka) {
         const int k = it / (N - 1);
         const int jj = it - k * (N - 1);
         const int i = jj + (jj >= k ? 1 : 0);
-        pair_adjoint(k, i, false, false, Wc + WC::pt + (k * N + i) * 8);
+        pair_adjoint(k, i, false, false, Wc + WC::pt + (k * N + i) * 8, P[Ly::jee_c + k * N + i], P[Ly::jee_a + k * N + i]);
       }
     } else {
       for (int it = lane; it < NPR; it += 64) {
         const int k = it / (N - 1);
         const int jj = it - k * (N - 1);
-        pair_adjoint(k, jj + (jj >= k ? 1 : 0), true, true, nullptr);
+        const int i = jj + (jj >= k ? 1 : 0);
+        pair_adjoint(k, i, true, true, nullptr, P[Ly::jee_c + k * N + i], P[Ly::jee_a + k * N + i]);
       }
     }
   }
