@@ -497,7 +497,10 @@ def main():
             "flop_model": "B*N*3*F_fwd, F_fwd=4.9e4 (SURVEY 8d)"}
         lap = {
             "kernel": "k_walker_rev<float,14,2,PREP> + k_walker_lap<float,14,2> (local energy, 2 launches)",
-            "bound": "valu", "achieved": achieved_el, "peak": peak, "unit": "TFLOP/s",
+            # fp32 VALU and MFMA share the 157.3 TF peak on gfx950; the adjoint pass forms
+            # Q_f = (W.Yt) B with v_mfma_f32_16x16x4f32, the rest is VALU
+            "bound": "valu", "compute_unit": "VALU fp32 + MFMA f32 (Q_f in the adjoint pass)",
+            "achieved": achieved_el, "peak": peak, "unit": "TFLOP/s",
             "frac": (achieved_el / peak) if achieved_el else None, "avg_launch_ms": m["lap_avg_ms"],
             "traffic": el_traffic,
             "mfma_util": pmc.get("local_energy_mfma_util") if use_pmc else None,

@@ -79,6 +79,7 @@ def summarise(root):
             # MFMA busy cycles are summed over the 1024 SIMDs; utilisation against the launch's
             # GPU-active cycles (GRBM_GUI_ACTIVE) x SIMDs
             d["mfma_util"] = (busy / (gui * 1024) if (busy and gui) else 0.0)
+            d["gui_active_per_launch"] = gui
         if get("mem", "SQ_INSTS_VMEM_RD") is not None and waves:
             d["vmem_rd_per_wave"] = get("mem", "SQ_INSTS_VMEM_RD") / waves
             d["vmem_wr_per_wave"] = get("mem", "SQ_INSTS_VMEM_WR") / waves
@@ -102,6 +103,12 @@ def main():
     el_bytes = None
     if prep.get("hbm_bytes_per_launch") is not None and lap.get("hbm_bytes_per_launch") is not None:
         el_bytes = prep["hbm_bytes_per_launch"] + lap["hbm_bytes_per_launch"]
+    # the local-energy pair's MFMA utilisation: both launches' MFMA busy cycles over both launches'
+    # active cycles (the adjoint pass forms Q_f on the matrix cores)
+    el_mfma = None
+    if prep.get("gui_active_per_launch") and lap.get("gui_active_per_launch"):
+        el_mfma = ((prep.get("mfma_busy_cycles_per_launch") or 0) + (lap.get("mfma_busy_cycles_per_launch") or 0)) / (
+            (prep["gui_active_per_launch"] + lap["gui_active_per_launch"]) * 1024)
     out = {
         "source": "tools/gpu_pmc3.sh: rocprofv3 --pmc, one counter group per run, tools/mc_loop.py "
                   f"(N2, {walkers} walkers, fp32, 10 sweeps + local energy per iteration); per-launch means",
@@ -113,7 +120,7 @@ def main():
         "proposal_nonfp_valu_insts_per_wave": prop.get("nonfp_valu_insts_per_wave"),
         "proposal_mfma_util": prop.get("mfma_util"),
         "local_energy_hbm_bytes_per_pair": el_bytes,
-        "local_energy_mfma_util": lap.get("mfma_util"),
+        "local_energy_mfma_util": el_mfma if el_mfma is not None else lap.get("mfma_util"),
         "kernels": k,
     }
     print(json.dumps(out, indent=1))
