@@ -68,41 +68,30 @@ __global__ __launch_bounds__(1024) void k_taueff(const T* __restrict__ x, int n,
   }
 }
 
-// fp32 limdrift reduction of an unfused sweep (batches above FUSE_REDUCE_MAX_B): TAUEFF_NB
-// workgroups, every element entering as tacc_fix(x) -- the fused accumulators' arithmetic, so the
-// factor is bit-for-bit the one the fused path derives, in any arrival order.  Each workgroup adds
-// its exact integer partial to acc[0]; the last one to finish (acc[1] counts them) forms taueff from
-// the total and clears acc for the next launch in stream order.  A single 1024-thread workgroup
-// (k_taueff) took 4.6 us for the N2 proposal batch.
-constexpr int TAUEFF_NB = 32;
-__global__ __launch_bounds__(256) void k_taueff_wide(const float* __restrict__ x, int n, double tstep, double* out,
-                                                     unsigned long long* acc) {
+// fp32 limdrift reduction of an unfused sweep (batches above FUSE_REDUCE_MAX_B): TPART
+// workgroups, every element entering as tacc_fix(x) -- the fused accumulators' arithmetic --
+// each workgroup writing its exact integer partial sum to part[blockIdx.x]; the consumers
+// (taueff_wave) add the TPART partials with one load per lane and form the factor themselves.
+// The same bits as the fused path at any batch size and in any order; no atomics, fences or a
+// finalising workgroup on the critical path (k_taueff, one 1024-thread workgroup, took 4.6 us for
+// the N2 proposal batch; a 32-workgroup version finishing in its last workgroup 4.5 us).
+__global__ __launch_bounds__(256) void k_taueff_part(const float* __restrict__ x, int n,
+                                                     unsigned long long* __restrict__ part) {
   __shared__ unsigned long long ws[4];
   unsigned long long v = 0;
-  const int stride = TAUEFF_NB * 256;
-  int i = blockIdx.x * 256 + (int)threadIdx.x;
-  for (; i + 7 * stride < n; i += 8 * stride) {
+  const int stride = TPART * 256;
+  for (int i = blockIdx.x * 256 + (int)threadIdx.x; i < n; i += 8 * stride) {
     float t[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) t[k] = x[i + k * stride];
+    for (int k = 0; k < 8; ++k) t[k] = i + k * stride < n ? x[i + k * stride] : 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v += tacc_fix((double)t[k]);
+    for (int k = 0; k < 8; ++k) v += i + k * stride < n ? tacc_fix((double)t[k]) : 0ull;
   }
-  for (; i < n; i += stride) v += tacc_fix((double)x[i]);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    atomicAdd(acc, (ws[0] + ws[1]) + (ws[2] + ws[3]));
-    __threadfence();
-    if (atomicAdd(acc + 1, 1ull) == TAUEFF_NB - 1) {
-      const unsigned long long tot = atomicAdd(acc, 0ull);
-      *out = (double)taueff_from_v2<float>((double)tot * (1.0 / TACC_SCALE), tstep);
-      atomicExch(acc, 0ull);
-      atomicExch(acc + 1, 0ull);
-    }
-  }
+  if (threadIdx.x == 0) part[blockIdx.x] = (ws[0] + ws[1]) + (ws[2] + ws[3]);
 }
 
 // Per-sweep random draws (production mode), one thread per (walker b, electron i):
@@ -380,6 +369,9 @@ static void free_ws(aiqmc_ctx* c) {
   if (c->d_tacc) (void)hipFree(c->d_tacc);
   c->d_tacc = nullptr;
   c->tacc_n = 0;
+  if (c->d_tpart) (void)hipFree(c->d_tpart);
+  c->d_tpart = nullptr;
+  c->tpart_n = 0;
   c->ws_B = 0;
   c->ws_bytes = 0;
 }
@@ -401,9 +393,7 @@ static int ensure_ws(aiqmc_ctx* c, int B) {
     HIPCHK(hipMalloc(ptrs[k], bytes[k]));
     tot += (int64_t)bytes[k];
   }
-  // [2] limdrift factors, then k_taueff_wide's two (sum, count) accumulator pairs, zeroed once
-  HIPCHK(hipMalloc((void**)&c->d_taueff, 6 * sizeof(double)));
-  HIPCHK(hipMemset(c->d_taueff + 2, 0, 4 * sizeof(double)));
+  HIPCHK(hipMalloc((void**)&c->d_taueff, 2 * sizeof(double)));
 
   c->ws_B = B;
   c->ws_bytes = tot + 16;
@@ -758,9 +748,10 @@ int aiqmc_debug_local_energy_forward(aiqmc_ctx* c, const void* pos, int32_t B, v
 static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double tstep, int rng_mode, const void* gauss1,
                     const void* gauss2, const void* u, int st, uint64_t seed, uint64_t step, int32_t* accept_out,
                     double* dmc, hipStream_t s, AccArgs* pending = nullptr, bool defer = false,
-                    unsigned long long* tacc = nullptr) {
+                    unsigned long long* tacc = nullptr, unsigned long long* tpart = nullptr) {
   const int N = c->N;
   if (dmc) tacc = nullptr;
+  if (dmc || tacc || c->dtype != AIQMC_F32) tpart = nullptr;
   const size_t es = c->dtype == AIQMC_F32 ? 4 : 8;
   double* dscr = dmc ? dmc_scratch(c) : nullptr;
   if (dmc && !dscr) return fail(AIQMC_EHIP, "hipMalloc: DMC scratch");
@@ -800,9 +791,8 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
   timed(c, 1, s, [&] { ops.walker(c->dtype, MODE_GRAD, ka, B, s); });
   // (2) limdrift factor over the device batch (:60) -- fused: summed by the walker launch
   if (!tacc) {
-    if (c->dtype == AIQMC_F32 && !dmc && c->wide_reduce)
-      k_taueff_wide<<<dim3(TAUEFF_NB), dim3(256), 0, s>>>((const float*)c->d_sq, B, tstep, c->d_taueff,
-                                                         (unsigned long long*)(c->d_taueff + 2));
+    if (tpart)
+      k_taueff_part<<<dim3(TPART), dim3(256), 0, s>>>((const float*)c->d_sq, B, tpart);
     else if (c->dtype == AIQMC_F32)
       k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)c->d_sq, B, tstep, c->d_taueff);
     else
@@ -817,6 +807,7 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
   kp.gauss1 = g1;
   kp.taueff = c->d_taueff;
   kp.tacc = tacc;
+  kp.tpart = tpart;
   kp.tstep = tstep;
   kp.seed = seed;
   kp.step = step;
@@ -836,9 +827,8 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
   // (4) limdrift factor of the proposal gradients over all B*N*3N entries (:80) -- fused:
   // summed by the proposal launch
   if (!tacc) {
-    if (c->dtype == AIQMC_F32 && !dmc && c->wide_reduce)
-      k_taueff_wide<<<dim3(TAUEFF_NB), dim3(256), 0, s>>>((const float*)c->d_sqn, B * N, tstep, c->d_taueff + 1,
-                                                         (unsigned long long*)(c->d_taueff + 4));
+    if (tpart)
+      k_taueff_part<<<dim3(TPART), dim3(256), 0, s>>>((const float*)c->d_sqn, B * N, tpart + TPART);
     else if (c->dtype == AIQMC_F32)
       k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)c->d_sqn, B * N, tstep,
                          c->d_taueff + 1);
@@ -866,6 +856,7 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
   a.u = uu;
   a.taueff = c->d_taueff;
   a.tacc = tacc;
+  a.tpart = tpart;
   a.tstep = tstep;
   a.count = accept_out;
   if (defer && pending && !dmc) {
@@ -924,10 +915,24 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
     tacc = c->d_tacc;
     HIPCHK(hipMemsetAsync(tacc, 0, (size_t)2 * TACC_SLOTS * nsteps * sizeof(unsigned long long), s));
   }
+  // unfused fp32 sweeps: per-sweep partial sums of the limdrift reductions (k_taueff_part), kept
+  // until the next sweep's walker launch has read them (fused acceptance)
+  unsigned long long* tpart = nullptr;
+  if (!tacc && c->dtype == AIQMC_F32 && c->wide_reduce) {
+    if (c->tpart_n < nsteps) {
+      if (c->d_tpart) (void)hipFree(c->d_tpart);
+      c->d_tpart = nullptr;
+      c->tpart_n = 0;
+      HIPCHK(hipMalloc((void**)&c->d_tpart, (size_t)2 * TPART * nsteps * sizeof(unsigned long long)));
+      c->tpart_n = nsteps;
+    }
+    tpart = c->d_tpart;
+  }
   AccArgs pending{};
   for (int st = 0; st < nsteps; ++st) {
     rc = mc_sweep(c, ops, pos, B, tstep, rng_mode, gauss1, gauss2, u, st, seed, offset + (uint64_t)st, accept_out,
-                  nullptr, s, &pending, c->fuse_accept && st + 1 < nsteps, tacc ? tacc + 2 * TACC_SLOTS * st : nullptr);
+                  nullptr, s, &pending, c->fuse_accept && st + 1 < nsteps, tacc ? tacc + 2 * TACC_SLOTS * st : nullptr,
+                  tpart ? tpart + 2 * TPART * st : nullptr);
     if (rc) return rc;
   }
   HIPCHK(hipGetLastError());

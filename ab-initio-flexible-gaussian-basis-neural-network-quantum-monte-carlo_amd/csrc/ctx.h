@@ -45,7 +45,9 @@ struct aiqmc_ctx {
   int ablate = 0;                                           // AQ_ABLATE development builds (walker_rev.h)
   int fuse_accept = 1;                                      // acceptance fused into the next walker launch
   int fuse_reduce = 1;                                      // fp32 mc_step: limdrift sums by integer atomics
-  int wide_reduce = 1;                                      // unfused fp32 sweeps: k_taueff_wide (0: k_taueff)
+  int wide_reduce = 1;                                      // unfused fp32 sweeps: k_taueff_part (0: k_taueff)
+  unsigned long long* d_tpart = nullptr;                    // their per-sweep partial sums [tpart_n][2][TPART]
+  int tpart_n = 0;
   unsigned long long* d_tacc = nullptr;                     // their per-sweep accumulators [tacc_n][2]
   int tacc_n = 0;
   int lap_waves = 0;                                        // waves per walker of k_walker_lap (0: by batch)

@@ -478,8 +478,8 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
   if constexpr (WALK) {
     // ---------------------------------------------------------------- F0 positions (+ acceptance)
     if (ka.acc.lpn) {
-      const T te1 = taueff_wave<T>(ka.acc.taueff, ka.acc.tacc, 0, ka.acc.tstep);
-      const T te2 = taueff_wave<T>(ka.acc.taueff, ka.acc.tacc, 1, ka.acc.tstep);
+      const T te1 = taueff_wave<T>(ka.acc.taueff, ka.acc.tacc, 0, ka.acc.tstep, ka.acc.tpart);
+      const T te2 = taueff_wave<T>(ka.acc.taueff, ka.acc.tacc, 1, ka.acc.tstep, ka.acc.tpart);
       if (sl < N) {   // the previous sweep's acceptance of this walker's N proposals
         T xn[3];
         const bool acc = accept_one<T, N>(ka.acc, (const T*)ka.pos, conf, sl, xn, te1, te2);

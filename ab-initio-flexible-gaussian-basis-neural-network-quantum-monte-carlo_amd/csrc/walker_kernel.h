@@ -64,8 +64,19 @@ template <typename T> __device__ __forceinline__ T taueff_from_v2(double v2, dou
 // Limdrift factor k (0: walkers, 1: proposals) of the sweep: the sum of the fused accumulators
 // (one slot per lane, exact integer wave sum) or k_taueff's result.  Every lane of the wave must
 // be active (call it outside divergent code); the result is wave-uniform.
+// part (unfused fp32 sweeps): the TPART partial sums of k_taueff_part for both kinds [2][TPART],
+// the same integers as the fused accumulators, summed here (one load per lane).
+constexpr int TPART = 32;
 template <typename T>
-__device__ __forceinline__ T taueff_wave(const double* te, const unsigned long long* acc, int k, double tstep) {
+__device__ __forceinline__ T taueff_wave(const double* te, const unsigned long long* acc, int k, double tstep,
+                                         const unsigned long long* part = nullptr) {
+  if (part) {
+    const int l = (int)(threadIdx.x & 63);
+    unsigned long long v = l < TPART ? part[k * TPART + l] : 0ull;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return taueff_from_v2<T>((double)v * (1.0 / TACC_SCALE), tstep);
+  }
   if (!acc) return (T)te[k];
   const unsigned long long* a = acc + k * TACC_SLOTS + (int)(threadIdx.x & 63);
   unsigned long long v = 0;
@@ -86,6 +97,7 @@ struct AccArgs {
   const void* u;          // [B][N]
   const double* taueff;   // [2]
   const unsigned long long* tacc;   // [2][TACC_SLOTS] fused accumulators of the sweep (nullptr: taueff)
+  const unsigned long long* tpart;  // [2][TPART] k_taueff_part sums of the sweep (unfused fp32), or nullptr
   double tstep;
   int32_t* count;         // [B] accepted moves (optional)
 };
@@ -145,6 +157,7 @@ struct KArgs {
   // walker launches add their |grad|^2 to kind 0, proposal launches to kind 1; readers of the
   // walker factor (moved electron, proposals from scratch) sum kind 0 (taueff_wave)
   unsigned long long* tacc;
+  const unsigned long long* tpart;   // [2][TPART] partial sums of k_taueff_part (read by taueff_wave)
   double tstep;
   uint64_t seed, step;
   // single-electron-move layout (proposal != 0, k_walker_rev / k_moved_electron): configuration

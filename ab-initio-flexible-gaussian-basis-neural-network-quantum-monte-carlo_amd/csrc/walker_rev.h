@@ -280,7 +280,7 @@ __global__ __launch_bounds__(64 * MOVED_WPB) void k_moved_electron(KArgs ka) {
     for (int c = 0; c < 3; ++c) xp[c] = ((const T*)ka.xnew)[(size_t)q * 3 + c];
   } else {
     const T tstep = (T)ka.tstep;
-    const T te = taueff_wave<T>(ka.taueff, ka.tacc, 0, ka.tstep);
+    const T te = taueff_wave<T>(ka.taueff, ka.tacc, 0, ka.tstep, ka.tpart);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const size_t o = (size_t)b * 3 * N + 3 * i + c;
@@ -441,11 +441,11 @@ k_walker_rev(KArgs ka) {
     pi = (conf - pb * mper) / mdiv;
   }
   // reuse-off proposals: the walker limdrift factor, read by the wave before the divergent F0
-  const T te_walk = (!PROP && isprop && !ka.xnew) ? taueff_wave<T>(ka.taueff, ka.tacc, 0, ka.tstep) : T(0);
+  const T te_walk = (!PROP && isprop && !ka.xnew) ? taueff_wave<T>(ka.taueff, ka.tacc, 0, ka.tstep, ka.tpart) : T(0);
   if (!PREP && !isprop && ka.acc.lpn) {
     // the previous sweep's acceptance of this walker's N proposals (k_accept's arithmetic)
-    const T te1 = taueff_wave<T>(ka.acc.taueff, ka.acc.tacc, 0, ka.acc.tstep);
-    const T te2 = taueff_wave<T>(ka.acc.taueff, ka.acc.tacc, 1, ka.acc.tstep);
+    const T te1 = taueff_wave<T>(ka.acc.taueff, ka.acc.tacc, 0, ka.acc.tstep, ka.acc.tpart);
+    const T te2 = taueff_wave<T>(ka.acc.taueff, ka.acc.tacc, 1, ka.acc.tstep, ka.acc.tpart);
     if (lane < N) {
       T xn[3];
       const bool acc = accept_one<T, N>(ka.acc, (const T*)ka.pos, conf, lane, xn, te1, te2);

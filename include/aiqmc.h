@@ -266,7 +266,7 @@ int aiqmc_debug_set_fuse_accept(aiqmc_ctx* ctx, int32_t on);
  * proposal launches, as exact 64-bit integer sums of |grad|^2 in units of 2^-16: no reduction
  * launches, and the same bits in any arrival order.  mode 1 (default) = for batches of at most
  * 1,024 walkers (where it is faster), 2 = always, 0 = never: reduction launches that sum the same
- * integers in 32 workgroups (k_taueff_wide; the same bits as the fused sums), 3 = never, with the
+ * integers in 32 workgroups (k_taueff_part; the same bits as the fused sums), 3 = never, with the
  * single-workgroup fp64 tree sum (k_taueff; fp64 always uses it; results agree with the integer
  * sums to the float rounding of v2). */
 int aiqmc_debug_set_fuse_reduce(aiqmc_ctx* ctx, int32_t on);

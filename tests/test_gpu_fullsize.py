@@ -279,7 +279,7 @@ def test_fused_limdrift_reduction_matches_reduction_launches(name):
     """fp32 mc_step sums the two limdrift reductions of a sweep (VMCmcstep.py:11-14) inside the
     walker and proposal launches as exact integer accumulations (walker_kernel.h TACC_SCALE)
     instead of two reduction launches.  The integer sum is order independent: repeated runs are
-    bitwise equal, and so is the unfused path, whose reduction launches (k_taueff_wide) sum the
+    bitwise equal, and so is the unfused path, whose reduction launches (k_taueff_part) sum the
     same integers.  Against the fp64 tree-sum launch (k_taueff, mode 3) the limdrift factor
     differs only in the float rounding of v2, so the positions agree to rounding, with at most a
     rare acceptance flip (a ratio within ~1e-6 of its uniform).  Be runs the
