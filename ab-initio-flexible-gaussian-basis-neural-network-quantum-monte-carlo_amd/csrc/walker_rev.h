@@ -1009,7 +1009,17 @@ k_walker_rev(KArgs ka) {
         const T y = ok ? sm[yo + ccl] : T(0);
         a2[t] = pair_make<T>(pair_re<T>(acc) * y, pair_im<T>(acc) * y);
       }
+      // the elimination and B2 (below) run at raised wave priority: dense VALU with short
+      // dependencies, issued ahead of co-resident waves in their load/LDS-bound phases
+      // (measured: 224.7-226.3 -> 221.1-221.6 us per N2 launch; F4 too, B3, or the F1 load issue
+      // were neutral or worse)
+#ifndef AQ_NO_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
       if (!AQ_ABL(4)) gj_fixed_regs<T, N>(a2, Mx, lane, rec, logdet, phr, phi, bad);
+#ifndef AQ_NO_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
     } else
     if (!AQ_ABL(4)) gj_inverse_fixed<T, N>(Ph, Yv, Mx, lane, sm + SM::pv, logdet, phr, phi, bad);
 #ifdef AQ_ABLATE
@@ -1178,6 +1188,9 @@ k_walker_rev(KArgs ka) {
   // ------------------------------------------------------------------ B2 back through the h-stream layers
   // lane map of F4: the adjoint of h^{l+1}[i][f] stays in a register.
   T* g2b = sm + SM::g2;    // forward g2 values are dead after F4: reuse for their adjoints
+#ifndef AQ_NO_PRIO
+  if constexpr (PROP) __builtin_amdgcn_s_setprio(1);
+#endif
   if (!AQ_ABL(16)) {
 #ifdef AQ_B2_PRELOAD
     // as in F4: this lane's layer weights (the single layer's rows of the conv outputs this lane
@@ -1300,6 +1313,9 @@ k_walker_rev(KArgs ka) {
     }
   }
   AQ_SYNC();
+#ifndef AQ_NO_PRIO
+  if constexpr (PROP) __builtin_amdgcn_s_setprio(0);
+#endif
 
   if constexpr (PREP) {
     // ---------------------------------------------------------------- local-energy adjoint pass: tail
