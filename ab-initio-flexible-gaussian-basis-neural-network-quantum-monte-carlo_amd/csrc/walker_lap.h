@@ -49,6 +49,18 @@ struct SmemLap {
   static_assert(end - ly >= 3 * 3 * 64, "multi-wave partial sums (W <= 4) must fit behind ly");
 };
 
+// Workgroup copy of n elements of a LapCache block to LDS in 16-byte pieces (n * sizeof(T) is a
+// multiple of 16 for every staged block; all offsets are 16-byte aligned): a quarter of the load
+// and store instructions of an element-wise copy, and one round of loads in flight per block.
+template <typename T>
+__device__ __forceinline__ void stage_copy(T* dst, cptr<T> src, int n) {
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  const __attribute__((address_space(4))) u4* s = (const __attribute__((address_space(4))) u4*)src;
+  u4* d = (u4*)dst;
+  const int cnt = n * (int)sizeof(T) / 16;
+  for (int i = threadIdx.x; i < cnt; i += blockDim.x) d[i] = s[i];
+}
+
 // One h-stream layer (nn.py:280-311) in first derivatives, column loop over electrons i.
 // ly: this layer's LapCache block (LDS); hb: dh/dx of every electron, updated in place
 // (column `lane` = min(lane, 48), see SmemLap).
@@ -319,7 +331,8 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
   T h0b[D0];
 #pragma unroll
   for (int m = 0; m < D0; ++m) h0b[m] = Lc[LC::h0b + le * D0 + m];
-  for (int idx = threadIdx.x; idx < LC::layer_n; idx += blockDim.x) ly[idx] = Lc[idx];
+  static_assert(LC::layer_n * sizeof(T) % 16 == 0 && SM::ly * sizeof(T) % 16 == 0, "16-byte staging");
+  stage_copy<T>(ly, Lc, LC::layer_n);
   __syncthreads();
 
   // ------------------------------------------------------------------ per-electron stage (electron.h)
@@ -348,11 +361,11 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
   // ------------------------------------------------------------------ h stream, first derivatives
   lap_layer<T, N, A, 0>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W);
   __syncthreads();
-  for (int idx = threadIdx.x; idx < LC::layer_n; idx += blockDim.x) ly[idx] = Lc[LC::layer_n + idx];
+  stage_copy<T>(ly, Lc + LC::layer_n, LC::layer_n);
   __syncthreads();
   lap_layer<T, N, A, 1>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W);
   __syncthreads();
-  for (int idx = threadIdx.x; idx < LC::layer_n; idx += blockDim.x) ly[idx] = Lc[2 * LC::layer_n + idx];
+  stage_copy<T>(ly, Lc + 2 * LC::layer_n, LC::layer_n);
   __syncthreads();
   lap_layer<T, N, A, 2>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W);
   if (W > 1) __syncthreads();   // the determinant terms read every wave's columns of dh/dx
@@ -377,10 +390,11 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
   __syncthreads();   // every wave has read its Yt jets (E1)
   {
     T* qd = sm + SM::qs;
-    for (int idx = threadIdx.x; idx < 8 * N * N; idx += blockDim.x) qd[idx] = Lc[LC::qs + idx];
+    static_assert(LC::qs % 4 == 0 && LC::bm % 4 == 0 && SM::qs % 4 == 0 && SM::bs % 4 == 0, "16-byte staging");
+    stage_copy<T>(qd, Lc + LC::qs, 8 * N * N);
     if constexpr (SM::stage_b) {
       T* bd = sm + SM::bs;
-      for (int idx = threadIdx.x; idx < 2 * N * N; idx += blockDim.x) bd[idx] = Lc[LC::bm + idx];
+      stage_copy<T>(bd, Lc + LC::bm, 2 * N * N);
     }
   }
   __syncthreads();
