@@ -416,12 +416,20 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
     wi[col] = pm * Yd1[col];
     wbr += wr[col] * br - wi[col] * bi;
     wbi += wr[col] * bi + wi[col] * br;
-    T dpr = T(0), dpi = T(0);
+    // d Phi[e, col] / dx for both spin blocks from wave-uniform weights (scalar loads, re-read per
+    // column through an opaque pointer), selected by the row's spin: the per-lane weight loads
+    // (spin-dependent address) were hoisted into registers and spilled
+    cptr<T> Pw = P;
+    asm volatile("" : "+s"(Pw));
+    T d0r = T(0), d0i = T(0), d1r = T(0), d1i = T(0);
 #pragma unroll
     for (int f = 0; f < NH; ++f) {
-      dpr += Ue[f] * P[Ly::orb_w + ((spe * NH + f) * N + col) * 2];
-      dpi += Ue[f] * P[Ly::orb_w + ((spe * NH + f) * N + col) * 2 + 1];
+      d0r += Ue[f] * Pw[Ly::orb_w + (f * N + col) * 2];
+      d0i += Ue[f] * Pw[Ly::orb_w + (f * N + col) * 2 + 1];
+      d1r += Ue[f] * Pw[Ly::orb_w + ((NH + f) * N + col) * 2];
+      d1i += Ue[f] * Pw[Ly::orb_w + ((NH + f) * N + col) * 2 + 1];
     }
+    const T dpr = spe ? d1r : d0r, dpi = spe ? d1i : d0i;
     const T xr = T(2) * dpr * Yd1[col] + pr * Yd2[col];
     const T xi = T(2) * dpi * Yd1[col] + pm * Yd2[col];
     t2 += xr * br - xi * bi;
