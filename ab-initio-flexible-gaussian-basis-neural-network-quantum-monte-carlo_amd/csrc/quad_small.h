@@ -17,9 +17,9 @@
 //      slot (DPP row_ror 4, 8, and a lane swizzle across the two rows of a 32-lane slot), the
 //      conv quads as in k_walker_rev;
 //   F5 Phi (x) Yt and its determinant by LU with partial pivoting (LAPACK izamax rule, virtual
-//      row exchanges): lane c of the slot's first row holds column c, column k is broadcast by
-//      DPP row_newbcast.  No inverse is needed for values, so no fixed pivot order and no
-//      fallback.
+//      row exchanges): lane 4r + c of the slot holds row r's entries c (and c + 4 for N > 4),
+//      column k reaches row r's lanes by quad broadcast, the pivot by a packed-key max over the
+//      row quads.  No inverse is needed for values, so no fixed pivot order and no fallback.
 // k_quad_grad (N <= 4, four per wave): the Metropolis proposals (value + gradient) and, WALK,
 // the walker launches -- see its own header below.
 // log|psi| = log|det| + J_ae + J_ee (the Jastrows multiply the matrix, nn.py:504, Q11).
@@ -316,15 +316,22 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
         b -= mr * ei + mi * er;
       }
     }
-  } else if (sl < NI) {
-    const int c = sl;
-    const int* rowsrc = ka.rowsrc;
-    T ar[NI], ai[NI];
+  } else {
+    // 5 <= N <= 8: lane 4r + g of the slot holds A[r][g] and A[r][g + 4] (row r, two columns).
+    // Column k reaches the lanes of its row by one quad broadcast; the pivot of column k is the
+    // max of packed keys (low three bits 7 - r) over the slot's eight row quads: DPP row_ror 4,
+    // 8 inside each 16-lane row, one lane exchange across the slot's two rows; the pivot row's
+    // two entries of this lane's columns come by lane permutes.
+    const int r = sl >> 2, g = sl & 3;
+    const bool rl = r < N;
+    T a[2], b[2];
 #pragma unroll
-    for (int r = 0; r < NI; ++r) {
-      T a = T(0), b = T(0);
-      if (r < N && c < N) {
-        const int src = rowsrc[r];
+    for (int h = 0; h < 2; ++h) {
+      const int c = g + 4 * h;
+      a[h] = T(0);
+      b[h] = T(0);
+      if (rl && c < N) {
+        const int src = ka.rowsrc[r];
         const int sp = r < nup ? 0 : 1;
         T re = P[Ly::orb_b + (sp * N + c) * 2 + 0], im = P[Ly::orb_b + (sp * N + c) * 2 + 1];
 #pragma unroll
@@ -334,40 +341,42 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
           im += hv * P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 1];
         }
         const T y = Yv[r * N + c];
-        a = re * y;
-        b = im * y;
+        a[h] = re * y;
+        b[h] = im * y;
       }
-      ar[r] = a;
-      ai[r] = b;
     }
+    const int sbase = lane & ~31;
     unsigned used = 0;
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-      T kr[NI], ki[NI];
-#pragma unroll
-      for (int r = 0; r < NI; ++r) {
-        kr[r] = row_bcast(ar[r], k);
-        ki[r] = row_bcast(ai[r], k);
+      const int kh = k >> 2;
+      T akr, aki;   // A[r][k]
+      if ((k & 3) == 0) { akr = quad_bcast<0>(a[kh]); aki = quad_bcast<0>(b[kh]); }
+      else if ((k & 3) == 1) { akr = quad_bcast<1>(a[kh]); aki = quad_bcast<1>(b[kh]); }
+      else if ((k & 3) == 2) { akr = quad_bcast<2>(a[kh]); aki = quad_bcast<2>(b[kh]); }
+      else { akr = quad_bcast<3>(a[kh]); aki = quad_bcast<3>(b[kh]); }
+      const bool open = rl && !((used >> r) & 1u);
+      unsigned key = open ? ((key_bits(f_abs(akr) + f_abs(aki)) & ~7u) | (unsigned)(7 - r)) : 0u;
+      {
+        const unsigned k4 = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x124, 0xF, 0xF, true);
+        key = key > k4 ? key : k4;
+        const unsigned k8 = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x128, 0xF, 0xF, true);
+        key = key > k8 ? key : k8;
+        const unsigned k16 = (unsigned)__shfl_xor((int)key, 16);
+        key = key > k16 ? key : k16;
       }
-      // pivot: first unused row with the largest |re| + |im| (izamax)
-      int p = 0;
-      T best = T(-1);
-#pragma unroll
-      for (int r = 0; r < N; ++r) {
-        const T m = f_abs(kr[r]) + f_abs(ki[r]);
-        const bool take = !((used >> r) & 1u) && m > best;
-        best = take ? m : best;
-        p = take ? r : p;
+      const int p = 7 - (int)(key & 7u);
+      const int srcl = sbase + 4 * p + g;
+      const T er0 = __shfl(a[0], srcl), ei0 = __shfl(b[0], srcl);   // A[p][g]
+      const T er1 = __shfl(a[1], srcl), ei1 = __shfl(b[1], srcl);   // A[p][g + 4]
+      T pr, pim;   // A[p][k]
+      {
+        const T sr = kh ? er1 : er0, si = kh ? ei1 : ei0;
+        if ((k & 3) == 0) { pr = quad_bcast<0>(sr); pim = quad_bcast<0>(si); }
+        else if ((k & 3) == 1) { pr = quad_bcast<1>(sr); pim = quad_bcast<1>(si); }
+        else if ((k & 3) == 2) { pr = quad_bcast<2>(sr); pim = quad_bcast<2>(si); }
+        else { pr = quad_bcast<3>(sr); pim = quad_bcast<3>(si); }
       }
-      T pr = T(0), pim = T(0), rpr = T(0), rpi = T(0);   // pivot, this lane's entry of row p
-#pragma unroll
-      for (int r = 0; r < N; ++r)
-        if (r == p) {
-          pr = kr[r];
-          pim = ki[r];
-          rpr = ar[r];
-          rpi = ai[r];
-        }
       inv += __builtin_popcount(used >> p);   // earlier pivots below p in the row order
       used |= 1u << p;
       const T den = pr * pr + pim * pim;
@@ -381,13 +390,12 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
         ui = ni;
       }
       const T ipr = pr * rden, ipi = -pim * rden;   // 1 / pivot
-#pragma unroll
-      for (int r = 0; r < N; ++r) {
-        if (!((used >> r) & 1u)) {
-          const T mr = kr[r] * ipr - ki[r] * ipi, mi = kr[r] * ipi + ki[r] * ipr;
-          ar[r] -= mr * rpr - mi * rpi;
-          ai[r] -= mr * rpi + mi * rpr;
-        }
+      if (rl && !((used >> r) & 1u)) {   // rows still open: A[r][:] -= (A[r][k] / pivot) A[p][:]
+        const T mr = akr * ipr - aki * ipi, mi = akr * ipi + aki * ipr;
+        a[0] -= mr * er0 - mi * ei0;
+        b[0] -= mr * ei0 + mi * er0;
+        a[1] -= mr * er1 - mi * ei1;
+        b[1] -= mr * ei1 + mi * er1;
       }
     }
   }
