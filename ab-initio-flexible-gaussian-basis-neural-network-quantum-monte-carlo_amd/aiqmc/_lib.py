@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
     "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves", "aiqmc_phase_param_grad",
     "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals", "aiqmc_debug_set_ablate", "aiqmc_debug_set_fuse_accept", "aiqmc_debug_set_lap_waves",
-    "aiqmc_debug_set_fuse_reduce",
+    "aiqmc_debug_set_fuse_reduce", "aiqmc_energy_stats", "aiqmc_energy_stats_final",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -149,13 +149,16 @@ def load() -> ctypes.CDLL:
                                            vp, vp]
     lib.aiqmc_profile_enable.argtypes = [vp, i32]
     lib.aiqmc_profile_read.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64)]
+    lib.aiqmc_energy_stats.argtypes = [vp, i32, i64, vp, i32, vp]
+    lib.aiqmc_energy_stats_final.argtypes = [vp, vp]
     lib.aiqmc_last_error.restype = ctypes.c_char_p
     lib.aiqmc_supported_shapes.restype = ctypes.c_char_p
     for name in ("aiqmc_create", "aiqmc_destroy", "aiqmc_set_params", "aiqmc_logpsi",
                  "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_mc_step", "aiqmc_profile_enable",
                  "aiqmc_profile_read", "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
                  "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves",
-                 "aiqmc_phase_param_grad", "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals"):
+                 "aiqmc_phase_param_grad", "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals",
+                 "aiqmc_energy_stats", "aiqmc_energy_stats_final"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib
@@ -181,6 +184,25 @@ def _ptr(t: Optional[torch.Tensor]):
 
 def _stream(device) -> ctypes.c_void_p:
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def energy_stats(e_l: torch.Tensor, finalize: bool = True) -> torch.Tensor:
+    """aiqmc_energy_stats on a device tensor of local energies (float32/float64): a float64 device
+    tensor [sum |e - m|^2, n m, n m^2, n, mean, variance] (the last two only with finalize)."""
+    if not e_l.is_cuda or e_l.dtype not in (torch.float32, torch.float64):
+        raise ValueError("energy_stats: a float32/float64 device tensor is required")
+    e = e_l.contiguous().reshape(-1)
+    out = torch.empty(6, dtype=torch.float64, device=e.device)
+    dt = AIQMC_F32 if e.dtype == torch.float32 else AIQMC_F64
+    check(load().aiqmc_energy_stats(_ptr(e), dt, e.numel(), _ptr(out), 1 if finalize else 0, _stream(e.device)),
+          "aiqmc_energy_stats")
+    return out
+
+
+def energy_stats_final(out: torch.Tensor) -> torch.Tensor:
+    """aiqmc_energy_stats_final: out[4..5] = [mean, variance] from a summed out[0..3], in place."""
+    check(load().aiqmc_energy_stats_final(_ptr(out), _stream(out.device)), "aiqmc_energy_stats_final")
+    return out
 
 
 class Context:

@@ -51,7 +51,21 @@ def pmean_stats(e_l: torch.Tensor):
         var = (sum_r M2_r + sum_r n_r (m_r - E)^2) / n,   sum_r n_r (m_r - E)^2 = sum_r n_r m_r^2 - n E^2,
     in float64; the within-rank spread never meets the E^2 cancellation.  Equal to the
     reference's two-pass value (for the equal per-device batches the drivers require).
+
+    Device tensors go through aiqmc_energy_stats (one workgroup forms the 4-vector, and the
+    mean/variance when there is no collective): 2 launches per iteration instead of ~17 small
+    elementwise/reduction kernels.  Host tensors (gloo ranks) and other dtypes take the same
+    formulas in torch.
     """
+    if e_l.is_cuda and e_l.dtype in (torch.float32, torch.float64):
+        from . import _lib
+        if not _active():
+            v = _lib.energy_stats(e_l, finalize=True)
+        else:
+            v = _lib.energy_stats(e_l, finalize=False)
+            dist.all_reduce(v, op=dist.ReduceOp.SUM)   # out[4..5] are rewritten below
+            _lib.energy_stats_final(v)
+        return v[4], v[5]
     e = e_l.to(torch.float64)
     n = float(e.numel())
     m = e.mean()

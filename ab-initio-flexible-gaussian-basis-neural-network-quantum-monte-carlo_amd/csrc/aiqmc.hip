@@ -158,6 +158,54 @@ __global__ void k_dmc_sum_fin(const double* __restrict__ part, int proposed, dou
   }
 }
 
+// Energy statistics of one iteration (loss.py:206-208 through constants.pmean_stats), one
+// workgroup: out[0..3] = [sum |e - m|^2, n m, n m^2, n] in fp64 (m = the mean of these n
+// energies; the summed 4-vector of all ranks gives the pooled mean and variance), and with
+// finalize out[4..5] = [mean, variance] from out[0..3] (k_energy_stats_final after an all-reduce).
+__device__ __forceinline__ double block_sum_1024(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += red[k];
+  return t;
+}
+__device__ __forceinline__ void energy_stats_final(double* out) {
+  const double mean = out[1] / out[3];
+  double between = out[2] - out[3] * mean * mean;
+  between = between > 0.0 ? between : 0.0;
+  out[4] = mean;
+  out[5] = (out[0] + between) / out[3];
+}
+template <typename T>
+__global__ __launch_bounds__(1024) void k_energy_stats(const T* __restrict__ e, int64_t n, double* __restrict__ out,
+                                                       int finalize) {
+  __shared__ double red[16];
+  double a = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) a += (double)e[i];
+  const double nn = (double)n;
+  const double m = block_sum_1024(a, red) / nn;
+  double q = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const double d = (double)e[i] - m;
+    q += d * d;
+  }
+  q = block_sum_1024(q, red);
+  if (threadIdx.x == 0) {
+    out[0] = q;
+    out[1] = nn * m;
+    out[2] = nn * m * m;
+    out[3] = nn;
+    if (finalize) energy_stats_final(out);
+  }
+}
+__global__ void k_energy_stats_final(double* out) {
+  if (threadIdx.x == 0) energy_stats_final(out);
+}
+
 // out[i] = grad[i] * taueff (limdrift, VMCmcstep.py:11-14 / drift_diffusion.py:9-12)
 template <typename T>
 __global__ __launch_bounds__(256) void k_scale_grad(const T* __restrict__ g, const double* __restrict__ taueff, int n,
@@ -1377,6 +1425,26 @@ int aiqmc_dmc_branch(aiqmc_ctx* c, int32_t B, const void* weights, double u, int
     k_dmc_branch<double><<<dim3(1), dim3(1024), 0, s>>>(B, (const double*)weights, u, csum, newinds,
                                                          (double*)weight_out);
   HIPCHK(hipFreeAsync(csum, s));
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_energy_stats(const void* e_l, int32_t dtype, int64_t n, double* out, int32_t finalize, void* stream) {
+  if (n <= 0) return fail(AIQMC_EINVAL, "empty batch");
+  if (!e_l || !out) return fail(AIQMC_EINVAL, "null argument");
+  if (dtype != AIQMC_F32 && dtype != AIQMC_F64) return fail(AIQMC_EINVAL, "dtype must be AIQMC_F32 or AIQMC_F64");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == AIQMC_F32)
+    k_energy_stats<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)e_l, n, out, finalize != 0);
+  else
+    k_energy_stats<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)e_l, n, out, finalize != 0);
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_energy_stats_final(double* out, void* stream) {
+  if (!out) return fail(AIQMC_EINVAL, "null argument");
+  k_energy_stats_final<<<dim3(1), dim3(64), 0, (hipStream_t)stream>>>(out);
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
 }

@@ -78,6 +78,66 @@ struct SmemQ {
   static constexpr int size = h3 + NI * 4;
 };
 
+// F1 of the packed kernels: walker pb's cached stage (positions X, walker cache Wc) with electron
+// pi's entries from its moved-electron record Eq, into the slot's LDS block.  Every load is
+// issued (at clamped in-bounds addresses; the moved electron's entries by one load from a
+// selected address) before the first LDS write, so a slot pays one memory round trip instead of
+// one per loop trip.  Returns this lane's share of J (J_ae of electron sl, + J_ee on lane 0).
+template <typename T, int N, int A, int SW>
+__device__ __forceinline__ T quad_stage_load(const T* X, const T* Wc, const T* Eq, int pi, int sl, T* xs, T* xo,
+                                             T* Yv, T* hl, T* g2) {
+  using WC = WCache<N, A>;
+  using EC = ECache<N, A>;
+  constexpr int D0 = 4 * A;
+  constexpr int NX = (3 * N + SW - 1) / SW, NY = (N * N + SW - 1) / SW, NHL = (N * D0 + SW - 1) / SW;
+  constexpr int NG = (24 * N + SW - 1) / SW;
+  T x0[NX], xv[NX], yv[NY], hv[NHL], gv[NG];
+#pragma unroll
+  for (int t = 0; t < NX; ++t) {
+    const int idx = sl + t * SW, ic = idx < 3 * N ? idx : 3 * N - 1;
+    x0[t] = X[ic];
+    xv[t] = *(ic / 3 == pi ? Eq + EC::xp + ic % 3 : X + ic);
+  }
+#pragma unroll
+  for (int t = 0; t < NY; ++t) {
+    const int idx = sl + t * SW, ic = idx < N * N ? idx : N * N - 1;
+    yv[t] = *(ic / N == pi ? Eq + EC::yv + ic % N : Wc + WC::yv + ic);
+  }
+#pragma unroll
+  for (int t = 0; t < NHL; ++t) {
+    const int idx = sl + t * SW, ic = idx < N * D0 ? idx : N * D0 - 1;
+    hv[t] = *(ic / D0 == pi ? Eq + EC::h0 + ic % D0 : Wc + WC::h0 + ic);
+  }
+#pragma unroll
+  for (int t = 0; t < NG; ++t) {
+    const int idx = sl + t * SW;
+    gv[t] = Wc[WC::g2 + (idx < 24 * N ? idx : 24 * N - 1)];
+  }
+  const int jc = sl < N ? sl : N - 1;
+  const T jv = *(jc == pi ? Eq + EC::jv : Wc + WC::jaev + jc);
+  const T jee = Wc[WC::jee];
+#pragma unroll
+  for (int t = 0; t < NX; ++t) {
+    const int idx = sl + t * SW;
+    if (idx < 3 * N) {
+      if (idx / 3 == pi) xo[idx - 3 * pi] = x0[t];
+      xs[idx] = xv[t];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NY; ++t)
+    if (sl + t * SW < N * N) Yv[sl + t * SW] = yv[t];
+#pragma unroll
+  for (int t = 0; t < NHL; ++t)
+    if (sl + t * SW < N * D0) hl[sl + t * SW] = hv[t];
+#pragma unroll
+  for (int t = 0; t < NG; ++t)
+    if (sl + t * SW < 24 * N) g2[sl + t * SW] = gv[t];
+  T jsum = sl < N ? jv : T(0);
+  if (sl == 0) jsum += jee;
+  return jsum;
+}
+
 template <typename T, int N, int A>
 __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
   static_assert(N <= 8, "several configurations per wave need N <= 8");
@@ -110,23 +170,8 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
   const T* Eq = (const T*)ka.ecache + (size_t)conf * EC::size;
 
   // ---------------------------------------------------------------- F1 cached stage of walker pb
-  for (int idx = sl; idx < 3 * N; idx += SW) {
-    const T x0 = ((const T*)ka.pos)[(size_t)pb * 3 * N + idx];
-    const bool mv = idx / 3 == pi;
-    if (mv) sm[SQ::xo + idx - 3 * pi] = x0;
-    xs[idx] = mv ? Eq[EC::xp + idx - 3 * pi] : x0;
-  }
-  for (int idx = sl; idx < N * N; idx += SW) {
-    const int r = idx / N;
-    Yv[idx] = r == pi ? Eq[EC::yv + idx - r * N] : Wc[WC::yv + idx];
-  }
-  for (int idx = sl; idx < N * D0; idx += SW) {
-    const int e = idx / D0;
-    hl[idx] = e == pi ? Eq[EC::h0 + idx - e * D0] : Wc[WC::h0 + idx];
-  }
-  for (int idx = sl; idx < 3 * 2 * N * 4; idx += SW) g2[idx] = Wc[WC::g2 + idx];
-  T jsum = sl < N ? (sl == pi ? Eq[EC::jv] : Wc[WC::jaev + sl]) : T(0);
-  if (sl == 0) jsum += Wc[WC::jee];
+  T jsum = quad_stage_load<T, N, A, SW>((const T*)ka.pos + (size_t)pb * 3 * N, Wc, Eq, pi, sl, xs, sm + SQ::xo,
+                                        Yv, hl, g2);
   wave_sync();
 
   // ---------------------------------------------------------------- F2 pairs of the moved electron
@@ -601,23 +646,8 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
     wave_sync();
   } else {
   // ---------------------------------------------------------------- F1 cached stage of walker pb
-  if (sl < 3 * N) {
-    const T x0 = ((const T*)ka.pos)[(size_t)pb * 3 * N + sl];
-    const bool mv = sl / 3 == pi;
-    if (mv) sm[SQ::xo + sl - 3 * pi] = x0;
-    xs[sl] = mv ? Eq[EC::xp + sl - 3 * pi] : x0;
-  }
-  if (sl < N * N) {
-    const int r = sl / N;
-    Yv[sl] = r == pi ? Eq[EC::yv + sl - r * N] : Wc[WC::yv + sl];
-  }
-  for (int idx = sl; idx < N * D0; idx += 16) {
-    const int e = idx / D0;
-    hl[idx] = e == pi ? Eq[EC::h0 + idx - e * D0] : Wc[WC::h0 + idx];
-  }
-  for (int idx = sl; idx < 3 * 2 * N * 4; idx += 16) g2[idx] = Wc[WC::g2 + idx];
-  jsum = sl < N ? (sl == pi ? Eq[EC::jv] : Wc[WC::jaev + sl]) : T(0);
-  if (sl == 0) jsum += Wc[WC::jee];
+  jsum = quad_stage_load<T, N, A, 16>((const T*)ka.pos + (size_t)pb * 3 * N, Wc, Eq, pi, sl, xs, sm + SQ::xo, Yv,
+                                      hl, g2);
   wave_sync();
 
   // ---------------------------------------------------------------- F2 pairs of the moved electron

@@ -223,6 +223,15 @@ int aiqmc_dmc_tmoves(aiqmc_ctx* ctx, void* pos_inout, int32_t B, double tstep, i
                      const void* u_sel, const void* u_acc, uint64_t seed, uint64_t offset, void* acceptance,
                      void* stream);
 
+/* Energy statistics of one VMC iteration (constants.pmean_stats; the reference's two pmeans,
+ * AIQMCrelease3 Loss/loss.py:206-208).  e_l[n] (dtype AIQMC_F32 | AIQMC_F64, device memory) is
+ * reduced in fp64 into out[0..3] = [sum |e - m|^2, n m, n m^2, n] (m = the mean of these n
+ * energies), one workgroup; the 4-vectors of all ranks sum (one all-reduce) to the pooled
+ * statistics.  finalize != 0 also writes out[4..5] = [mean, variance] of these n energies.
+ * aiqmc_energy_stats_final writes out[4..5] from a summed out[0..3].  out: >= 6 device doubles. */
+int aiqmc_energy_stats(const void* e_l, int32_t dtype, int64_t n, double* out, int32_t finalize, void* stream);
+int aiqmc_energy_stats_final(double* out, void* stream);
+
 /* Optional HIP-event timing of the hot kernels, recorded on the caller's
  * stream around each launch while enabled.  Slots: 0 = proposal
  * value+gradient launches of aiqmc_mc_step, 1 = walker gradient launches of

@@ -171,3 +171,35 @@ def test_network_orbitals_match_oracle(name, dtype):
     assert np.all(np.abs(got - ref) <= tol * scale), float(np.max(np.abs(got - ref) / scale))
     sign, ld = np.linalg.slogdet(got)
     np.testing.assert_allclose(ld, logabs.double().cpu().numpy(), rtol=tol, atol=tol * 10)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("n", [1, 7, 1000, 4096, 33000])
+def test_pmean_stats_device_kernel_matches_two_pass(dtype, n):
+    """constants.pmean_stats on a device tensor runs aiqmc_energy_stats; compare with the
+    reference's two pmeans (loss.py:206-208) on one rank in float64: E = mean(e),
+    var = mean(|e - E|^2), including heavy-tailed energies like the bench's random network."""
+    from aiqmc import constants, _lib
+    g = torch.Generator().manual_seed(n)
+    e = torch.randn(n, generator=g, dtype=torch.float64) * 30.0 - 100.0
+    e[:: 97] *= 1e3
+    ed = e.to("cuda", dtype)
+    mean, var = constants.pmean_stats(ed)
+    e64 = ed.cpu().to(torch.float64)
+    m_ref = e64.mean()
+    v_ref = ((e64 - m_ref) ** 2).mean()
+    assert mean.dtype == torch.float64 and mean.is_cuda
+    np.testing.assert_allclose(float(mean), float(m_ref), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(float(var), float(v_ref), rtol=1e-12, atol=0)
+    v = _lib.energy_stats(ed, finalize=False)
+    _lib.energy_stats_final(v)
+    np.testing.assert_array_equal(v[4:].cpu().numpy(), torch.stack([mean, var]).cpu().numpy())
+    assert float(v[3]) == n
+
+
+def test_energy_stats_rejects_empty_and_host():
+    from aiqmc import _lib
+    with pytest.raises(RuntimeError, match="empty"):
+        _lib.energy_stats(torch.empty(0, device="cuda"))
+    with pytest.raises(ValueError):
+        _lib.energy_stats(torch.ones(4))
