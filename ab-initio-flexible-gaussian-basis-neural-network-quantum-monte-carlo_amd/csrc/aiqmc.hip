@@ -161,7 +161,9 @@ __global__ void k_dmc_sum_fin(const double* __restrict__ part, int proposed, dou
 // Energy statistics of one iteration (loss.py:206-208 through constants.pmean_stats), one
 // workgroup: out[0..3] = [sum |e - m|^2, n m, n m^2, n] in fp64 (m = the mean of these n
 // energies; the summed 4-vector of all ranks gives the pooled mean and variance), and with
-// finalize out[4..5] = [mean, variance] from out[0..3] (k_energy_stats_final after an all-reduce).
+// finalize (one rank) out[4..5] = [m, sum |e - m|^2 / n], the reference's two-pass values.
+// k_energy_stats_final forms them from a summed 4-vector after the all-reduce (Chan's
+// combination; products not contracted into FMAs, so one rank's between-term n m^2 - n m^2 is 0).
 __device__ __forceinline__ double block_sum_1024(double v, double* red) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -174,6 +176,7 @@ __device__ __forceinline__ double block_sum_1024(double v, double* red) {
   return t;
 }
 __device__ __forceinline__ void energy_stats_final(double* out) {
+#pragma clang fp contract(off)
   const double mean = out[1] / out[3];
   double between = out[2] - out[3] * mean * mean;
   between = between > 0.0 ? between : 0.0;
@@ -199,7 +202,10 @@ __global__ __launch_bounds__(1024) void k_energy_stats(const T* __restrict__ e, 
     out[1] = nn * m;
     out[2] = nn * m * m;
     out[3] = nn;
-    if (finalize) energy_stats_final(out);
+    if (finalize) {
+      out[4] = m;
+      out[5] = q / nn;
+    }
   }
 }
 __global__ void k_energy_stats_final(double* out) {
