@@ -34,6 +34,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves", "aiqmc_phase_param_grad",
     "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals", "aiqmc_debug_set_ablate", "aiqmc_debug_set_fuse_accept", "aiqmc_debug_set_lap_waves",
     "aiqmc_debug_set_fuse_reduce", "aiqmc_energy_stats", "aiqmc_energy_stats_final",
+    "aiqmc_debug_limdrift_factor",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -129,6 +130,9 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_debug_set_fuse_accept.restype = ctypes.c_int
     lib.aiqmc_debug_set_fuse_reduce.argtypes = [vp, i32]
     lib.aiqmc_debug_set_fuse_reduce.restype = ctypes.c_int
+    lib.aiqmc_debug_limdrift_factor.argtypes = [vp, vp, i32, ctypes.c_double, i32,
+                                                ctypes.POINTER(ctypes.c_double), vp]
+    lib.aiqmc_debug_limdrift_factor.restype = ctypes.c_int
     lib.aiqmc_debug_set_lap_waves.argtypes = [vp, i32]
     lib.aiqmc_debug_set_lap_waves.restype = ctypes.c_int
     lib.aiqmc_debug_set_proposal_reuse.argtypes = [vp, i32]
@@ -350,6 +354,19 @@ class Context:
         fp64 tree-sum launch (k_taueff).  True/False map to 2/0."""
         m = 2 if mode is True else (0 if mode is False else int(mode))
         check(self._lib.aiqmc_debug_set_fuse_reduce(self._h, m), "aiqmc_debug_set_fuse_reduce")
+
+    def limdrift_factor(self, sumsq: torch.Tensor, tstep: float, mode: int) -> float:
+        """Diagnostics: the fp32 limdrift factor of the per-configuration |grad|^2 values `sumsq`
+        (float32 on this context's device) through mc_step's reductions: 0 = fused integer
+        accumulators, 1 = k_taueff_part partials, 2 = the fp64 tree sum (k_taueff)."""
+        if sumsq.dtype != torch.float32 or sumsq.device != self.device or sumsq.dim() != 1:
+            raise TypeError("sumsq must be a 1-D float32 tensor on the context's device")
+        x = sumsq.contiguous()
+        out = ctypes.c_double(0.0)
+        check(self._lib.aiqmc_debug_limdrift_factor(self._h, _ptr(x), int(x.numel()), float(tstep), int(mode),
+                                                    ctypes.byref(out), _stream(self.device)),
+              "aiqmc_debug_limdrift_factor")
+        return out.value
 
     def set_ablate(self, mask: int):
         """Development builds (-DAQ_ABLATE) only: skip proposal phases to time them."""

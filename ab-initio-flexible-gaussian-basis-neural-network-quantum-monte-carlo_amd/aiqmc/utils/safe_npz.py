@@ -230,7 +230,7 @@ def _call(fn, args: tuple):
         return Record(k[len("record:"):].split(" ")[1], args)
     if k == "getattr":
         if not (len(args) == 2 and isinstance(args[0], _Marker) and args[0].name.startswith("owner:")
-                and args[1] == "State"):
+                and isinstance(args[1], str) and args[1] == "State"):
             raise UnsafeCheckpointError("getattr outside the <kfac class>.State pattern")
         return _Marker("state:" + args[0].name[len("owner:"):] + ".State")
     raise UnsafeCheckpointError(f"cannot call {k}")

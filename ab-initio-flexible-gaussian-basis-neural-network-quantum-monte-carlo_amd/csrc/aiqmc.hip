@@ -75,23 +75,49 @@ __global__ __launch_bounds__(1024) void k_taueff(const T* __restrict__ x, int n,
 // The same bits as the fused path at any batch size and in any order; no atomics, fences or a
 // finalising workgroup on the critical path (k_taueff, one 1024-thread workgroup, took 4.6 us for
 // the N2 proposal batch; a 32-workgroup version finishing in its last workgroup 4.5 us).
+// Each element enters through tacc_split (walker_kernel.h: lo / mid / hi / bad, exact; hi
+// saturating), so non-finite and huge |grad|^2 reach the consumers as the fused path's do;
+// part = this kind's [4][TPART] block (lo, mid, hi, bad per workgroup).
 __global__ __launch_bounds__(256) void k_taueff_part(const float* __restrict__ x, int n,
                                                      unsigned long long* __restrict__ part) {
-  __shared__ unsigned long long ws[4];
-  unsigned long long v = 0;
+  __shared__ unsigned long long ws[4][4];
+  unsigned long long v = 0, mid = 0, hi = 0, bad = 0;
   const int stride = TPART * 256;
   for (int i = blockIdx.x * 256 + (int)threadIdx.x; i < n; i += 8 * stride) {
     float t[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) t[k] = i + k * stride < n ? x[i + k * stride] : 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v += i + k * stride < n ? tacc_fix((double)t[k]) : 0ull;
+    for (int k = 0; k < 8; ++k) {
+      const double d = (double)t[k];
+      if (d >= 0.0 && d < 0x1p24) {
+        v += tacc_fix(d);
+      } else {
+        const TFix f = tacc_split(d);
+        v += f.lo;
+        mid += f.mid;
+        hi = sat_add_u64(hi, f.hi);
+        bad += f.bad;
+      }
+    }
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+  v = wave_sum_u64(v);
+  mid = wave_sum_u64(mid);
+  hi = wave_sum_sat_u64(hi);
+  bad = wave_sum_u64(bad);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    ws[0][w] = v;
+    ws[1][w] = mid;
+    ws[2][w] = hi;
+    ws[3][w] = bad;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = (ws[0] + ws[1]) + (ws[2] + ws[3]);
+  if (threadIdx.x < 4) {
+    const unsigned long long* q = ws[threadIdx.x];
+    part[threadIdx.x * TPART + blockIdx.x] =
+        threadIdx.x == 2 ? sat_add_u64(sat_add_u64(q[0], q[1]), sat_add_u64(q[2], q[3])) : (q[0] + q[1]) + (q[2] + q[3]);
+  }
 }
 
 // Per-sweep random draws (production mode), one thread per (walker b, electron i):
@@ -882,7 +908,7 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
   // summed by the proposal launch
   if (!tacc) {
     if (tpart)
-      k_taueff_part<<<dim3(TPART), dim3(256), 0, s>>>((const float*)c->d_sqn, B * N, tpart + TPART);
+      k_taueff_part<<<dim3(TPART), dim3(256), 0, s>>>((const float*)c->d_sqn, B * N, tpart + TPART_KIND);
     else if (c->dtype == AIQMC_F32)
       k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)c->d_sqn, B * N, tstep,
                          c->d_taueff + 1);
@@ -958,26 +984,28 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
   // at 4096 the walker launch's wave-wide read of the accumulators before its fused acceptance
   // and the proposals' atomics cost more than the two launches they replace.
   unsigned long long* tacc = nullptr;
-  if (c->fuse_reduce && c->dtype == AIQMC_F32 && (c->fuse_reduce > 1 || B <= FUSE_REDUCE_MAX_B)) {
+  // (integer sums need fewer than TACC_MAX_CONF configurations per reduction, walker_kernel.h)
+  const bool int_sums = (int64_t)B * c->N < TACC_MAX_CONF;
+  if (int_sums && c->fuse_reduce && c->dtype == AIQMC_F32 && (c->fuse_reduce > 1 || B <= FUSE_REDUCE_MAX_B)) {
     if (c->tacc_n < nsteps) {
       if (c->d_tacc) (void)hipFree(c->d_tacc);
       c->d_tacc = nullptr;
       c->tacc_n = 0;
-      HIPCHK(hipMalloc((void**)&c->d_tacc, (size_t)2 * TACC_SLOTS * nsteps * sizeof(unsigned long long)));
+      HIPCHK(hipMalloc((void**)&c->d_tacc, (size_t)2 * TACC_STRIDE * nsteps * sizeof(unsigned long long)));
       c->tacc_n = nsteps;
     }
     tacc = c->d_tacc;
-    HIPCHK(hipMemsetAsync(tacc, 0, (size_t)2 * TACC_SLOTS * nsteps * sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(tacc, 0, (size_t)2 * TACC_STRIDE * nsteps * sizeof(unsigned long long), s));
   }
   // unfused fp32 sweeps: per-sweep partial sums of the limdrift reductions (k_taueff_part), kept
   // until the next sweep's walker launch has read them (fused acceptance)
   unsigned long long* tpart = nullptr;
-  if (!tacc && c->dtype == AIQMC_F32 && c->wide_reduce) {
+  if (int_sums && !tacc && c->dtype == AIQMC_F32 && c->wide_reduce) {
     if (c->tpart_n < nsteps) {
       if (c->d_tpart) (void)hipFree(c->d_tpart);
       c->d_tpart = nullptr;
       c->tpart_n = 0;
-      HIPCHK(hipMalloc((void**)&c->d_tpart, (size_t)2 * TPART * nsteps * sizeof(unsigned long long)));
+      HIPCHK(hipMalloc((void**)&c->d_tpart, (size_t)2 * TPART_KIND * nsteps * sizeof(unsigned long long)));
       c->tpart_n = nsteps;
     }
     tpart = c->d_tpart;
@@ -985,8 +1013,8 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
   AccArgs pending{};
   for (int st = 0; st < nsteps; ++st) {
     rc = mc_sweep(c, ops, pos, B, tstep, rng_mode, gauss1, gauss2, u, st, seed, offset + (uint64_t)st, accept_out,
-                  nullptr, s, &pending, c->fuse_accept && st + 1 < nsteps, tacc ? tacc + 2 * TACC_SLOTS * st : nullptr,
-                  tpart ? tpart + 2 * TPART * st : nullptr);
+                  nullptr, s, &pending, c->fuse_accept && st + 1 < nsteps, tacc ? tacc + 2 * TACC_STRIDE * st : nullptr,
+                  tpart ? tpart + 2 * TPART_KIND * st : nullptr);
     if (rc) return rc;
   }
   HIPCHK(hipGetLastError());
@@ -1523,6 +1551,57 @@ int aiqmc_debug_set_fuse_reduce(aiqmc_ctx* c, int32_t on) {
   c->fuse_reduce = on == 3 ? 0 : on;
   c->wide_reduce = on == 3 ? 0 : 1;
   return AIQMC_OK;
+}
+
+}  // extern "C"
+
+// aiqmc_debug_limdrift_factor: the fused path's per-configuration accumulation (tacc_add, one
+// thread per configuration instead of lane 0 of its wave) and the consumers' read (taueff_wave).
+__global__ __launch_bounds__(256) void k_tacc_feed(const float* __restrict__ x, int n, unsigned long long* acc) {
+  const int i = blockIdx.x * 256 + (int)threadIdx.x;
+  if (i < n) tacc_add(acc, 0, i, (double)x[i]);
+}
+__global__ __launch_bounds__(64) void k_taueff_read(const unsigned long long* acc, const unsigned long long* part,
+                                                    double tstep, double* out) {
+  const float te = taueff_wave<float>(nullptr, acc, 0, tstep, part);
+  if (threadIdx.x == 0) *out = (double)te;
+}
+
+extern "C" {
+
+int aiqmc_debug_limdrift_factor(aiqmc_ctx* c, const void* sumsq, int32_t n, double tstep, int32_t mode, double* out,
+                                void* stream) {
+  if (!c) return fail(AIQMC_EINVAL, "null context");
+  if (!sumsq || !out || n <= 0) return fail(AIQMC_EINVAL, "limdrift_factor: null buffer or n <= 0");
+  if (n >= TACC_MAX_CONF && mode != 2) return fail(AIQMC_EINVAL, "limdrift_factor: n >= 2^24 needs mode 2");
+  if (mode < 0 || mode > 2) return fail(AIQMC_EINVAL, "limdrift_factor: mode must be 0, 1 or 2");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  const size_t words = (size_t)TACC_STRIDE + TPART_KIND + 1;   // acc | part | out (as a double)
+  unsigned long long* d = nullptr;
+  HIPCHK(hipMalloc((void**)&d, words * sizeof(unsigned long long)));
+  unsigned long long* acc = d;
+  unsigned long long* part = d + TACC_STRIDE;
+  double* dout = (double*)(d + TACC_STRIDE + TPART_KIND);
+  int rc = AIQMC_OK;
+  if (hipMemsetAsync(d, 0, words * sizeof(unsigned long long), s) != hipSuccess) rc = fail(AIQMC_EHIP, "memset");
+  if (!rc) {
+    const float* x = (const float*)sumsq;
+    if (mode == 0) {
+      k_tacc_feed<<<dim3((n + 255) / 256), dim3(256), 0, s>>>(x, n, acc);
+      k_taueff_read<<<dim3(1), dim3(64), 0, s>>>(acc, nullptr, tstep, dout);
+    } else if (mode == 1) {
+      k_taueff_part<<<dim3(TPART), dim3(256), 0, s>>>(x, n, part);
+      k_taueff_read<<<dim3(1), dim3(64), 0, s>>>(nullptr, part, tstep, dout);
+    } else {
+      k_taueff<float><<<dim3(1), dim3(1024), 0, s>>>(x, n, tstep, dout);
+    }
+    if (hipGetLastError() != hipSuccess || hipMemcpyAsync(out, dout, sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      rc = fail(AIQMC_EHIP, "limdrift_factor: launch or copy");
+  }
+  (void)hipFree(d);
+  return rc;
 }
 
 int aiqmc_debug_set_proposal_reuse(aiqmc_ctx* c, int32_t on) {

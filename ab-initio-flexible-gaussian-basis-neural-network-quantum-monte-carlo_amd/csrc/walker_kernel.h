@@ -45,15 +45,72 @@ constexpr int MODE_GRAD_FWD = 3;   // forward-mode gradient (diagnostics / cross
 // (TACC_SCALE).  Integer
 // addition is exact and associative, so the sums -- and the limdrift factor every consumer
 // derives from them -- are bit-for-bit the same in any arrival order.  The quantum is far below
-// the float rounding of v2 (>= ~1 per configuration); an accumulator holds up to 2.8e14.  Two
-// launches and two inter-kernel gaps fewer per sweep.
+// the float rounding of v2 (>= ~1 per configuration).  Two launches and two inter-kernel gaps
+// fewer per sweep.
+//
+// Range (VERDICT r3 "weak" #2): v is a float (the reference's dtype, jnp.sum(g**2) at
+// VMCmcstep.py:12), so it is +inf, NaN or finite below 2^128.  It enters as three exact integers,
+//   lo  = (v mod 2^24) in units of 2^-16   (< 2^40; the only non-zero part for v < 2^24),
+//   mid = floor(v / 2^24) mod 2^40         (units of 2^24),
+//   hi  = floor(v / 2^64)                  (units of 2^64, < 2^64),
+// lo into one of the TACC_SLOTS slots, mid / hi / a "bad" count into three shared words after
+// them (rare: only configurations with v >= 2^24 ~ 1.7e7 touch them).  lo and mid cannot wrap
+// for fewer than 2^24 configurations per reduction (the host checks); hi saturates (a wrap of
+// its word counts as bad), which only happens when the exact total is >= 2^128, where the
+// reference's float sum is +inf.  A non-finite v counts as bad.  The consumers form
+//   v2 = lo 2^-16 + mid 2^24 + hi 2^64  (= NaN if bad > 0)
+// and the factor from (float)v2: +inf v2 (float overflow) and NaN both give a NaN factor, as the
+// reference's (sqrt(1 + 2 tau a v2) - 1) / (a v2) does for an inf or NaN sum.  With mid = hi =
+// bad = 0 (every ordinary sweep) v2 is exactly the round-3 integer sum.
 constexpr double TACC_SCALE = 65536.0;
 constexpr int TACC_SLOTS = 1024;
-__device__ __forceinline__ unsigned long long tacc_fix(double x) {
+constexpr int TACC_STRIDE = TACC_SLOTS + 64;   // per kind: lo slots, then [mid, hi, bad, 0 ...]
+constexpr int TACC_MID = TACC_SLOTS, TACC_HI = TACC_SLOTS + 1, TACC_BAD = TACC_SLOTS + 2;
+constexpr int TACC_MAX_CONF = 1 << 24;          // configurations per reduction (lo / mid headroom)
+__device__ __forceinline__ unsigned long long tacc_fix(double x) {   // 0 <= x < 2^24
   return (unsigned long long)(x * TACC_SCALE + 0.5);
 }
+__device__ __forceinline__ unsigned long long sat_add_u64(unsigned long long a, unsigned long long b) {
+  const unsigned long long s = a + b;
+  return s < a ? ~0ull : s;
+}
+// The exact split of v >= 2^24 (or non-finite: bad = 1).  Every step is exact in double: v is a
+// float, h 2^64 and m 2^24 are multiples of its ulp, and r, l are representable.
+struct TFix {
+  unsigned long long lo, mid, hi, bad;
+};
+__device__ __forceinline__ TFix tacc_split(double v) {
+  TFix f{0ull, 0ull, 0ull, 0ull};
+  if (v >= 0.0 && v < 0x1p24) {
+    f.lo = tacc_fix(v);
+  } else if (v >= 0.0 && v < 0x1p128) {
+    const double h = floor(v * 0x1p-64);
+    const double r = v - h * 0x1p64;
+    const double m = floor(r * 0x1p-24);
+    f.lo = tacc_fix(r - m * 0x1p24);
+    f.mid = (unsigned long long)m;
+    f.hi = (unsigned long long)h;
+  } else {
+    f.bad = 1ull;   // +inf, NaN (or a negative value, which a sum of squares never is)
+  }
+  return f;
+}
+__device__ __noinline__ void tacc_add_big(unsigned long long* a, int conf, double v) {
+  TFix f = tacc_split(v);
+  if (f.lo) atomicAdd(a + (conf & (TACC_SLOTS - 1)), f.lo);
+  if (f.mid) atomicAdd(a + TACC_MID, f.mid);
+  if (f.hi) {
+    const unsigned long long old = atomicAdd(a + TACC_HI, f.hi);
+    if (old + f.hi < old) f.bad = 1ull;   // the word wrapped: exact total >= 2^128
+  }
+  if (f.bad) atomicAdd(a + TACC_BAD, f.bad);
+}
 __device__ __forceinline__ void tacc_add(unsigned long long* acc, int kind, int conf, double v) {
-  atomicAdd(acc + kind * TACC_SLOTS + (conf & (TACC_SLOTS - 1)), tacc_fix(v));
+  unsigned long long* a = acc + kind * TACC_STRIDE;
+  if (v >= 0.0 && v < 0x1p24)
+    atomicAdd(a + (conf & (TACC_SLOTS - 1)), tacc_fix(v));
+  else
+    tacc_add_big(a, conf, v);
 }
 // taueff = (sqrt(1 + 2 tau a v2) - 1) / (a v2), a = 0.25, in T (k_taueff's arithmetic)
 template <typename T> __device__ __forceinline__ T taueff_from_v2(double v2, double tstep) {
@@ -61,30 +118,54 @@ template <typename T> __device__ __forceinline__ T taueff_from_v2(double v2, dou
   const T v2t = (T)v2;
   return (sqrt((T)1 + (T)2 * (T)tstep * (T)a * v2t) - (T)1) / ((T)a * v2t);
 }
+__device__ __forceinline__ double tacc_v2(unsigned long long lo, unsigned long long mid, unsigned long long hi,
+                                          unsigned long long bad) {
+  if (bad) return __builtin_nan("");
+  return (double)lo * (1.0 / TACC_SCALE) + (double)mid * 0x1p24 + (double)hi * 0x1p64;
+}
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+__device__ __forceinline__ unsigned long long wave_sum_sat_u64(unsigned long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = sat_add_u64(v, __shfl_xor(v, off));
+  return v;
+}
 // Limdrift factor k (0: walkers, 1: proposals) of the sweep: the sum of the fused accumulators
 // (one slot per lane, exact integer wave sum) or k_taueff's result.  Every lane of the wave must
 // be active (call it outside divergent code); the result is wave-uniform.
-// part (unfused fp32 sweeps): the TPART partial sums of k_taueff_part for both kinds [2][TPART],
-// the same integers as the fused accumulators, summed here (one load per lane).
+// part (unfused fp32 sweeps): the TPART partial sums of k_taueff_part, per kind [4][TPART] =
+// lo, mid, hi, bad (the same integers as the fused accumulators), summed here (two loads per lane).
 constexpr int TPART = 32;
+constexpr int TPART_KIND = 4 * TPART;
 template <typename T>
 __device__ __forceinline__ T taueff_wave(const double* te, const unsigned long long* acc, int k, double tstep,
                                          const unsigned long long* part = nullptr) {
+  const int l = (int)(threadIdx.x & 63);
   if (part) {
-    const int l = (int)(threadIdx.x & 63);
-    unsigned long long v = l < TPART ? part[k * TPART + l] : 0ull;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    return taueff_from_v2<T>((double)v * (1.0 / TACC_SCALE), tstep);
+    const unsigned long long* p = part + k * TPART_KIND;
+    const unsigned long long x0 = p[l];        // lanes < 32: lo partials, lanes >= 32: mid
+    const unsigned long long x1 = p[64 + l];   // lanes < 32: hi partials, lanes >= 32: bad
+    if (!__any(x1 != 0ull || (l >= TPART && x0 != 0ull)))
+      return taueff_from_v2<T>(tacc_v2(wave_sum_u64(x0), 0ull, 0ull, 0ull), tstep);
+    const unsigned long long lo = wave_sum_u64(l < TPART ? x0 : 0ull);
+    const unsigned long long mid = wave_sum_u64(l < TPART ? 0ull : x0);
+    const unsigned long long hi = wave_sum_sat_u64(l < TPART ? x1 : 0ull);
+    const unsigned long long bad = wave_sum_u64(l < TPART ? 0ull : x1);
+    return taueff_from_v2<T>(tacc_v2(lo, mid, hi, bad), tstep);
   }
   if (!acc) return (T)te[k];
-  const unsigned long long* a = acc + k * TACC_SLOTS + (int)(threadIdx.x & 63);
+  const unsigned long long* a = acc + k * TACC_STRIDE;
   unsigned long long v = 0;
 #pragma unroll
-  for (int j = 0; j < TACC_SLOTS / 64; ++j) v += a[64 * j];
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return taueff_from_v2<T>((double)v * (1.0 / TACC_SCALE), tstep);
+  for (int j = 0; j < TACC_SLOTS / 64; ++j) v += a[l + 64 * j];
+  const unsigned long long x = a[TACC_SLOTS + l];   // lane 0: mid, 1: hi, 2: bad
+  v = wave_sum_u64(v);
+  if (!__any(x != 0ull)) return taueff_from_v2<T>(tacc_v2(v, 0ull, 0ull, 0ull), tstep);
+  const unsigned long long mid = __shfl(x, 0), hi = __shfl(x, 1), bad = __shfl(x, 2);
+  return taueff_from_v2<T>(tacc_v2(v, mid, hi, bad), tstep);
 }
 
 struct AccArgs {
@@ -96,8 +177,8 @@ struct AccArgs {
   const void* gauss2;     // [B][N][3]
   const void* u;          // [B][N]
   const double* taueff;   // [2]
-  const unsigned long long* tacc;   // [2][TACC_SLOTS] fused accumulators of the sweep (nullptr: taueff)
-  const unsigned long long* tpart;  // [2][TPART] k_taueff_part sums of the sweep (unfused fp32), or nullptr
+  const unsigned long long* tacc;   // [2][TACC_STRIDE] fused accumulators of the sweep (nullptr: taueff)
+  const unsigned long long* tpart;  // [2][TPART_KIND] k_taueff_part sums of the sweep (unfused fp32), or nullptr
   double tstep;
   int32_t* count;         // [B] accepted moves (optional)
 };
@@ -153,11 +234,11 @@ struct KArgs {
   const void* pgrad;      // [B][3N] grad log|psi| at the walkers
   const void* gauss1;     // [B][3N] standard normals (host draws or k_draws output)
   const double* taueff;   // device scalar: limdrift factor of pgrad (VMCmcstep.py:11-14)
-  // fused limdrift accumulators of the sweep [2][TACC_SLOTS] (fp32 mc_step; nullptr elsewhere):
+  // fused limdrift accumulators of the sweep [2][TACC_STRIDE] (fp32 mc_step; nullptr elsewhere):
   // walker launches add their |grad|^2 to kind 0, proposal launches to kind 1; readers of the
   // walker factor (moved electron, proposals from scratch) sum kind 0 (taueff_wave)
   unsigned long long* tacc;
-  const unsigned long long* tpart;   // [2][TPART] partial sums of k_taueff_part (read by taueff_wave)
+  const unsigned long long* tpart;   // [2][TPART_KIND] partial sums of k_taueff_part (read by taueff_wave)
   double tstep;
   uint64_t seed, step;
   // single-electron-move layout (proposal != 0, k_walker_rev / k_moved_electron): configuration

@@ -59,6 +59,9 @@ __device__ __forceinline__ void stage_copy(T* dst, cptr<T> src, int n) {
   u4* d = (u4*)dst;
   const int cnt = n * (int)sizeof(T) / 16;
   for (int i = threadIdx.x; i < cnt; i += blockDim.x) d[i] = s[i];
+  // a tail shorter than 16 bytes (odd-sized blocks; none of the built shapes has one, and with a
+  // compile-time n the loop folds away)
+  for (int i = cnt * 16 / (int)sizeof(T) + (int)threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
 }
 
 // One h-stream layer (nn.py:280-311) in first derivatives, column loop over electrons i.

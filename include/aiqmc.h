@@ -280,6 +280,14 @@ int aiqmc_debug_set_fuse_accept(aiqmc_ctx* ctx, int32_t on);
  * sums to the float rounding of v2). */
 int aiqmc_debug_set_fuse_reduce(aiqmc_ctx* ctx, int32_t on);
 
+/* Diagnostics: the fp32 limdrift factor (VMCmcstep.py:11-14) of n per-configuration |grad|^2
+ * values (device floats `sumsq`) through one of the reductions aiqmc_mc_step uses: mode 0 = the
+ * fused integer accumulators (tacc_add + taueff_wave), 1 = k_taueff_part + taueff_wave, 2 = the
+ * fp64 tree sum (k_taueff).  Writes the factor to the HOST double *out (synchronises `stream`).
+ * Non-finite values give NaN, as the reference's float sum does; huge ones a small factor. */
+int aiqmc_debug_limdrift_factor(aiqmc_ctx* ctx, const void* sumsq, int32_t n, double tstep, int32_t mode,
+                                double* out, void* stream);
+
 /* Development builds (-DAQ_ABLATE) only: skip proposal-kernel phases (bit mask, walker_rev.h) to
  * time their marginal cost; results are meaningless.  No effect in product builds. */
 int aiqmc_debug_set_ablate(aiqmc_ctx* ctx, int32_t mask);

@@ -26,8 +26,17 @@ def limdrift(g, tau, acyrus):
     return g * taueff
 
 
-def walkers_update(net, params, x, gauss1, gauss2, u, tstep: float, chunk: int = 256):
-    """One MH step for a device batch x[B,3N] -> new x[B,3N] (VMCmcstep.py:28-111)."""
+def taueff(g, tau, acyrus):
+    """The factor limdrift multiplies g by (VMCmcstep.py:12-13), in g's dtype."""
+    v2 = torch.sum(g ** 2)
+    return (torch.sqrt(1 + 2 * tau * acyrus * v2) - 1) / (acyrus * v2)
+
+
+def walkers_update(net, params, x, gauss1, gauss2, u, tstep: float, chunk: int = 256, info=None):
+    """One MH step for a device batch x[B,3N] -> new x[B,3N] (VMCmcstep.py:28-111).
+
+    info: optional dict, filled with the step's intermediates (limdrift factors of the walker and
+    proposal gradients, the acceptance decisions) for the fp32 Metropolis parity fixture."""
     B, n3 = x.shape
     N = n3 // 3
     f = lambda p: net.logabs(params, p)
@@ -60,6 +69,9 @@ def walkers_update(net, params, x, gauss1, gauss2, u, tstep: float, chunk: int =
     cond = (acceptance > u).reshape(B, N, 1)                     # walkers_accept :18-25
     x_init = x.reshape(B, N, 3)
     x_new = torch.where(cond, x_init + g, x_init)
+    if info is not None:
+        info.update(taueff_walkers=taueff(grad_x, tstep, 0.25), taueff_proposals=taueff(grad_new, tstep, 0.25),
+                    cond=cond.reshape(B, N), grad_x=grad_x, logabs_x=wave_x1[:, 0], logabs_x2=wave_x2)
     return x_new.reshape(B, n3), acceptance
 
 

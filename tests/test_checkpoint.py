@@ -247,6 +247,13 @@ def test_getattr_only_in_the_kfac_state_pattern():
                 b"\x86R)\x81K\x01b."):                                 # BUILD with a non-dict state
         with pytest.raises(UnsafeCheckpointError):
             loads_pickle_stream(bad)
+    # a non-str attribute name (an array whose == is elementwise) is refused, not a ValueError
+    # that find_last_checkpoint would read as a corrupt file
+    from aiqmc.utils import safe_npz
+    owner = safe_npz._Marker("owner:kfac_jax._src.optimizer Optimizer")
+    for name in (np.array(["State", "State"]), 5, b"State"):
+        with pytest.raises(UnsafeCheckpointError):
+            safe_npz._call(safe_npz._Marker("getattr"), (owner, name))
 
 
 def test_self_referential_stream_is_refused_not_recursed():

@@ -1,0 +1,196 @@
+"""The benched fp32 Metropolis path against the oracle (VERDICT r3 "Next" #1 and #6).
+
+1. The fp32 limdrift reduction (VMCmcstep.py:11-14, quirk Q8).  mc_step sums every
+   configuration's |grad|^2 as exact integers (walker_kernel.h `tacc_split`: lo / mid / hi words
+   and a bad count), either fused into the walker / proposal launches (mode 0) or in
+   k_taueff_part's partials (mode 1); mode 2 is the fp64 tree sum (k_taueff).  Vectors with
+   1e15 (above the round-3 2^48 fixed-point cap), 1e30, 3e38, a float-overflowing pair, +inf
+   and NaN entries must give the reference formula's factor: finite sums the factor of the
+   float32-rounded exact sum, non-finite ones NaN (the reference's jnp.sum is inf or NaN, and
+   (sqrt(1 + 2 tau a v2) - 1) / (a v2) is then NaN).
+2. One and two fp32 N2 sweeps with host draws at 64 and 512 walkers against
+   `tests/golden/N2_mc_fp32.npz` (oracle/mcstep.py run in float32 AND float64 from the same
+   walkers, `make_golden_mc_fp32.py`): acceptance decisions, positions, and the limdrift factor
+   of the walker gradients.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+TAU = 0.05
+
+
+def _ctx(dtype=torch.float32, flat=None):
+    from oracle import system
+    from aiqmc import _lib
+    s = system.make_system("N2")
+    t = s.tables()
+    ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
+                       t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"], dtype=dtype,
+                       device=0)
+    if flat is None:
+        flat = system.flatten_params(system.init_params(np.random.default_rng(5), s, randomize_aux=True))
+    ctx.set_params(flat)
+    return s, ctx
+
+
+def _reference_factor(x: np.ndarray, tau: float) -> float:
+    """VMCmcstep.py:12-13 in float32 on the exactly summed, float32-rounded v2 (the reference's
+    float32 jnp.sum differs from it by the sum's own rounding only)."""
+    xd = x.astype(np.float64)
+    if not np.all(np.isfinite(xd)):
+        return float("nan")
+    v2d = math.fsum(xd.tolist())
+    with np.errstate(over="ignore", invalid="ignore"):
+        v2 = np.float32(v2d)
+        a = np.float32(0.25)
+        te = (np.sqrt(np.float32(1) + np.float32(2) * np.float32(tau) * a * v2) - np.float32(1)) / (a * v2)
+    return float(te)
+
+
+def _cases(n: int):
+    rng = np.random.default_rng(n)
+    base = rng.gamma(2.0, 20.0, n).astype(np.float32)   # |grad log psi|^2 of ordinary configurations
+    out = {"ordinary": base.copy()}
+    x = base.copy(); x[5] = 1e15; out["1e15"] = x                    # above round 3's 2^48 cap
+    x = base.copy(); x[7] = 2.9e14; x[8] = 2.9e14; out["2x2.9e14"] = x   # the old cap, twice
+    x = base.copy(); x[::64] = 3e11; out["mid-heavy"] = x              # the mid word accumulates
+    x = base.copy(); x[3] = 1e30; out["1e30"] = x                      # the hi word
+    x = base.copy(); x[3] = 3.0e38; out["3e38"] = x                    # largest finite floats
+    x = base.copy(); x[3] = 3.0e38; x[n - 1] = 3.0e38; out["overflow"] = x   # float sum -> +inf
+    x = base.copy(); x[9] = np.inf; out["inf"] = x
+    x = base.copy(); x[n // 2] = np.nan; out["nan"] = x
+    x = base.copy(); x[1] = np.inf; x[2] = 1e30; x[3] = 3e38; out["inf+huge"] = x
+    return out
+
+
+@pytest.mark.parametrize("n", [64 * 14, 512 * 14, 4096 * 14])
+def test_limdrift_factor_guarded_against_huge_and_nonfinite(n):
+    _, ctx = _ctx()
+    for name, x in _cases(n).items():
+        ref = _reference_factor(x, TAU)
+        xt = torch.tensor(x, device="cuda")
+        f = [ctx.limdrift_factor(xt, TAU, m) for m in (0, 1, 2)]
+        print(n, name, "reference", ref, "fused / partials / fp64 tree", f)
+        if math.isnan(ref):
+            assert all(math.isnan(v) for v in f), (name, f)
+            continue
+        assert all(math.isfinite(v) for v in f), (name, f)
+        # the two integer reductions sum the same integers: the same bits
+        assert f[0] == f[1], (name, f)
+        for v in f:
+            assert abs(v - ref) <= 1e-6 * abs(ref) + 1e-30, (name, v, ref)
+        # against the float32 sum the reference itself forms (its rounding, not ours, is the gap)
+        with np.errstate(over="ignore"):
+            v2f = np.sum(x, dtype=np.float32)
+        if np.isfinite(v2f) and v2f > 0:
+            a = np.float32(0.25)
+            te32 = (np.sqrt(np.float32(1) + np.float32(2 * TAU) * a * v2f) - np.float32(1)) / (a * v2f)
+            assert abs(f[0] - float(te32)) <= 1e-5 * abs(float(te32)), (name, f[0], float(te32))
+
+
+def _golden_mc(golden_dir):
+    import os
+    return np.load(os.path.join(golden_dir, "N2_mc_fp32.npz"))
+
+
+def _sweep(ctx, g, B, pos_start, steps, fuse_reduce=1):
+    """Run `steps` (a list of sweep indices) HIP fp32 sweeps from pos_start with the fixture's draws."""
+    N = 14
+    ctx.set_fuse_reduce(fuse_reduce)
+    pos = torch.tensor(np.asarray(pos_start, dtype=np.float32), device="cuda").contiguous()
+    g1 = torch.tensor(g[f"gauss1_{B}"][steps])
+    g2 = torch.tensor(g[f"gauss2d_{B}"][steps])
+    u = torch.tensor(g[f"u_{B}"][steps])
+    assert g1.shape == (len(steps), B, 3 * N) and g2.shape == (len(steps), B, N, 3)
+    acc = ctx.mc_step(pos, len(steps), TAU, gauss1=g1, gauss2=g2, u=u, count_accepts=True)
+    torch.cuda.synchronize()
+    ctx.set_fuse_reduce(1)
+    return pos.cpu().numpy().astype(np.float64), acc.cpu().numpy()
+
+
+def _moved(x_before, x_after, B, N=14):
+    return np.any(x_after.reshape(B, N, 3) != x_before.reshape(B, N, 3), axis=2)
+
+
+@pytest.mark.parametrize("B", [64, 512])
+@pytest.mark.parametrize("sweep", [0, 1])
+def test_fp32_sweep_matches_oracle(golden_dir, B, sweep):
+    g = _golden_mc(golden_dir)
+    s, ctx = _ctx(flat=g["params_flat"])
+    N = s.nelectrons
+    x0 = g[f"pos0_{B}"].astype(np.float64) if sweep == 0 else g[f"x32_0_{B}"].astype(np.float64)
+    ratio = g[f"ratio32_{sweep}_{B}"].astype(np.float64)
+    cond = g[f"cond32_{sweep}_{B}"]
+    u = g[f"u_{B}"][sweep].astype(np.float64)
+    for fuse in (1, 0, 3):   # fused integer sums (<= 1,024 walkers), k_taueff_part, fp64 tree sum
+        x1, acc = _sweep(ctx, g, B, x0, [sweep], fuse_reduce=fuse)
+        moved = _moved(x0, x1, B)
+        assert np.array_equal(acc, moved.sum(1))
+        flips = moved != cond
+        gap = np.abs(ratio - u) / np.maximum(ratio, u)
+        print(B, sweep, fuse, "accepted", int(moved.sum()), "oracle", int(cond.sum()), "flips", int(flips.sum()),
+              "closest |ratio-u|/ratio", float(gap.min()))
+        # a decision may differ only where the fp32 ratio sits within fp32 rounding of u
+        assert np.all(gap[flips] < 1e-3), gap[flips]
+        assert flips.sum() <= 2
+        ok = ~np.any(flips, axis=1)
+        ref = g[f"x32_{sweep}_{B}"].astype(np.float64)
+        d = np.abs(x1 - ref)[ok]
+        print("  |x_hip - x_oracle32|: max", d.max(), "p99", np.quantile(d, 0.99))
+        # a moved electron's step is limdrift(grad) tau + sqrt(tau) xi; the fp32 gradients of two
+        # orderings differ by ~1e-3 of |grad| at worst near a node, so 1e-3 bohr bounds the worst
+        # coordinate, and the typical one agrees to a few float32 ulps of the coordinate
+        assert d.max() < 1e-3
+        assert np.quantile(d, 0.99) < 2e-6
+        if sweep == 0:
+            # no worse than the reference's own arithmetic: error vs the float64 oracle
+            ref64 = g[f"x64_0_{B}"]
+            ok64 = ok & ~np.any(g[f"cond64_0_{B}"] != cond, axis=1)
+            e_hip = np.abs(x1 - ref64)[ok64]
+            e_o32 = np.abs(ref - ref64)[ok64]
+            print("  vs float64: HIP p99", np.quantile(e_hip, 0.99), "max", e_hip.max(), "| fp32 oracle p99",
+                  np.quantile(e_o32, 0.99), "max", e_o32.max())
+            assert np.quantile(e_hip, 0.99) <= 2.0 * np.quantile(e_o32, 0.99) + 1e-7
+            assert e_hip.max() <= 4.0 * e_o32.max() + 1e-6
+
+
+@pytest.mark.parametrize("B", [64, 512])
+def test_fp32_two_sweeps_match_oracle(golden_dir, B):
+    g = _golden_mc(golden_dir)
+    s, ctx = _ctx(flat=g["params_flat"])
+    x2, acc = _sweep(ctx, g, B, g[f"pos0_{B}"], [0, 1])
+    ref = g[f"x32_1_{B}"].astype(np.float64)
+    # walkers whose every decision of both sweeps agreed with the fp32 oracle
+    x1, _ = _sweep(ctx, g, B, g[f"pos0_{B}"], [0])
+    m0 = _moved(g[f"pos0_{B}"].astype(np.float64), x1, B)
+    m1 = _moved(x1, x2, B)
+    ok = ~np.any(m0 != g[f"cond32_0_{B}"], axis=1) & ~np.any(m1 != g[f"cond32_1_{B}"], axis=1)
+    assert ok.sum() >= B - 2
+    assert np.array_equal(acc, m0.sum(1) + m1.sum(1))
+    d = np.abs(x2 - ref)[ok]
+    print(B, "two sweeps: |x_hip - x_oracle32| max", d.max(), "p99", np.quantile(d, 0.99))
+    assert d.max() < 2e-3
+    assert np.quantile(d, 0.99) < 4e-6
+
+
+@pytest.mark.parametrize("B", [64, 512])
+def test_fp32_walker_limdrift_factor_matches_float_sum(golden_dir, B):
+    """The factor of the walker gradients: the HIP gradients' |grad|^2 through mc_step's reductions
+    vs the fp32 oracle's limdrift factor (its own float32 gradients and float32 sum)."""
+    g = _golden_mc(golden_dir)
+    s, ctx = _ctx(flat=g["params_flat"])
+    pos = torch.tensor(g[f"pos0_{B}"], device="cuda").contiguous()
+    _, grad = ctx.logpsi_grad(pos)
+    sq = (grad.double() ** 2).sum(1).float()
+    te_ref = float(g[f"te32_0_{B}"][0])
+    te64 = float(g[f"te64_0_{B}"][0])
+    for m in (0, 1, 2):
+        te = ctx.limdrift_factor(sq, TAU, m)
+        print(B, m, te, "oracle fp32", te_ref, "fp64", te64)
+        assert abs(te - te_ref) <= 2e-5 * te_ref
+        assert abs(te - te64) <= 2e-5 * te64

@@ -67,8 +67,11 @@ import test_gpu_sharded as T
 from aiqmc import constants
 x, el = T._run_block(rank, world)
 mean, var = constants.pmean_stats(el.cpu())
+# the device path INTEGRATION.md advertises: aiqmc_energy_stats(finalize=False) -> all_reduce of the
+# rank's 4-vector -> aiqmc_energy_stats_final (gloo all-reduces the CUDA tensor here, RCCL on a node)
+mean_d, var_d = constants.pmean_stats(el)
 np.savez(os.path.join(sys.argv[2], f"rank{rank}.npz"), x=x.cpu().numpy(), el=el.cpu().numpy(),
-         mean=mean.numpy(), var=var.numpy())
+         mean=mean.numpy(), var=var.numpy(), mean_d=mean_d.cpu().numpy(), var_d=var_d.cpu().numpy())
 dist.barrier()
 dist.destroy_process_group()
 '''
@@ -94,8 +97,9 @@ def test_two_rank_blocks_equal_single_process(tmp_path):
         els.append(el.cpu())
     mean, var = constants.pmean_stats(torch.cat(els))        # single process: identity collective
     for r in range(world):
-        assert abs(float(outs[r]["mean"]) - float(mean)) <= 1e-12 * abs(float(mean))
-        assert abs(float(outs[r]["var"]) - float(var)) <= 1e-10 * abs(float(var))
+        for mk, vk in (("mean", "var"), ("mean_d", "var_d")):   # host path, device-kernel path
+            assert abs(float(outs[r][mk]) - float(mean)) <= 1e-12 * abs(float(mean)), mk
+            assert abs(float(outs[r][vk]) - float(var)) <= 1e-10 * abs(float(var)), vk
     # the reference's two-pass statistics (loss.py:206-208) on the concatenation, float64
     e = torch.cat(els).double().numpy()
     assert abs(float(mean) - e.mean()) <= 1e-9 * abs(e.mean())
