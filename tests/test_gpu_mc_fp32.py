@@ -142,11 +142,11 @@ def test_fp32_sweep_matches_oracle(golden_dir, B, sweep):
         ref = g[f"x32_{sweep}_{B}"].astype(np.float64)
         d = np.abs(x1 - ref)[ok]
         print("  |x_hip - x_oracle32|: max", d.max(), "p99", np.quantile(d, 0.99))
-        # a moved electron's step is limdrift(grad) tau + sqrt(tau) xi; the fp32 gradients of two
-        # orderings differ by ~1e-3 of |grad| at worst near a node, so 1e-3 bohr bounds the worst
-        # coordinate, and the typical one agrees to a few float32 ulps of the coordinate
-        assert d.max() < 1e-3
-        assert np.quantile(d, 0.99) < 2e-6
+        # a moved electron's step is limdrift(grad) tau + sqrt(tau) xi: two fp32 orderings of the
+        # gradient and the factor.  Measured on MI355X (profiles/r04_s1_mc_fp32.txt): max 2.4e-7,
+        # p99 6e-8 bohr -- one or two float32 ulps of the coordinate
+        assert d.max() < 1e-5
+        assert np.quantile(d, 0.99) < 5e-7
         if sweep == 0:
             # no worse than the reference's own arithmetic: error vs the float64 oracle
             ref64 = g[f"x64_0_{B}"]
@@ -174,8 +174,8 @@ def test_fp32_two_sweeps_match_oracle(golden_dir, B):
     assert np.array_equal(acc, m0.sum(1) + m1.sum(1))
     d = np.abs(x2 - ref)[ok]
     print(B, "two sweeps: |x_hip - x_oracle32| max", d.max(), "p99", np.quantile(d, 0.99))
-    assert d.max() < 2e-3
-    assert np.quantile(d, 0.99) < 4e-6
+    assert d.max() < 2e-5      # measured 2.4e-7
+    assert np.quantile(d, 0.99) < 1e-6
 
 
 @pytest.mark.parametrize("B", [64, 512])
