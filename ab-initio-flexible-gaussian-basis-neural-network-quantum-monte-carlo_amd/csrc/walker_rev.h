@@ -762,15 +762,34 @@ k_walker_rev(KArgs ka) {
   const int ic = ilive ? fi : N - 1;
   const bool inG1 = ic >= nup;
   T hreg = T(0);
+  // fp32 proposals with 13 <= N <= 16 (4 rows per lane in F5's register layout = the 16x16 MFMA
+  // accumulator layout): Phi = h^3 W + b on the matrix cores (F5 below).  Round 4, interleaved A/B
+  // on one box (N2, 4096 walkers, µs per proposal launch): 224.2-225.1 -> 219.1-221.9, the
+  // 16 orbital-weight VGPRs of the VALU form replaced by 4 (profiles/r04_s2_ab_mfma.txt)
+#ifndef AQ_NO_PHI_MFMA
+  constexpr bool phi_mfma = PROP && sizeof(T) == 4 && (N + 3) / 4 == 4 && NH == 4;
+#else
+  constexpr bool phi_mfma = false;
+#endif
   // PROP: F5's orbital-weight column (lane column ccl of the spin-stacked [W_up; W_down] and both
   // biases), issued during F4's last layer so that F5 finds it loaded
   using V2o = typename Pair<T>::type;
   V2o ow[8], obs[2];
+  T owm[4];   // phi_mfma: the MFMA B operand W_s[f = lane >> 4][c = lane & 15] (re, im) of both spins
   auto orb_load = [&]() {
     const int cl = (lane & 15) < N ? (lane & 15) : N - 1;
     const cptr<T> wcol = P + 2 * cl;
+    if constexpr (phi_mfma) {
+      const int fq = lane >> 4;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) ow[s] = pair_make<T>(wcol[Ly::orb_w + s * N * 2], wcol[Ly::orb_w + s * N * 2 + 1]);
+      for (int s = 0; s < 2; ++s) {
+        owm[2 * s] = wcol[Ly::orb_w + (s * 4 + fq) * N * 2];
+        owm[2 * s + 1] = wcol[Ly::orb_w + (s * 4 + fq) * N * 2 + 1];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) ow[s] = pair_make<T>(wcol[Ly::orb_w + s * N * 2], wcol[Ly::orb_w + s * N * 2 + 1]);
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) obs[s] = pair_make<T>(wcol[Ly::orb_b + s * N * 2], wcol[Ly::orb_b + s * N * 2 + 1]);
   };
@@ -992,6 +1011,40 @@ k_walker_rev(KArgs ka) {
       const V2* bsp = obs;
       const int* stab = (const int*)(sm + SM::st) + 4 * RW * rg;
       V2 a2[RW];
+      if constexpr (phi_mfma) {
+        // Phi[slot][c] = sum_f h3[slot][f] W_s[f][c] + b_s[c] as two K = 4 steps (one per spin) of
+        // v_mfma_f32_16x16x4f32 per component: A[i = slot][k = f] = h^3 of the slot's electron
+        // (the zero row for the other spin), B[k = f][j = c] = W_s[f][c], C = the slot's bias;
+        // accumulator v of lane 16 rg + c is Phi[slot 4 rg + v][c], a2's layout (nn.py:432-456)
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        const int* sti = (const int*)(sm + SM::st) + 4 * (lane & 15);
+        const int fq = lane >> 4;
+        const float hu = sm[sti[1] + fq], hd = sm[sti[2] + fq];
+        int yo4[RW], fl4[RW];
+        v4f pre, pim;
+#pragma unroll
+        for (int t = 0; t < RW; ++t) {
+          yo4[t] = stab[4 * t];
+          fl4[t] = stab[4 * t + 3];
+          pre[t] = fl4[t] == 1 ? pair_re<T>(bsp[1]) : pair_re<T>(bsp[0]);
+          pim[t] = fl4[t] == 1 ? pair_im<T>(bsp[1]) : pair_im<T>(bsp[0]);
+        }
+        pre = __builtin_amdgcn_mfma_f32_16x16x4f32(hu, owm[0], pre, 0, 0, 0);
+        pim = __builtin_amdgcn_mfma_f32_16x16x4f32(hu, owm[1], pim, 0, 0, 0);
+        pre = __builtin_amdgcn_mfma_f32_16x16x4f32(hd, owm[2], pre, 0, 0, 0);
+        pim = __builtin_amdgcn_mfma_f32_16x16x4f32(hd, owm[3], pim, 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < RW; ++t) {
+          const bool ok = fl4[t] != 2 && cc < N;
+          if (ok) {
+            const int e = yo4[t] - SM::yv + cc;   // r N + c
+            Ph[e * 2 + 0] = pre[t];
+            Ph[e * 2 + 1] = pim[t];
+          }
+          const T y = ok ? sm[yo4[t] + ccl] : T(0);
+          a2[t] = pair_make<T>(pre[t] * y, pim[t] * y);
+        }
+      } else
 #pragma unroll
       for (int t = 0; t < RW; ++t) {
         const int yo = stab[4 * t], hu = stab[4 * t + 1], hd = stab[4 * t + 2], fl = stab[4 * t + 3];
@@ -1077,6 +1130,52 @@ k_walker_rev(KArgs ka) {
 #else
   constexpr bool q_mfma = false;
 #endif
+#ifdef AQ_B1_MFMA
+  // fp32 value + gradient (proposals and walker launches): B1's H adjoint on the matrix cores.
+  // Opt-in, measured slower (round 4, interleaved A/B on one box, N2 4096 walkers, µs per
+  // proposal launch: 230.2-233.7 with it against 219.1-221.9 without; the walker launch 50.0-50.3
+  // against 49.3-49.4; profiles/r04_s2_ab_mfma.txt): the proposal instantiation spills at the
+  // 5-wave budget (96 VGPRs + 16 B) and the eight dependent MFMAs serialise on one accumulator
+  constexpr bool b1_mfma = !PREP && sizeof(T) == 4 && NH == 4;
+#else
+  constexpr bool b1_mfma = false;
+#endif
+  if constexpr (b1_mfma) {
+    // dL/dH[r][f] = Re Q_f[r,r] = Re sum_c W_{s(r)}[f][c] G[c][r], G[c][r] = Yt[r][c] B[c][r]:
+    // the (8 x N)(N x N) product [W_up; W_down] G on v_mfma_f32_16x16x4f32 (Re = W_re G_re -
+    // W_im G_im, two MFMAs per K-step of four columns c = 4 k + t, k = lane >> 4); A[i = f + 4 s][k]
+    // = W_s[f][c] (rows 8..15 zero), B[k][j = r] = G[c][r] from B (LDS) and Yt; accumulator v of
+    // lane 16 s + r is row f = v of spin block s, kept for the rows r of spin s (nn.py:432-456)
+    if (!AQ_ABL(8)) {
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      const int j = lane & 15, kq = lane >> 4;
+      const bool jok = j < N;
+      const int jr = jok ? j : N - 1;
+      const int si = (j >> 2) & 1, fi = j & 3;   // A row j = f + 4 s
+      const bool iok = j < 8;
+      v4f acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int c = 4 * kq + t;
+        const bool cok = c < N;
+        const int cl = cok ? c : N - 1;
+        const float wr = P[Ly::orb_w + ((si * 4 + fi) * N + cl) * 2];
+        const float wi = P[Ly::orb_w + ((si * 4 + fi) * N + cl) * 2 + 1];
+        const float ar = (iok && cok) ? wr : 0.f, ai = (iok && cok) ? -wi : 0.f;
+        const float y = Yv[jr * N + cl];
+        const bool gok = cok && jok;
+        const float gr = gok ? y * (float)Mx[(cl * N + jr) * 2] : 0.f;
+        const float gi = gok ? y * (float)Mx[(cl * N + jr) * 2 + 1] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ar, gr, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ai, gi, acc, 0, 0, 0);
+      }
+      if (jok && kq == (j >= nup ? 1 : 0)) {
+        const int h = SM::hoff(3) + rowsrc[j] * 4;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) hbar[h + v] = acc[v];
+      }
+    }
+  } else
   if (!q_mfma && lane < 4 * N && !AQ_ABL(8)) {
     const int r = lane >> 2, f = lane & 3;
     const int sp = r < nup ? 0 : 1;
