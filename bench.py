@@ -359,20 +359,27 @@ def adam_side_bench(dtype, device, walkers, steps):
 
 def load_pmc(lib_sha):
     """PMC-derived per-launch figures of the proposal kernel (rocprofv3 --pmc passes, one counter
-    group per run, corrected per MI355X_MICROARCH.md; tools/gpu_pmc3.sh -> profiles/pmc_r03.json).
-    They are used only if the file was taken on THIS library build (``lib_sha16`` equal to the
-    loaded .so's hash); otherwise every counter-derived field is null and the reason is given."""
-    f = os.path.join(ROOT, "profiles", "pmc_r03.json")
-    if not os.path.exists(f):
-        return {}, "no PMC summary committed (profiles/pmc_r03.json)"
-    try:
-        pmc = json.load(open(f))
-    except Exception as e:
-        return {}, f"unreadable PMC summary: {e!r}"
-    if pmc.get("lib_sha16") != lib_sha:
-        return {}, (f"PMC summary taken on library {pmc.get('lib_sha16')}, this run loads {lib_sha}: "
-                    "counters not reported for a different build")
-    return pmc, None
+    group per run, corrected per MI355X_MICROARCH.md; tools/gpu_pmc3.sh -> profiles/pmc_rNN.json,
+    one file per round).  They are used only if a file was taken on THIS library build
+    (``lib_sha16`` equal to the loaded .so's hash; the newest round's file is checked first);
+    otherwise every counter-derived field is null and the reason is given."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r[0-9][0-9].json")), reverse=True)
+    if not files:
+        return {}, "no PMC summary committed (profiles/pmc_rNN.json)"
+    seen = []
+    for f in files:
+        try:
+            pmc = json.load(open(f))
+        except Exception as e:
+            seen.append(f"{os.path.basename(f)} unreadable ({e!r})")
+            continue
+        if pmc.get("lib_sha16") == lib_sha:
+            pmc["pmc_file"] = os.path.relpath(f, ROOT)
+            return pmc, None
+        seen.append(f"{os.path.basename(f)} taken on library {pmc.get('lib_sha16')}")
+    return {}, (f"this run loads library {lib_sha}; " + "; ".join(seen) +
+                ": counters not reported for a different build")
 
 
 def main():
@@ -480,9 +487,10 @@ def main():
                                                                   f"walkers per GPU, this run has {B}")
         prop = {
             "kernel": "k_walker_rev<float,14,2,PROP> proposal launch (B*N value+gradient configs)",
-            # the bound is the fp32 vector ALU (157.3 TF = 64 FLOP/clk/SIMD, MI355X_MICROARCH.md): no
-            # MFMA on this path (SQ_INSTS_MFMA = 0 in the committed PMC pass), HBM at a few % of 8 TB/s
-            "bound": "valu", "compute_unit": "VALU fp32 (no MFMA on this path)",
+            # the bound is the fp32 vector ALU (157.3 TF = 64 FLOP/clk/SIMD, MI355X_MICROARCH.md; f32
+            # MFMA shares that peak on gfx950): F5 forms Phi = h3 W + b with four
+            # v_mfma_f32_16x16x4f32 per configuration (round 4), the rest is VALU; HBM at a few % of 8 TB/s
+            "bound": "valu", "compute_unit": "VALU fp32 + MFMA f32 (Phi in F5)",
             "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
             "frac": (achieved / peak) if achieved else None, "traffic": traffic,
             "hbm_gbs": (traffic / (m["prop_avg_ms"] * 1e-3) / 1e9) if traffic else None,
@@ -491,6 +499,7 @@ def main():
             "valu_insts_per_wave": pmc.get("proposal_valu_insts_per_wave") if use_pmc else None,
             "nonfp_valu_insts_per_wave": pmc.get("proposal_nonfp_valu_insts_per_wave") if use_pmc else None,
             "pmc_lib_sha16": pmc.get("lib_sha16") if pmc else None, "lib_sha16": lib_sha,
+            "pmc_file": pmc.get("pmc_file") if pmc else None,
             "pmc_null_reason": why,
             "avg_launch_ms": m["prop_avg_ms"], "launches": m["prop_n"],
             "flop_per_launch": flop_prop,

@@ -23,4 +23,4 @@ for spec in "${passes[@]}"; do
     -d "$OUT/$name" -o "$name" -f csv -- python3 $GRAFT_REPO_ROOT/tools/mc_loop.py 2 N2 $W > "$OUT/$name.log" 2>&1 || { echo "PASS $name FAILED"; tail -5 "$OUT/$name.log"; exit 1; }
   echo "pass $name done"
 done
-cd $GRAFT_REPO_ROOT && python3 profiles/pmc_r03.py $OUT $SHA $W > gpurun_out/pmc_r03${PMC_TAG:+_$PMC_TAG}.json && echo PMC_OK
+cd $GRAFT_REPO_ROOT && python3 profiles/pmc_r03.py $OUT $SHA $W > gpurun_out/pmc_${PMC_ROUND:-r04}${PMC_TAG:+_$PMC_TAG}.json && echo PMC_OK
