@@ -231,7 +231,7 @@ static int set_lds_impl() {
     }
   }
   {   // proposal launches: RevWpb configurations per workgroup
-    const int pb = RevWpb<float, true>::value * SmemRev<float, N, A>::bytes;
+    const int pb = RevWpb<float, true>::value * SmemRev<float, N, A, kFwdReg>::bytes;
     if (pb > 65536) {
       hipError_t e = hipFuncSetAttribute((const void*)&k_walker_rev<float, N, A, false, true>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, pb);
@@ -284,7 +284,7 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
     else if (mode == MODE_GRAD && ka.proposal && ka.ecache)   // proposals from the walker cache
       k_walker_rev<float, N, A, false, true><<<dim3(prop_blocks(nconf, RevWpb<float, true>::value)),
                                               dim3(64 * RevWpb<float, true>::value),
-                                              RevWpb<float, true>::value * SmemRev<float, N, A>::bytes, s>>>(ka);
+                                              RevWpb<float, true>::value * SmemRev<float, N, A, kFwdReg>::bytes, s>>>(ka);
     else if (mode == MODE_GRAD)
       k_walker_rev<float, N, A><<<dim3((nconf + RevWpb<float, false>::value - 1) / RevWpb<float, false>::value),
                                   dim3(64 * RevWpb<float, false>::value),
@@ -297,7 +297,7 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
     else if (mode == MODE_GRAD && ka.proposal && ka.ecache)   // proposals from the walker cache
       k_walker_rev<double, N, A, false, true><<<dim3(prop_blocks(nconf, RevWpb<double, true>::value)),
                                               dim3(64 * RevWpb<double, true>::value),
-                                              RevWpb<double, true>::value * SmemRev<double, N, A>::bytes, s>>>(ka);
+                                              RevWpb<double, true>::value * SmemRev<double, N, A, kFwdReg>::bytes, s>>>(ka);
     else if (mode == MODE_GRAD)
       k_walker_rev<double, N, A><<<dim3(nconf), dim3(64), SmemRev<double, N, A>::bytes, s>>>(ka);
     else

@@ -62,7 +62,18 @@ static __device__ unsigned long long aq_phase_cycles[32];
 #define AQ_ABL(b) false
 #endif
 
-template <typename T, int N, int A>
+// FWDREG (proposal instantiations with AQ_FWD_REG): the conv and single-layer outputs of F4 stay
+// in registers until B2 instead of the cq / sv blocks (1.68 KB less LDS per wave for N2).
+// Round 4, interleaved A/B on one box (N2, 4096 walkers, µs per proposal launch): 219.2-221.7
+// with the LDS blocks, 217.9-218.8 with registers (96 VGPRs, no spill; the same 5 waves/SIMD).
+// The LDS saving would allow 6 waves/SIMD, but at the 80-VGPR budget that needs, the kernel spills
+// 19 VGPRs and measured 230.0-231.1 (profiles/r04_s3_ab_fwdreg.txt).
+#ifndef AQ_NO_FWD_REG
+constexpr bool kFwdReg = true;
+#else
+constexpr bool kFwdReg = false;
+#endif
+template <typename T, int N, int A, bool FWDREG = false>
 struct SmemRev {
   static constexpr int D0 = 4 * A;               // layer-0 h width
   static constexpr int DFM = 3 * D0 + 8;         // widest conv input (layer 0)
@@ -74,9 +85,9 @@ struct SmemRev {
   static constexpr int hbar = hl;                // their adjoints, same layout (B1..B4)
   static constexpr int QL = (3 * 4 + 8) / 4;     // conv outputs of layers 1, 2
   static constexpr int cq = hl + hl_n;           // conv outputs (kept for backward): [N][QM], [2][N][QL]
-  static constexpr int sv = cq + N * QM + 2 * N * QL;   // [3][N][4]   single outputs
+  static constexpr int sv = cq + (FWDREG ? 0 : N * QM + 2 * N * QL);   // [3][N][4]   single outputs
   static constexpr int cqo(int l, int i) { return l == 0 ? i * QM : N * QM + ((l - 1) * N + i) * QL; }
-  static constexpr int g2 = sv + 3 * N * 4;      // [3][2][N][4] g2 values (forward) / adjoints (backward)
+  static constexpr int g2 = sv + (FWDREG ? 0 : 3 * N * 4);   // [3][2][N][4] g2 values (forward) / adjoints (backward)
   static constexpr int yv = g2 + 3 * 2 * N * 4;  // [N][N]  Yt (F1..B1)
   static constexpr int ybar = yv;                // [N][N]  its adjoint (B1..B4)
   // region R, lifetimes disjoint: reuse scratch (F0..F2) -> {Phi [N][N][2], B [N][N][2]} (F5..B1)
@@ -401,7 +412,8 @@ template <typename T, int N, int A, bool PREP = false, bool PROP = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * RevWpb<T, PROP, PREP>::value))) __attribute__((amdgpu_waves_per_eu(RevWaves<T, N, A, PREP, PROP>::value))) void
 k_walker_rev(KArgs ka) {
   using Ly = Lay<N, A>;
-  using SM = SmemRev<T, N, A>;
+  constexpr bool fwd_reg = PROP && kFwdReg;
+  using SM = SmemRev<T, N, A, fwd_reg>;
   using LCc = LapCache<N, A>;
   constexpr int D0 = SM::D0;
   constexpr int WPB = RevWpb<T, PROP, PREP>::value;
@@ -757,6 +769,9 @@ k_walker_rev(KArgs ka) {
   T* hl = sm + SM::hl;
   T* cqv = sm + SM::cq;
   T* sv = sm + SM::sv;
+  // fwd_reg: this lane's conv outputs (its own output of each full quad, then the Q mod 4 outputs
+  // every lane evaluates) and single-layer output per layer, kept for B2
+  T cqr[3][2], svr[3];
   const int fi = lane >> 2, ff = lane & 3;
   const bool ilive = fi < N;
   const int ic = ilive ? fi : N - 1;
@@ -884,6 +899,11 @@ k_walker_rev(KArgs ka) {
         else if (q < 3 * T4) F = gown[(q - T4) / T4][(q - T4) % T4];
         else F = g2[((l * 2 + (q - 3 * T4)) * N + ic) * 4 + ff];
         T z = F * AQ_CW(q);
+#ifndef AQ_NO_CONV_FOLD
+        // opaque product: otherwise z + dpp(z) is contracted into fma(F, w, dpp(z)) and the DPP
+        // move cannot fold into the add (v_mul + v_mov_dpp + v_fmac instead of v_mul + v_add_dpp)
+        asm volatile("" : "+v"(z));
+#endif
         z += dpp<0xB1>(z);
         z += dpp<0x4E>(z);
         zc[q] = z;
@@ -908,7 +928,8 @@ k_walker_rev(KArgs ka) {
         const T zs = ff == 0 ? zc[q0] : (ff == 1 ? zc[q0 + 1] : (ff == 2 ? zc[q0 + 2] : zc[q0 + 3]));
 #endif
         const T c = f_tanh(zs * T(0.25) + AQ_CB(s4));
-        if (ilive) cqv[SM::cqo(l, ic) + q0 + ff] = c;
+        if constexpr (fwd_reg) cqr[l][s4] = c;
+        else if (ilive) cqv[SM::cqo(l, ic) + q0 + ff] = c;
         cq[q0 + 0] = quad_bcast<0>(c);
         cq[q0 + 1] = quad_bcast<1>(c);
         cq[q0 + 2] = quad_bcast<2>(c);
@@ -919,7 +940,8 @@ k_walker_rev(KArgs ka) {
     for (int q = 0; q < SM::QM; ++q) {
       if (q >= 4 * QF && q < Q) {
         cq[q] = f_tanh(zc[q] * T(0.25) + AQ_CR(q));
-        if (ilive && (q & 3) == ff) cqv[SM::cqo(l, ic) + q] = cq[q];
+        if constexpr (fwd_reg) cqr[l][QF + q - 4 * QF] = cq[q];
+        else if (ilive && (q & 3) == ff) cqv[SM::cqo(l, ic) + q] = cq[q];
       }
     }
     T z = AQ_SB(), z1 = T(0);   // even / odd q: two independent chains
@@ -931,7 +953,8 @@ k_walker_rev(KArgs ka) {
       }
     z += z1;
     const T sval = f_tanh(z);
-    if (ilive) sv[(l * N + ic) * 4 + ff] = sval;
+    if constexpr (fwd_reg) svr[l] = sval;
+    else if (ilive) sv[(l * N + ic) * 4 + ff] = sval;
     const T hin = l == 0 ? hl[ic * D0 + ff] : hreg;
     hreg = (d1 == NH) ? (hin + sval) * RSQ2 : sval;
 #undef AQ_CW
@@ -990,6 +1013,14 @@ k_walker_rev(KArgs ka) {
   }
   if constexpr (!PROP) AQ_SYNC();   // PROP: one wave, the Gauss-Jordan below forms Phi itself
   T logdet, phr, phi;
+#ifndef AQ_NO_YBAR_REG
+  constexpr bool ybar_reg = PROP;
+#else
+  constexpr bool ybar_reg = false;
+#endif
+  // PROP: the Gauss-Jordan's register block, after it X = (P A)^{-1}: lane 16 rg + c holds
+  // X[4 rg + t][c] = B[4 rg + t][rec[c]] in a2[t] (gj.h), kept for B1's Yt adjoint
+  V2o a2[(N + 3) / 4];
   if (reuse) {
     // the walker's pivot order (partial pivoting rerun only if a pivot comes out small)
     bool bad = false;
@@ -1010,7 +1041,6 @@ k_walker_rev(KArgs ka) {
       const V2* w = ow;
       const V2* bsp = obs;
       const int* stab = (const int*)(sm + SM::st) + 4 * RW * rg;
-      V2 a2[RW];
       if constexpr (phi_mfma) {
         // Phi[slot][c] = sum_f h3[slot][f] W_s[f][c] + b_s[c] as two K = 4 steps (one per spin) of
         // v_mfma_f32_16x16x4f32 per component: A[i = slot][k = f] = h^3 of the slot's electron
@@ -1086,6 +1116,18 @@ k_walker_rev(KArgs ka) {
       AQ_PH(10);   // tools/isa_phases.py: the rarely taken pivoted fallback, counted apart
 #endif
       gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi);
+      if constexpr (ybar_reg) {
+        // the register block of B for B1, from the pivoted inverse (natural layout in Mx)
+        wave_sync();
+        const int cc = lane & 15, rg = lane >> 4;
+        const int r = (int)sm[SM::pv + (cc < N ? cc : 0)];
+#pragma unroll
+        for (int t = 0; t < (N + 3) / 4; ++t) {
+          const int c = rg * ((N + 3) / 4) + t;
+          const int e = ((c < N ? c : 0) * N + r) * 2;
+          a2[t] = pair_make<T>(Mx[e], Mx[e + 1]);
+        }
+      }
 #ifdef AQ_PHASE_MARK
       AQ_PH(11);
 #endif
@@ -1271,6 +1313,25 @@ k_walker_rev(KArgs ka) {
     }
   }
   AQ_SYNC();   // ybar overwrites Yt
+  if constexpr (ybar_reg) {
+    // dL/dYt[r][c] = Re(B[c][r] Phi[r][c]) from the register block: B[c][r] = a2[t] of lane
+    // 16 rg + cc with c = 4 rg + t, r = rec[cc] (no B reads, no per-element index division)
+    if (!AQ_ABL(8)) {
+      const int cc = lane & 15, rg = lane >> 4;
+      constexpr int RW = (N + 3) / 4;
+      if (cc < N) {
+        const int r = (int)sm[SM::pv + cc];
+#pragma unroll
+        for (int t = 0; t < RW; ++t) {
+          const int c = rg * RW + t;
+          if (c < N) {
+            const int e = r * N + c;
+            ybar[e] = pair_re<T>(a2[t]) * Ph[e * 2] - pair_im<T>(a2[t]) * Ph[e * 2 + 1];
+          }
+        }
+      }
+    }
+  } else
   if constexpr (!PREP) {
     if (!AQ_ABL(8)) {
       for (int idx = lane; idx < N * N; idx += 64) {
@@ -1326,7 +1387,7 @@ k_walker_rev(KArgs ka) {
       asm volatile("" ::: "memory");
 #endif
       // single: s = tanh(c Ws + b), h_out = res(h_in, s)
-      const T sval = sv[(l * N + ic) * 4 + ff];
+      const T sval = fwd_reg ? svr[l] : sv[(l * N + ic) * 4 + ff];
       const T sb = (d1 == NH) ? hb * RSQ2 : hb;
       const T zs = sb * (T(1) - sval * sval);
       if constexpr (PREP) {
@@ -1358,7 +1419,7 @@ k_walker_rev(KArgs ka) {
             cb += zq[m] * sngw[qq * 4 + m];
 #endif
           }
-          const T c = cqv[SM::cqo(l, ic) + qq];
+          const T c = fwd_reg ? cqr[l][full ? q / 4 : QF + q - 4 * QF] : cqv[SM::cqo(l, ic) + qq];
           const T g = cb * (T(1) - c * c) * T(0.25);
           if constexpr (PREP) {
             // conv node (stored once, by the lane of its quad position): tanh', abar * tanh''

@@ -22,13 +22,20 @@ if os.environ.get("AIQMC_LAPW"):      # waves per walker of the local energy's s
 if os.environ.get("AIQMC_NOREUSE"):   # every proposal from scratch (PMC comparison of the two paths)
     ctx.set_proposal_reuse(False)
 pos = init_electrons(1000, None, s.atoms, s.charges, s.spins, B, 1.0)[0].to("cuda", torch.float32).contiguous()
-ctx.mc_step(pos, 10, 0.05, seed=1, offset=0)
+draws = {}
+if os.environ.get("AIQMC_HOST_DRAWS"):   # device-resident draws passed in (no Philox in the walker launch)
+    N = s.nelectrons
+    g = torch.Generator(device="cuda").manual_seed(3)
+    draws = dict(gauss1=torch.randn(10, B, 3 * N, device="cuda", generator=g),
+                 gauss2=torch.randn(10, B, N, 3, device="cuda", generator=g),
+                 u=torch.rand(10, B, N, device="cuda", generator=g))
+ctx.mc_step(pos, 10, 0.05, seed=1, offset=0, **draws)
 ctx.local_energy(pos)
 torch.cuda.synchronize()
 ctx.profile(True)
 t0 = time.perf_counter()
 for k in range(iters):
-    ctx.mc_step(pos, 10, 0.05, seed=1, offset=10 * (k + 1))
+    ctx.mc_step(pos, 10, 0.05, seed=1, offset=10 * (k + 1), **draws)
     el, _, _ = ctx.local_energy(pos)
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / iters
