@@ -581,6 +581,7 @@ int aiqmc_create(const aiqmc_cfg* cfg, aiqmc_ctx** out) {
     if (v < 0 || v >= N) { delete c; return fail(AIQMC_EINVAL, "antiparallel_indices out of range"); }
   c->ncanon = ops.ncanon(c->npar, c->nanti);
   c->nkern = ops.nkern;
+  c->nprm = ops.nprm;
   hipError_t e = hipSetDevice(c->device);
   if (e != hipSuccess) { delete c; return fail(AIQMC_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(e)); }
   int rc = ops.set_lds();
@@ -588,7 +589,7 @@ int aiqmc_create(const aiqmc_cfg* cfg, aiqmc_ctx** out) {
   if (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->ncu <= 0)
     c->ncu = 256;
   const size_t s = c->dtype == AIQMC_F32 ? 4 : 8;
-  e = hipMalloc(&c->d_prm, (size_t)c->nkern * s);
+  e = hipMalloc(&c->d_prm, (size_t)c->nprm * s);
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_rowsrc, 16 * sizeof(int));
   if (e != hipSuccess) {
     if (c->d_prm) (void)hipFree(c->d_prm);

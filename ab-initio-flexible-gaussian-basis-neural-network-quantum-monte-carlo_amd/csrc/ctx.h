@@ -28,7 +28,7 @@ struct aiqmc_ctx {
   int npar = 0, nanti = 0;
   std::vector<double> atoms, charges;
   std::vector<int> up, dn, par, anti;
-  int64_t ncanon = 0, nkern = 0;
+  int64_t ncanon = 0, nkern = 0, nprm = 0;   // nprm: device parameter buffer (nkern + lane-order copies)
   void* d_prm = nullptr;
   int* d_rowsrc = nullptr;
   bool params_set = false;
@@ -89,6 +89,7 @@ struct ShapeOps {
   int wcache_n, ecache_n;                                      // cache entries per walker / per proposal
   int lcache_n;                                                // LapCache entries per walker
   int64_t nkern;
+  int64_t nprm;
   long (*ncanon)(int npar, int nanti);
   void (*pack)(const aiqmc_ctx* c, const double* flat, std::vector<double>& out);
   void (*gmap)(const aiqmc_ctx* c, std::vector<int>& map);                        // canonical -> kernel index

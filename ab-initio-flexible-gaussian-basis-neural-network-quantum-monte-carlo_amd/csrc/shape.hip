@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void k_accept(T* __restrict__ pos, AccArgs a, 
 template <int N, int A>
 static void pack_params(const aiqmc_ctx* c, const double* flat, std::vector<double>& out) {
   using Ly = Lay<N, A>;
-  out.assign(Ly::total, 0.0);
+  out.assign(Ly::total_ext, 0.0);
   const double* p = flat;
   auto take = [&](int n) {
     const double* q = p;
@@ -104,6 +104,20 @@ static void pack_params(const aiqmc_ctx* c, const double* flat, std::vector<doub
     const double* swp = take(Q[l] * NH);
     for (int k = 0; k < NH; ++k) out[sb[l] + k] = sbp[k];
     for (int k = 0; k < Q[l] * NH; ++k) out[sw[l] + k] = swp[k];
+  }
+  // lane-order copies of the h-stream weights (layout.h x* blocks)
+  for (int l = 0; l < 3; ++l) {
+    const int QF = Q[l] / 4;
+    for (int i = 0; i < N; ++i)
+      for (int f = 0; f < 4; ++f) {
+        for (int q = 0; q < Q[l]; ++q) out[Ly::xcw(l) + (i * 4 + f) * Ly::XQ + q] = out[cw[l] + i * D[l] + 4 * q + f];
+        for (int s4 = 0; s4 < QF; ++s4) out[Ly::xcb(l) + (i * 4 + f) * 4 + s4] = out[cb[l] + i * Q[l] + 4 * s4 + f];
+        for (int q = 4 * QF; q < Q[l]; ++q) out[Ly::xcb(l) + (i * 4 + f) * 4 + QF + q - 4 * QF] = out[cb[l] + i * Q[l] + q];
+      }
+    for (int f = 0; f < 4; ++f)
+      for (int q = 0; q < Q[l]; ++q) out[Ly::xsw(l) + f * Ly::XQ + q] = out[sw[l] + q * NH + f];
+    for (int q = 0; q < Q[l]; ++q)
+      for (int f = 0; f < 4; ++f) out[Ly::xsr(l) + q * 4 + f] = out[sw[l] + q * NH + f];
   }
   // layers.streams_y[l].single_Ynlm {b, w}
   const int yin[3] = {Ly::DY0, NYW, NYW};
@@ -396,6 +410,7 @@ bool AQ_CAT(AQ_N, AQ_A)(ShapeOps* ops) {
   ops->wcache_n = WCache<AQ_N, AQ_A>::size;
   ops->ecache_n = ECache<AQ_N, AQ_A>::size;
   ops->nkern = Lay<AQ_N, AQ_A>::total;
+  ops->nprm = Lay<AQ_N, AQ_A>::total_ext;
   ops->ncanon = &Lay<AQ_N, AQ_A>::canon;
   ops->pack = &pack_params<AQ_N, AQ_A>;
   ops->gmap = &gmap_impl<AQ_N, AQ_A>;

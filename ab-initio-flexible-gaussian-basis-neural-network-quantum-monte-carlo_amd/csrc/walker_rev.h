@@ -196,6 +196,38 @@ template <int M, typename T> __device__ __forceinline__ T quad_bcast(T x) {
   return dpp<M | (M << 2) | (M << 4) | (M << 6)>(x);
 }
 
+// NV (a multiple of 16 bytes' worth) consecutive parameters from a 16-byte aligned offset of the
+// parameter buffer, in 16-byte loads (layout.h lane-order blocks)
+template <typename T, int NV>
+__device__ __forceinline__ void ld_vec(cptr<T> p, T* out) {
+  if constexpr (sizeof(T) == 4) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const __attribute__((address_space(4))) f4* q = (const __attribute__((address_space(4))) f4*)p;
+#pragma unroll
+    for (int j = 0; j < NV / 4; ++j) {
+      const f4 v = q[j];
+      out[4 * j] = v.x;
+      out[4 * j + 1] = v.y;
+      out[4 * j + 2] = v.z;
+      out[4 * j + 3] = v.w;
+    }
+  } else {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const __attribute__((address_space(4))) d2* q = (const __attribute__((address_space(4))) d2*)p;
+#pragma unroll
+    for (int j = 0; j < NV / 2; ++j) {
+      const d2 v = q[j];
+      out[2 * j] = v.x;
+      out[2 * j + 1] = v.y;
+    }
+  }
+}
+#ifndef AQ_NO_XLANE
+constexpr bool kXLane = true;    // F4 / B2 read the lane-order weight blocks in 16-byte loads
+#else
+constexpr bool kXLane = false;
+#endif
+
 // Barrier of a one-configuration wave: LDS traffic of one wave is processed in order, so a
 // wavefront-scope fence (a compiler barrier, no s_waitcnt) orders its cross-lane LDS accesses.
 __device__ __forceinline__ void wave_sync() {
@@ -413,6 +445,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * RevWpb<T, PROP, PR
 k_walker_rev(KArgs ka) {
   using Ly = Lay<N, A>;
   constexpr bool fwd_reg = PROP && kFwdReg;
+  // the lane-order weight blocks in F4 / B2: proposals only (round 4, interleaved A/B on one box:
+  // proposal launch 216.3-219.0 -> 215.1-218.2 us; the same in the walker launch and the local
+  // energy's adjoint pass measured +0.5 us and +7-11 us per launch, profiles/r04_s5_ab_xlane.txt)
+  constexpr bool xlane = PROP && kXLane;
   using SM = SmemRev<T, N, A, fwd_reg>;
   using LCc = LapCache<N, A>;
   constexpr int D0 = SM::D0;
@@ -822,6 +858,25 @@ k_walker_rev(KArgs ka) {
     const cptr<T> cb = P + (l == 0 ? Ly::conv_b0 : (l == 1 ? Ly::conv_b1 : Ly::conv_b2)) + ic * Q;
     const cptr<T> sw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
     const cptr<T> sb = P + (l == 0 ? Ly::sng_b0 : (l == 1 ? Ly::sng_b1 : Ly::sng_b2));
+    if constexpr (xlane) {
+      // the lane's records of the lane-order blocks: 2 + 2 + 1 sixteen-byte loads
+      T cw8[Ly::XQ], sw8[Ly::XQ], cb4[4];
+      ld_vec<T, Ly::XQ>(P + Ly::xcw(l) + (ic * 4 + ff) * Ly::XQ, cw8);
+      ld_vec<T, Ly::XQ>(P + Ly::xsw(l) + ff * Ly::XQ, sw8);
+      ld_vec<T, 4>(P + Ly::xcb(l) + (ic * 4 + ff) * 4, cb4);
+#pragma unroll
+      for (int q = 0; q < SM::QM; ++q)
+        if (q < Q) {
+          wcv[l][q] = cw8[q];
+          wsw[l][q] = sw8[q];
+        }
+#pragma unroll
+      for (int s4 = 0; s4 < SM::QM / 4; ++s4)
+        if (s4 < Q / 4) wcb[l][s4] = cb4[s4];
+#pragma unroll
+      for (int q = 0; q < SM::QM; ++q)
+        if (q >= 4 * (Q / 4) && q < Q) wcb[l][q] = cb4[Q / 4 + q - 4 * (Q / 4)];
+    } else {
 #pragma unroll
     for (int q = 0; q < SM::QM; ++q)
       if (q < Q) {
@@ -835,6 +890,7 @@ k_walker_rev(KArgs ka) {
 #pragma unroll
     for (int q = 0; q < SM::QM; ++q)
       if (q >= 4 * (Q / 4) && q < Q) wcb[l][q] = cb[q];
+    }
     wsb[l] = sb[ff];
   };
   lw_load(0);
@@ -1405,18 +1461,22 @@ k_walker_rev(KArgs ka) {
       // and DPP broadcasts it (as the forward tanh's); the Q mod 4 rest on every lane
       const int QF = Q / 4;
       T cg[SM::QM];
+      T bcw8[Ly::XQ];   // kXLane: this lane's conv weights (electron ic, unit ff), 2 sixteen-byte loads
+      if constexpr (xlane) ld_vec<T, Ly::XQ>(P + Ly::xcw(l) + (ic * 4 + ff) * Ly::XQ, bcw8);
 #pragma unroll
       for (int q = 0; q < SM::QM; ++q) {
         const bool full = q < 4 * QF;
         if (q < Q && (!full || (q & 3) == 0)) {
           const int qq = full ? q + ff : q;     // output this lane forms
           T cb = T(0);
+          T srow[4];   // kXLane: single-layer weight row qq, one sixteen-byte load
+          if constexpr (xlane) ld_vec<T, 4>(P + Ly::xsr(l) + qq * 4, srow);
 #pragma unroll
           for (int m = 0; m < 4; ++m) {
 #ifdef AQ_B2_PRELOAD
             cb += zq[m] * (full ? bsw[l][q / 4][m] : sngw[qq * 4 + m]);
 #else
-            cb += zq[m] * sngw[qq * 4 + m];
+            cb += zq[m] * (xlane ? srow[m] : sngw[qq * 4 + m]);
 #endif
           }
           const T c = fwd_reg ? cqr[l][full ? q / 4 : QF + q - 4 * QF] : cqv[SM::cqo(l, ic) + qq];
@@ -1446,7 +1506,7 @@ k_walker_rev(KArgs ka) {
 #ifdef AQ_B2_PRELOAD
         if (q < Q) fb[q] = cg[q] * bcw[l][q];
 #else
-        if (q < Q) fb[q] = cg[q] * convw[4 * q + ff];
+        if (q < Q) fb[q] = cg[q] * (xlane ? bcw8[q] : convw[4 * q + ff]);
 #endif
       // g2 adjoints (inputs 3 d1 + 4G + f), consumed by B3
       if (ilive) {   // pre-scaled by the group-mean weights 1/|G| of the pair sums
@@ -1574,7 +1634,7 @@ k_walker_rev(KArgs ka) {
   // from the walker cache, or the moved electron's entry of this proposal
   const int c4 = lc < 3 ? lc : 0;
   T lv[N + D0];
-  {
+  auto lv_load = [&]() {
     const bool mov = reuse && le == pi;
     const T* la = mov ? Eq + EC::yd + c4 * N : Wc + WC::loc + (lane < 48 ? lane : 47);
     const T* lb = mov ? Eq + EC::hd + c4 * D0 : Wc + WC::loc + N * 48 + (lane < 48 ? lane : 47);
@@ -1583,7 +1643,15 @@ k_walker_rev(KArgs ka) {
     for (int m = 0; m < N; ++m) lv[m] = la[m * st];
 #pragma unroll
     for (int m = 0; m < D0; ++m) lv[N + m] = lb[m * st];
-  }
+  };
+  // where the proposal path issues B4's Jacobian loads: 0 = before B3 (their latency overlaps all
+  // of B3), k = after B3's iteration k - 1.  Round 4: 1..3 leave the fp32 N2 proposal kernel at 95
+  // VGPRs and do not remove the spills of a 6-wave build (15-16 VGPRs): not the pressure point
+#ifndef AQ_LV_AT
+#define AQ_LV_AT 0
+#endif
+  constexpr int lv_at = (reuse && PROP) ? AQ_LV_AT : 0;
+  if (lv_at == 0) lv_load();
   AQ_PH(6);
   // ------------------------------------------------------------------ B3 pair adjoints d(logpsi)/d(x_i - x_k)
   T* dbar = sm + SM::dbar;
@@ -1706,6 +1774,7 @@ k_walker_rev(KArgs ka) {
     for (int u = 0; u < NIT; ++u) {
       const int it = lane + 64 * u;
       if (it < NPR) pair_adjoint(pk[u], pi2[u], u == 0, u == 0 && it < M, tc[u], jc[u], ja[u]);
+      if (lv_at == u + 1) lv_load();
     }
   } else if (!reuse) {
     if (!PREP && !isprop && ka.wcache) {
