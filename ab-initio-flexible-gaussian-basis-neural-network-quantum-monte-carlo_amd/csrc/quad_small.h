@@ -469,41 +469,52 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
 template <typename T, int N, int A>
 struct SmemQG {
   static constexpr int D0 = 4 * A;
+  static constexpr int NI = QSlot<N>::NI, SW = QSlot<N>::SW;   // electron slots, lanes per configuration
   static constexpr int QM = (3 * D0 + 8) / 4;    // conv outputs of layer 0
   static constexpr int QL = (3 * 4 + 8) / 4;     // conv outputs of layers 1, 2
-  static constexpr int xs = 0;                   // [12] positions; [12..15] old position of the moved electron
-  static constexpr int xo = 12;
-  static constexpr int yv = 16;                  // [N][N] Yt, then its adjoint
-  static constexpr int hl = yv + 16;             // h^0 [4][D0], h^3 [4][4]; then their adjoints
-  static constexpr int h3 = hl + 4 * D0;
-  static constexpr int g2 = h3 + 16;             // [3][2][N][4] pair column means, then their adjoints
-  static constexpr int S = g2 + 96;              // [16][12] patch pair values; then dbar [N][N][3]
-  static constexpr int cq = S + 192;             // conv outputs [4][QM] + [2][4][QL]
-  static constexpr int sv = cq + 4 * QM + 8 * QL;   // [3][4][4] single outputs
-  static constexpr int ph = sv + 48;             // [N][N][2] Phi
-  static constexpr int mx = ph + 32;             // [N][N][2] B = A^{-1}
-  static constexpr int size = mx + 32;
-  static constexpr int cqo(int l, int i) { return l == 0 ? i * QM : 4 * QM + ((l - 1) * 4 + i) * QL; }
+  static constexpr int cmax(int a, int b) { return a > b ? a : b; }
+  static constexpr int xs = 0;                   // [3 NI] positions; then [4] old position of the moved electron
+  static constexpr int xo = 3 * NI;
+  static constexpr int yv = xo + 4;              // [N][N] Yt, then its adjoint
+  static constexpr int hl = yv + NI * NI;        // h^0 [NI][D0], h^3 [NI][4]; then their adjoints
+  static constexpr int h3 = hl + NI * D0;
+  static constexpr int g2 = h3 + NI * 4;         // [3][2][N][4] pair column means, then their adjoints
+  static constexpr int S = g2 + 24 * NI;         // [SW][12] patch pair values; then dbar [N][N][3]
+  static constexpr int cq = S + cmax(SW * 12, 3 * NI * NI);   // conv outputs [NI][QM] + [2][NI][QL]
+  static constexpr int sv = cq + NI * QM + 2 * NI * QL;      // [3][NI][4] single outputs
+  static constexpr int ph = sv + 12 * NI;        // [N][N][2] Phi
+  static constexpr int mx = ph + 2 * NI * NI;    // [N][N][2] B = A^{-1}
+  static constexpr int size = mx + 2 * NI * NI;
+  static constexpr int cqo(int l, int i) { return l == 0 ? i * QM : NI * QM + ((l - 1) * NI + i) * QL; }
 };
 
 // WALK = true: the walker launch of a sweep (k_walker_rev's walker path): the previous sweep's
 // acceptance (fused), every electron's stage on lane 4c + e (its local Jacobians stay in the
 // lane's registers for B4), the full pair stream on lane k N + i, and the complete walker cache
 // (WCache, including the pair tanh's and the pivot record the one-wave proposal path reads).
+// 5 <= N <= 8 (round 4; the C atom all-electron (6, 1), C2 (8, 2) -- the reference's example/C2):
+// the proposals two configurations per wave, one 32-lane slot each, with the same phases: the
+// spin-group class sums take one lane exchange across the slot's two 16-lane rows, the Gauss-Jordan
+// holds two matrix elements per lane (lane 4 r + g: columns g and g + 4 of row r; the pivot is the
+// packed-key max over the slot's eight row quads, as k_quad_value's LU), B3 runs the N (N - 1)
+// pairs in two passes of 32, and B4 puts direction x_{e,c} on lane 8 c + e.  The walker launches of
+// these shapes stay on k_walker_rev (WALK is N <= 4 only).
 template <typename T, int N, int A, bool WALK = false>
 __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
-  static_assert(N <= 4, "k_quad_grad: four configurations per wave need N <= 4");
+  static_assert(N <= 8, "k_quad_grad: several configurations per wave need N <= 8");
+  static_assert(!WALK || N <= 4, "k_quad_grad: the packed walker launch is built for N <= 4");
   using Ly = Lay<N, A>;
   using WC = WCache<N, A>;
   using EC = ECache<N, A>;
   using SQ = SmemQG<T, N, A>;
   constexpr int D0 = 4 * A;
   constexpr int QM = SQ::QM;
+  constexpr int SW = QSlot<N>::SW, NI = QSlot<N>::NI, NSL = QSlot<N>::NSL;
   const cptr<T> P = param_ptr<T>(ka.prm);
-  __shared__ T smq[4 * SQ::size];
+  __shared__ T smq[NSL * SQ::size];
   const int lane = threadIdx.x;
-  const int slot = lane >> 4, sl = lane & 15;
-  const int c0 = xcd_major(blockIdx.x, gridDim.x) * 4 + slot;
+  const int slot = lane / SW, sl = lane % SW;
+  const int c0 = xcd_major(blockIdx.x, gridDim.x) * NSL + slot;
   const bool act = c0 < ka.nconf;
   const int conf = act ? c0 : ka.nconf - 1;
   T* sm = smq + slot * SQ::size;
@@ -646,13 +657,13 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
     wave_sync();
   } else {
   // ---------------------------------------------------------------- F1 cached stage of walker pb
-  jsum = quad_stage_load<T, N, A, 16>((const T*)ka.pos + (size_t)pb * 3 * N, Wc, Eq, pi, sl, xs, sm + SQ::xo, Yv,
+  jsum = quad_stage_load<T, N, A, SW>((const T*)ka.pos + (size_t)pb * 3 * N, Wc, Eq, pi, sl, xs, sm + SQ::xo, Yv,
                                       hl, g2);
   wave_sync();
 
   // ---------------------------------------------------------------- F2 pairs of the moved electron
   {
-    const int part = sl >> 2, o = sl & 3;
+    const int part = sl / NI, o = sl % NI;
     const int os = o < N ? o : N - 1;
     const T* xp = (part & 1) ? sm + SQ::xo : xs + pi * 3;
     T d[3];
@@ -678,17 +689,17 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
     for (int l = 0; l < 3; ++l)
 #pragma unroll
       for (int f = 0; f < 4; ++f)
-        g2[((l * 2 + Gp) * N + sl) * 4 + f] += (S[sl * 12 + l * 4 + f] - S[(4 + sl) * 12 + l * 4 + f]) * gw;
+        g2[((l * 2 + Gp) * N + sl) * 4 + f] += (S[sl * 12 + l * 4 + f] - S[(NI + sl) * 12 + l * 4 + f]) * gw;
   }
 #pragma unroll
-  for (int t0 = 0; t0 < 24; t0 += 16) {
+  for (int t0 = 0; t0 < 24; t0 += SW) {
     const int t = t0 + sl;
     if (t < 24) {
       const int l = t >> 3, G = (t >> 2) & 1, f = t & 3;
       const int k0 = G ? nup : 0, k1 = G ? N : nup;
       T acc = T(0);
       for (int k = k0; k < k1; ++k)
-        if (k != pi) acc += S[(8 + k) * 12 + l * 4 + f] - S[(12 + k) * 12 + l * 4 + f];
+        if (k != pi) acc += S[(2 * NI + k) * 12 + l * 4 + f] - S[(3 * NI + k) * 12 + l * 4 + f];
       g2[((l * 2 + G) * N + pi) * 4 + f] += acc * (G ? ginv1 : ginv0);
     }
   }
@@ -719,8 +730,8 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
     for (int t = 0; t < D0 / 4; ++t) {
       if (t < T4) {
         const T x = ilive ? hown[t] : T(0);
-        gown[0][t] = row_class4_sum(inG1 ? T(0) : x) * ginv0;
-        gown[1][t] = row_class4_sum(inG1 ? x : T(0)) * ginv1;
+        gown[0][t] = slot_class4_sum<SW>(inG1 ? T(0) : x) * ginv0;
+        gown[1][t] = slot_class4_sum<SW>(inG1 ? x : T(0)) * ginv1;
       }
     }
     T zc[QM];
@@ -767,7 +778,7 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
       }
     z += z1;
     const T sval = f_tanh(z);
-    if (ilive) svv[(l * 4 + ic) * 4 + ff] = sval;
+    if (ilive) svv[(l * NI + ic) * 4 + ff] = sval;
     const T hin = l == 0 ? hl[ic * D0 + ff] : hreg;
     hreg = (d1 == NH) ? (hin + sval) * RSQ2 : sval;
   }
@@ -783,7 +794,7 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
   // rows not used yet.
   T lsum = T(0), ur = T(1), ui = T(0);
   int inv = 0;
-  {
+  if constexpr (SW == 16) {
     const int r = sl >> 2, c = sl & 3;
     const bool rl = r < N;
     T a = T(0), b = T(0);
@@ -861,6 +872,111 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
       Wc[WC::pv + 2 * N] = T(inv & 1);
       Wc[WC::pv + 2 * N + 1] = T(0.5) * lsum;
     }
+  } else {
+    // 5 <= N <= 8: lane 4 r + g of the slot holds A[r][g] and A[r][g + 4].  Step k: column k
+    // reaches row r's lanes by a quad broadcast, the pivot row p is the packed-key max over the
+    // slot's eight row quads (low three bits 7 - r: the first maximal row, izamax, as gj.h), the
+    // pivot row's entries of this lane's two columns come by lane permutes; then, as above,
+    // q = A[p][:] / pivot (q_k = 1 / pivot), A[r][c] -= A[r][k] q_c for r != p (column k:
+    // -A[r][k] q_k), row p <- q.  B[k][p_c] = X[p_k][c].
+    const int r = sl >> 2, g = sl & 3;
+    const bool rl = r < N;
+    T a[2], b[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = g + 4 * h;
+      a[h] = T(0);
+      b[h] = T(0);
+      if (rl && c < N) {
+        const int src = rowsrc[r];
+        const int sp = r < nup ? 0 : 1;
+        T re = P[Ly::orb_b + (sp * N + c) * 2 + 0], im = P[Ly::orb_b + (sp * N + c) * 2 + 1];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const T hv = H3[src * 4 + f];
+          re += hv * P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 0];
+          im += hv * P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 1];
+        }
+        Ph[(r * N + c) * 2 + 0] = re;
+        Ph[(r * N + c) * 2 + 1] = im;
+        const T y = Yv[r * N + c];
+        a[h] = re * y;
+        b[h] = im * y;
+      }
+    }
+    const int sbase = lane & ~31;
+    unsigned used = 0;
+    int stepk = 0;      // the step at which this lane's row was the pivot row
+    int pc[2] = {0, 0};   // the pivot row of step c for this lane's two columns
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const int kh = k >> 2;
+      T akr, aki;   // A[r][k]
+      if ((k & 3) == 0) { akr = quad_bcast<0>(a[kh]); aki = quad_bcast<0>(b[kh]); }
+      else if ((k & 3) == 1) { akr = quad_bcast<1>(a[kh]); aki = quad_bcast<1>(b[kh]); }
+      else if ((k & 3) == 2) { akr = quad_bcast<2>(a[kh]); aki = quad_bcast<2>(b[kh]); }
+      else { akr = quad_bcast<3>(a[kh]); aki = quad_bcast<3>(b[kh]); }
+      const bool open = rl && !((used >> r) & 1u);
+      unsigned key = open ? ((key_bits(f_abs(akr) + f_abs(aki)) & ~7u) | (unsigned)(7 - r)) : 0u;
+      {
+        const unsigned k4 = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x124, 0xF, 0xF, true);
+        key = key > k4 ? key : k4;
+        const unsigned k8 = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x128, 0xF, 0xF, true);
+        key = key > k8 ? key : k8;
+        const unsigned k16 = (unsigned)__shfl_xor((int)key, 16);
+        key = key > k16 ? key : k16;
+      }
+      const int p = 7 - (int)(key & 7u);
+      const int srcl = sbase + 4 * p + g;
+      T er[2], ei[2];   // A[p][g], A[p][g + 4]
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        er[h] = __shfl(a[h], srcl);
+        ei[h] = __shfl(b[h], srcl);
+      }
+      T pr, pim;   // A[p][k]
+      {
+        const T sr = er[kh], si = ei[kh];
+        if ((k & 3) == 0) { pr = quad_bcast<0>(sr); pim = quad_bcast<0>(si); }
+        else if ((k & 3) == 1) { pr = quad_bcast<1>(sr); pim = quad_bcast<1>(si); }
+        else if ((k & 3) == 2) { pr = quad_bcast<2>(sr); pim = quad_bcast<2>(si); }
+        else { pr = quad_bcast<3>(sr); pim = quad_bcast<3>(si); }
+      }
+      inv += __builtin_popcount(used >> p);
+      used |= 1u << p;
+      const T den = pr * pr + pim * pim;
+      const T rden = f_rcp(den);
+      lsum += f_log(den);
+      {
+        const T rm = f_sqrt(rden);
+        const T xr = pr * rm, xi = pim * rm;
+        const T nr = ur * xr - ui * xi, ni = ur * xi + ui * xr;
+        ur = nr;
+        ui = ni;
+      }
+      const T ir = pr * rden, ii = -pim * rden;   // 1 / pivot
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const bool ck = (g + 4 * h == k);
+        const T qr = ck ? ir : er[h] * ir - ei[h] * ii;
+        const T qi = ck ? ii : er[h] * ii + ei[h] * ir;
+        const T br = ck ? T(0) : a[h], bi = ck ? T(0) : b[h];
+        const T nr = br - (akr * qr - aki * qi);
+        const T ni = bi - (akr * qi + aki * qr);
+        a[h] = r == p ? qr : nr;
+        b[h] = r == p ? qi : ni;
+        pc[h] = ck ? p : pc[h];
+      }
+      stepk = r == p ? k : stepk;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = g + 4 * h;
+      if (rl && c < N) {
+        Mx[(stepk * N + pc[h]) * 2 + 0] = a[h];
+        Mx[(stepk * N + pc[h]) * 2 + 1] = b[h];
+      }
+    }
   }
   wave_sync();
 #define BRE(c, s) Mx[((c) * N + (s)) * 2]
@@ -882,9 +998,13 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
     H3[rowsrc[r] * 4 + f] = q;   // adjoint of h^3 (same place)
   }
   wave_sync();   // ybar overwrites Yt
-  if (sl < N * N) {
-    const int r = sl / N, c = sl - r * N;
-    Yv[sl] = BRE(c, r) * Ph[sl * 2] - BIM(c, r) * Ph[sl * 2 + 1];
+#pragma unroll
+  for (int e0 = 0; e0 < N * N; e0 += SW) {
+    const int e = e0 + sl;
+    if (e < N * N) {
+      const int r = e / N, c = e - r * N;
+      Yv[e] = BRE(c, r) * Ph[e * 2] - BIM(c, r) * Ph[e * 2 + 1];
+    }
   }
 #undef BRE
 #undef BIM
@@ -902,7 +1022,7 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
       const int T4 = d1 / 4;
       const cptr<T> convw = P + (l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2)) + ic * DF;
       const cptr<T> sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
-      const T sval = svv[(l * 4 + ic) * 4 + ff];
+      const T sval = svv[(l * NI + ic) * 4 + ff];
       const T sb = (d1 == NH) ? hb * RSQ2 : hb;
       const T zs = sb * (T(1) - sval * sval);
       const T zq[4] = {quad_bcast<0>(zs), quad_bcast<1>(zs), quad_bcast<2>(zs), quad_bcast<3>(zs)};
@@ -940,8 +1060,8 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
 #pragma unroll
       for (int t = 0; t < D0 / 4; ++t) {
         if (t < T4) {
-          const T s0 = row_class4_sum(ilive ? fb[T4 + t] : T(0)) * ginv0;
-          const T s1 = row_class4_sum(ilive ? fb[2 * T4 + t] : T(0)) * ginv1;
+          const T s0 = slot_class4_sum<SW>(ilive ? fb[T4 + t] : T(0)) * ginv0;
+          const T s1 = slot_class4_sum<SW>(ilive ? fb[2 * T4 + t] : T(0)) * ginv1;
           T v = fb[t] + (inG1 ? s1 : s0);
           if (d1 == NH) v += hb * RSQ2;
           if (l == 0) {
@@ -958,8 +1078,11 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
 
   // ---------------------------------------------------------------- B3 pair adjoints (every pair fresh)
   T* dbar = S;   // [N][N][3]
-  if (sl < N * (N - 1)) {
-    const int k = sl / (N - 1), jj = sl - k * (N - 1);
+#pragma unroll
+  for (int it0 = 0; it0 < N * (N - 1); it0 += SW) {
+  const int it = it0 + sl;
+  if (it < N * (N - 1)) {
+    const int k = it / (N - 1), jj = it - k * (N - 1);
     const int i = jj + (jj >= k ? 1 : 0);
     const int G = k >= nup ? 1 : 0;
     T d[3];
@@ -1015,10 +1138,11 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) dbar[(k * N + i) * 3 + c] = pb0[1 + c] + rb * d[c] * ir;
   }
+  }
   wave_sync();
 
-  // ---------------------------------------------------------------- B4 gradient, lane 4c + e
-  const int gc = sl >> 2, ge = sl & 3;
+  // ---------------------------------------------------------------- B4 gradient, lane NI c + e
+  const int gc = sl / NI, ge = sl % NI;
   const bool gdir = gc < 3 && ge < N;
   const int gcc = gc < 3 ? gc : 0, gee = ge < N ? ge : N - 1;
   T g = T(0);
@@ -1053,8 +1177,8 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
     }
   }
   const T gd = gdir ? g : T(0);
-  const T sumsq = row16_sum(gd * gd);
-  const T jt = row16_sum(jsum);
+  const T sumsq = slot_sum<SW>(gd * gd);
+  const T jt = slot_sum<SW>(jsum);
   const T lsum0 = quad_bcast<0>(lsum), ur0 = quad_bcast<0>(ur), ui0 = quad_bcast<0>(ui);
   if (act) {
     if (ka.grad && gdir) ((T*)ka.grad)[(size_t)conf * 3 * N + 3 * gee + gcc] = g;

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "ctx.h"
@@ -267,6 +268,15 @@ static inline unsigned prop_blocks(int nconf, int wpb) {
 // single-electron-moved configurations from the walker cache (quad_small.h): value only (pp
 // quadrature, N <= 8) or value + gradient (Metropolis proposals and walker launches, N <= 4),
 // several configurations per wave
+// AIQMC_QUAD_GRAD=0 routes the packed proposals of 5 <= N <= 8 back to k_walker_rev (A/B timing)
+static bool quad_grad_off() {
+  static const int off = [] {
+    const char* e = std::getenv("AIQMC_QUAD_GRAD");
+    return (e && e[0] == '0') ? 1 : 0;
+  }();
+  return off != 0 && AQ_N > 4;
+}
+
 template <typename T, int N, int A>
 static bool quad_small(const KArgs& ka, int nconf, hipStream_t s) {
   if constexpr (N <= 8) {   // pp quadrature: 4 (N <= 4) or 2 (N <= 8) configurations per wave
@@ -275,11 +285,13 @@ static bool quad_small(const KArgs& ka, int nconf, hipStream_t s) {
       return true;
     }
   }
-  if constexpr (N <= 4) {
-    if (ka.proposal && ka.ecache && !ka.value_only && !ka.orb && !ka.ablate) {   // Metropolis proposals
-      k_quad_grad<T, N, A><<<dim3((nconf + 3) / 4), dim3(64), 0, s>>>(ka);
+  if constexpr (N <= 8) {   // Metropolis proposals: 4 (N <= 4) or 2 (N <= 8) configurations per wave
+    if (ka.proposal && ka.ecache && !ka.value_only && !ka.orb && !ka.ablate && !quad_grad_off()) {
+      k_quad_grad<T, N, A><<<dim3((nconf + QSlot<N>::NSL - 1) / QSlot<N>::NSL), dim3(64), 0, s>>>(ka);
       return true;
     }
+  }
+  if constexpr (N <= 4) {
     if (!ka.proposal && ka.wcache && !ka.value_only && !ka.orb && !ka.lapcache) {   // walker launches
       k_quad_grad<T, N, A, true><<<dim3((nconf + 3) / 4), dim3(64), 0, s>>>(ka);
       return true;

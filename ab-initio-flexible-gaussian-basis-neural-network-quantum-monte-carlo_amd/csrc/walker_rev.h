@@ -106,7 +106,9 @@ struct SmemRev {
   static constexpr int st = ((g2 + 2 * N + 2 + 3) / 4) * 4;
   static constexpr int zr = st + (4 * RW * 4 * 4 + (int)sizeof(T) - 1) / (int)sizeof(T);
   static_assert(zr + 4 <= g2 + 3 * 2 * N * 4, "slot table outside the g2 region");
-  static constexpr int end = R + R_n;
+  // FWDREG (proposals): the e-n Jastrow gradient of the direction lanes, parked from F2 to B4
+  static constexpr int jdo = R + R_n;
+  static constexpr int end = jdo + (FWDREG ? 64 : 0);
   static constexpr int bytes = ((end * (int)sizeof(T)) + 15) & ~15;
   static constexpr int hoff(int l) { return l == 0 ? 0 : N * D0; }   // l = 0 or 3
 };
@@ -536,6 +538,7 @@ k_walker_rev(KArgs ka) {
   T* Yv = sm + SM::yv;
   T* g2 = sm + SM::g2;
   T jv = T(0), jd1 = T(0), jve = T(0);
+  T jsum_p = T(0);   // fwd_reg: wave_sum(jv + jve), formed in F2
   T pvr = T(0);
   int rsl = 0;   // PROP: rowsrc[lane]
   T jvp = T(0);  // F2's Jastrow terms of the moved electron's pairs
@@ -694,6 +697,13 @@ k_walker_rev(KArgs ka) {
       AQ_SYNC();
     }
     jve += jvp;
+    if constexpr (fwd_reg) {
+      // the Jastrow terms are complete: their wave sum (log|psi| = logdet + it) and the e-n
+      // gradient of the direction lanes (B4) leave the registers until the end of the kernel
+      jsum_p = wave_sum(jv + jve);
+      sm[SM::jdo + lane] = jd1;
+      jv = jve = jd1 = T(0);
+    }
     if (lane < 16) {
       if (lane < N && lane != pi) {
         const int Gp = pi >= nup ? 1 : 0;
@@ -1193,7 +1203,7 @@ k_walker_rev(KArgs ka) {
   }
   if constexpr (!PREP) {
     if (ka.value_only) {   // ECP quadrature configurations: log|psi| and phase only
-      const T jsum = wave_sum(jv + jve);
+      const T jsum = fwd_reg ? jsum_p : wave_sum(jv + jve);
       const T lpsi = logdet + jsum;
       if (lane == 0) {
         if (ka.logabs) ((T*)ka.logabs)[conf] = lpsi;
@@ -1801,7 +1811,7 @@ k_walker_rev(KArgs ka) {
 
   AQ_PH(7);
   // ------------------------------------------------------------------ B4 gradient per direction lane (c, e)
-  T g = jd1;
+  T g = fwd_reg ? sm[SM::jdo + lane] : jd1;
   if (!AQ_ABL(64)) {
     // four partial sums: the LDS reads and FMAs of one chain do not wait on each other
     T ga = T(0), gb = T(0), gc = T(0);
@@ -1828,7 +1838,7 @@ k_walker_rev(KArgs ka) {
   // ------------------------------------------------------------------ outputs
   const T gd = dir ? g : T(0);
   const T sumsq = wave_sum(gd * gd);
-  const T lpsi = logdet + wave_sum(jv + jve);
+  const T lpsi = logdet + (fwd_reg ? jsum_p : wave_sum(jv + jve));
   const auto* kl = late_args();
   if (kl->grad && dir) ((T*)kl->grad)[(size_t)conf * 3 * N + 3 * le + lc] = g;
   if (kl->gown && dir && le == pi) ((T*)kl->gown)[(size_t)conf * 3 + lc] = g;

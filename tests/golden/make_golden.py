@@ -25,8 +25,8 @@ from oracle import hamiltonian, mcstep, network, system  # noqa: E402
 
 torch.set_default_dtype(torch.float64)
 
-SYSTEMS = {"H2": 8, "Be": 8, "N2": 8, "Ne": 8, "C2": 4, "O2": 4}
-SEEDS = {"H2": 11, "Be": 12, "N2": 13, "Ne": 14, "C2": 16, "O2": 15}
+SYSTEMS = {"H2": 8, "Be": 8, "N2": 8, "Ne": 8, "C2": 4, "O2": 4, "C": 8}
+SEEDS = {"H2": 11, "Be": 12, "N2": 13, "Ne": 14, "C2": 16, "O2": 15, "C": 17}
 
 
 def make(name: str, B: int, out_dir: str):

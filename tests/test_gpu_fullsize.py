@@ -244,13 +244,14 @@ def test_other_shapes_local_energy_adjoint_vs_forward(name):
     assert torch.allclose(g1, g0, rtol=1e-8, atol=1e-8)
 
 
-@pytest.mark.parametrize("name", ["Be", "H2"])
+@pytest.mark.parametrize("name", ["Be", "H2", "C", "C2_ecp"])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_small_n_packed_proposals_match_one_wave_path(name, dtype):
     """N <= 4: the Metropolis proposals run four configurations per wave (quad_small.h
-    k_quad_grad); with the walker cache off every proposal goes through k_walker_rev's general
-    path instead.  Same host draws -> same trajectory (fp64: to 1e-10, identical accept
-    counts; fp32: all but rounding-level acceptance flips)."""
+    k_quad_grad); 5 <= N <= 8 (the all-electron C atom, C2 with ccECP -- the reference's example/C2): two
+    per wave in 32-lane slots (round 4).  With the walker cache off every proposal goes through
+    k_walker_rev's general path instead.  Same host draws -> same trajectory (fp64: to 1e-10,
+    identical accept counts; fp32: all but rounding-level acceptance flips)."""
     s, ctx = _ctx(name, dtype)
     B, NS, N = 1001, 3, s.nelectrons    # odd B: the last wave of the walker launch (and of H2's proposals) is partial
     x0 = torch.tensor(_walkers(s, B, seed=4), dtype=dtype, device="cuda")

@@ -16,7 +16,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-SYSTEMS = ["H2", "Be", "N2", "Ne", "C2", "O2"]   # (2,2) (4,1) (14,2) (10,1) (12,2) (16,2)
+SYSTEMS = ["H2", "Be", "N2", "Ne", "C2", "O2", "C"]   # (2,2) (4,1) (14,2) (10,1) (12,2) (16,2) (6,1)
 
 
 def _ctx(name, dtype):

@@ -32,19 +32,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _block(rank, world):
+def _block(rank, world, b_total=B_TOTAL):
     from aiqmc import systems
     from aiqmc.initial_electrons_positions.init import init_electrons
     s = systems.make_system("N2")
-    pos, _ = init_electrons(2024, None, s.atoms, s.charges, s.spins, B_TOTAL, 1.0)
-    n = B_TOTAL // world
+    pos, _ = init_electrons(2024, None, s.atoms, s.charges, s.spins, b_total, 1.0)
+    n = b_total // world
     return s, pos[rank * n:(rank + 1) * n]
 
 
-def _run_block(rank, world):
+def _run_block(rank, world, b_total=B_TOTAL):
     """mc_step + local_energy on this rank's block (fp32, Philox stream seed 77 + rank)."""
     from aiqmc import systems
-    s, pos = _block(rank, world)
+    s, pos = _block(rank, world, b_total)
     ctx = s.context(dtype=torch.float32)
     net = s.make_network()
     ctx.set_params(__import__("aiqmc.wavefunction_Ynlm.nn", fromlist=["flatten_params"]).flatten_params(net.init(9)))
@@ -65,7 +65,7 @@ torch.cuda.set_device(0)
 dist.init_process_group("gloo")
 import test_gpu_sharded as T
 from aiqmc import constants
-x, el = T._run_block(rank, world)
+x, el = T._run_block(rank, world, int(sys.argv[3]))
 mean, var = constants.pmean_stats(el.cpu())
 # the device path INTEGRATION.md advertises: aiqmc_energy_stats(finalize=False) -> all_reduce of the
 # rank's 4-vector -> aiqmc_energy_stats_final (gloo all-reduces the CUDA tensor here, RCCL on a node)
@@ -77,21 +77,23 @@ dist.destroy_process_group()
 '''
 
 
-def test_two_rank_blocks_equal_single_process(tmp_path):
-    world = 2
+@pytest.mark.parametrize("world,b_total", [(2, B_TOTAL), (8, 32768)])
+def test_two_rank_blocks_equal_single_process(tmp_path, world, b_total):
+    """(8, 32768): BASELINE config 4's walker count sharded 8 ways (4,096 per rank; the reference's
+    KFAC leg is out of scope), eight gloo ranks on the one test GPU."""
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
-        procs.append(subprocess.Popen([sys.executable, "-c", _WORKER, ROOT, str(tmp_path)], env=env))
+        procs.append(subprocess.Popen([sys.executable, "-c", _WORKER, ROOT, str(tmp_path), str(b_total)], env=env))
     for p in procs:
         assert p.wait(timeout=240) == 0
     outs = [dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(world)]
     from aiqmc import constants
     els = []
     for r in range(world):
-        x, el = _run_block(r, world)
+        x, el = _run_block(r, world, b_total)
         np.testing.assert_array_equal(outs[r]["x"], x.cpu().numpy())
         np.testing.assert_array_equal(outs[r]["el"], el.cpu().numpy())
         els.append(el.cpu())
@@ -106,9 +108,9 @@ def test_two_rank_blocks_equal_single_process(tmp_path):
     assert abs(float(var) - np.mean(np.abs(e - e.mean()) ** 2)) <= 1e-9 * np.var(e)
 
 
-def _bench_two_ranks(tmp_path, extra):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
+def _bench_two_ranks(tmp_path, extra, n=2):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps",
            "2", "--warmup", "1", "--no-cpu-baseline", "--no-ecp", "--no-adam", "--no-dmc",
            "--dist-backend", "gloo"] + extra
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
@@ -129,6 +131,15 @@ def test_bench_two_ranks_under_torchrun(tmp_path):
     assert r["value"] > 0 and r["roofline"]["avg_launch_ms"] > 0
     w = r["weak_scaling"]
     assert w["walkers_per_gpu"] == 256 and w["global_walkers"] == 512 and w["value"] > 0 and w["finite"]
+
+
+def test_bench_eight_ranks_under_torchrun(tmp_path):
+    """The driver's N = 8 launch line (gloo rehearsal, eight ranks on the one test GPU): the
+    default strong scaling splits BASELINE's 4,096 walkers into 512 per rank."""
+    r = _bench_two_ranks(tmp_path, [], n=8)
+    assert r["n_gpus"] == 8 and r["scaling"] == "strong" and r["finite"]
+    assert r["config"]["global_walkers"] == 4096 and r["config"]["walkers_per_gpu"] == 512
+    assert r["value"] > 0 and r["weak_scaling"]["walkers_per_gpu"] == 4096
 
 
 def test_bench_two_ranks_weak_headline(tmp_path):

@@ -32,7 +32,8 @@ if os.environ.get("AIQMC_HOST_DRAWS"):   # device-resident draws passed in (no P
 ctx.mc_step(pos, 10, 0.05, seed=1, offset=0, **draws)
 ctx.local_energy(pos)
 torch.cuda.synchronize()
-ctx.profile(True)
+noprof = bool(os.environ.get("AIQMC_NOPROF"))   # no HIP events around the launches
+ctx.profile(not noprof)
 t0 = time.perf_counter()
 for k in range(iters):
     ctx.mc_step(pos, 10, 0.05, seed=1, offset=10 * (k + 1), **draws)
