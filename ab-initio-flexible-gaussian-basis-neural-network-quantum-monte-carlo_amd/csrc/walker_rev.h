@@ -93,10 +93,13 @@ struct SmemRev {
   // region R, lifetimes disjoint: reuse scratch (F0..F2) -> {Phi [N][N][2], B [N][N][2]} (F5..B1)
   // -> dbar [N][N][3] (B3..B4)
   static constexpr int R = yv + N * N;
+  // FWDREG (proposals): Phi stays in registers (F5 -> B1), B alone in R, and F2's pair-patch
+  // scratch holds new - old differences [32][12] instead of the four parts [64][12]
   static constexpr int ph = R;
-  static constexpr int mx = R + N * N * 2;
+  static constexpr int mx = FWDREG ? R : R + N * N * 2;
   static constexpr int dbar = R;
-  static constexpr int R_n = cmax(cmax(4 * N * N, 3 * N * N), 4 + 64 * 12);
+  static constexpr int R_n = FWDREG ? cmax(cmax(2 * N * N, 3 * N * N), 4 + 32 * 12)
+                                    : cmax(cmax(4 * N * N, 3 * N * N), 4 + 64 * 12);
   // the walker's pivot record [2N+2] (proposals) lives in the g2 region during F5: the g2
   // values are dead after F4 and their adjoints are written from B2 on
   static constexpr int pv = g2;
@@ -556,10 +559,21 @@ k_walker_rev(KArgs ka) {
     for (int c = 0; c < 3; ++c) d[c] = (part < 2) ? xs[os * 3 + c] - xp[c] : xp[c] - xs[os * 3 + c];
     T v[3][4];
     pair_values<T, N, A>(d, P, v);
+    if constexpr (fwd_reg) {
+      // new - old: part 1 (3) sends its values to part 0 (2) sixteen lanes down; D[16 (part / 2) + o]
+#pragma unroll
+      for (int l = 0; l < 3; ++l)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const T w = __shfl_down(v[l][f], 16);
+          if ((part & 1) == 0) S[(16 * (part >> 1) + o) * 12 + l * 4 + f] = v[l][f] - w;
+        }
+    } else {
 #pragma unroll
     for (int l = 0; l < 3; ++l)
 #pragma unroll
       for (int f = 0; f < 4; ++f) S[lane * 12 + l * 4 + f] = v[l][f];
+    }
     if (part < 2 && o < N && o != pi) {
       if constexpr (!PROP) {
         cusp = P[Ly::jee_c + pi * N + o];
@@ -712,7 +726,8 @@ k_walker_rev(KArgs ka) {
         for (int l = 0; l < 3; ++l)
 #pragma unroll
           for (int f = 0; f < 4; ++f)
-            g2[((l * 2 + Gp) * N + lane) * 4 + f] += (S[lane * 12 + l * 4 + f] - S[(16 + lane) * 12 + l * 4 + f]) * gw;
+            g2[((l * 2 + Gp) * N + lane) * 4 + f] +=
+                (fwd_reg ? S[lane * 12 + l * 4 + f] : S[lane * 12 + l * 4 + f] - S[(16 + lane) * 12 + l * 4 + f]) * gw;
       }
     } else if (lane < 40) {
       const int t = lane - 16;
@@ -723,7 +738,7 @@ k_walker_rev(KArgs ka) {
       // issued together instead of one dependent round trip per electron of the group
 #pragma unroll
       for (int k = 0; k < N; ++k) {
-        const T dv = S[(32 + k) * 12 + l * 4 + f] - S[(48 + k) * 12 + l * 4 + f];
+        const T dv = fwd_reg ? S[(16 + k) * 12 + l * 4 + f] : S[(32 + k) * 12 + l * 4 + f] - S[(48 + k) * 12 + l * 4 + f];
         acc += (k >= k0 && k < k1 && k != pi) ? dv : T(0);
       }
       g2[((l * 2 + G) * N + pi) * 4 + f] += acc * (G ? ginv1 : ginv0);
@@ -1087,6 +1102,8 @@ k_walker_rev(KArgs ka) {
   // PROP: the Gauss-Jordan's register block, after it X = (P A)^{-1}: lane 16 rg + c holds
   // X[4 rg + t][c] = B[4 rg + t][rec[c]] in a2[t] (gj.h), kept for B1's Yt adjoint
   V2o a2[(N + 3) / 4];
+  // fwd_reg (compact proposal LDS): Phi[rec[rg RW + t]][c] of lane 16 rg + c, kept for B1 / fallback
+  V2o phr4[(N + 3) / 4];
   if (reuse) {
     // the walker's pivot order (partial pivoting rerun only if a pivot comes out small)
     bool bad = false;
@@ -1132,7 +1149,9 @@ k_walker_rev(KArgs ka) {
 #pragma unroll
         for (int t = 0; t < RW; ++t) {
           const bool ok = fl4[t] != 2 && cc < N;
-          if (ok) {
+          if constexpr (fwd_reg) {
+            phr4[t] = pair_make<T>(pre[t], pim[t]);
+          } else if (ok) {
             const int e = yo4[t] - SM::yv + cc;   // r N + c
             Ph[e * 2 + 0] = pre[t];
             Ph[e * 2 + 1] = pim[t];
@@ -1150,7 +1169,9 @@ k_walker_rev(KArgs ka) {
 #pragma unroll
         for (int f = 0; f < 4; ++f) acc = pair_fma<T>(sm[hd + f], w[4 + f], acc);
         const bool ok = fl != 2 && cc < N;
-        if (ok) {
+        if constexpr (fwd_reg) {
+          phr4[t] = acc;
+        } else if (ok) {
           const int e = yo - SM::yv + cc;   // r N + c
           Ph[e * 2 + 0] = pair_re<T>(acc);
           Ph[e * 2 + 1] = pair_im<T>(acc);
@@ -1181,8 +1202,27 @@ k_walker_rev(KArgs ka) {
 #ifdef AQ_PHASE_MARK
       AQ_PH(10);   // tools/isa_phases.py: the rarely taken pivoted fallback, counted apart
 #endif
-      gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi);
-      if constexpr (ybar_reg) {
+      if constexpr (fwd_reg) {
+        // compact layout: no Phi block in LDS; the pivoted inverse reads Phi from the B block it
+        // then overwrites (gj_inverse loads its whole input before it writes)
+        wave_sync();
+        const int cc = lane & 15, rg = lane >> 4;
+        constexpr int RW = (N + 3) / 4;
+#pragma unroll
+        for (int t = 0; t < RW; ++t) {
+          const int i = rg * RW + t;
+          if (i < N && cc < N) {
+            const int r = (int)sm[SM::pv + i];
+            Mx[(r * N + cc) * 2] = pair_re<T>(phr4[t]);
+            Mx[(r * N + cc) * 2 + 1] = pair_im<T>(phr4[t]);
+          }
+        }
+        wave_sync();
+        gj_inverse<T, N>(Mx, Yv, Mx, lane, logdet, phr, phi);
+      } else {
+        gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi);
+      }
+      if constexpr (ybar_reg && !fwd_reg) {
         // the register block of B for B1, from the pivoted inverse (natural layout in Mx)
         wave_sync();
         const int cc = lane & 15, rg = lane >> 4;
@@ -1379,6 +1419,25 @@ k_walker_rev(KArgs ka) {
     }
   }
   AQ_SYNC();   // ybar overwrites Yt
+  if constexpr (fwd_reg) {
+    // dL/dYt[r][c] = Re(B[c][r] Phi[r][c]) with Phi from F5's registers (lane 16 rg + c, slot
+    // rg RW + t, r = rec[slot]) and B from LDS
+    if (!AQ_ABL(8)) {
+      const int cc = lane & 15, rg = lane >> 4;
+      constexpr int RW = (N + 3) / 4;
+      if (cc < N) {
+#pragma unroll
+        for (int t = 0; t < RW; ++t) {
+          const int i = rg * RW + t;
+          if (i < N) {
+            const int r = (int)sm[SM::pv + i];
+            const int e = r * N + cc;
+            ybar[e] = Mx[(cc * N + r) * 2] * pair_re<T>(phr4[t]) - Mx[(cc * N + r) * 2 + 1] * pair_im<T>(phr4[t]);
+          }
+        }
+      }
+    }
+  } else
   if constexpr (ybar_reg) {
     // dL/dYt[r][c] = Re(B[c][r] Phi[r][c]) from the register block: B[c][r] = a2[t] of lane
     // 16 rg + cc with c = 4 rg + t, r = rec[cc] (no B reads, no per-element index division)
