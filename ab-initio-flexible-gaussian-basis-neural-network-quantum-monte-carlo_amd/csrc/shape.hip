@@ -300,6 +300,27 @@ static bool quad_small(const KArgs& ka, int nconf, hipStream_t s) {
   return false;
 }
 
+// fp32 N2 proposals of small batches (the per-rank share of a strong-scaling run): the PW7
+// instantiation (7 waves/SIMD, compact LDS) when it needs fewer rounds of waves than the 5-wave
+// one and the batch takes at most three of those (AIQMC_PW7=0 / 1 forces it off / on)
+static bool use_pw7(int nconf) {
+  static const int force = [] {
+    const char* e = std::getenv("AIQMC_PW7");
+    return e ? (e[0] == '0' ? 0 : 1) : -1;
+  }();
+  if (force >= 0) return force == 1;
+#ifndef AQ_PW7_DEFAULT
+  return false;   // off until measured
+#endif
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+    ncu = 256;
+  const long s5 = 20L * ncu, s7 = 28L * ncu;
+  const long r5 = (nconf + s5 - 1) / s5, r7 = (nconf + s7 - 1) / s7;
+  return r7 < r5 && r5 <= 3;
+}
+
 template <int N, int A>
 static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStream_t s) {
   if (mode == MODE_GRAD && (dtype == AIQMC_F32 ? quad_small<float, N, A>(ka, nconf, s) : quad_small<double, N, A>(ka, nconf, s)))
@@ -307,10 +328,20 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
   if (dtype == AIQMC_F32) {
     if (mode == MODE_LAP)
       k_walker<float, N, A, MODE_LAP><<<dim3(nconf), dim3(64), Smem<float, N, true>::bytes, s>>>(ka);
-    else if (mode == MODE_GRAD && ka.proposal && ka.ecache)   // proposals from the walker cache
+    else if (mode == MODE_GRAD && ka.proposal && ka.ecache) {   // proposals from the walker cache
+      if constexpr (N == 14 && A == 2) {
+        if (use_pw7(nconf)) {
+          k_walker_rev<float, N, A, false, true, true><<<dim3(prop_blocks(nconf, RevWpb<float, true>::value)),
+                                                        dim3(64 * RevWpb<float, true>::value),
+                                                        RevWpb<float, true>::value * SmemRev<float, N, A, kFwdReg, true>::bytes,
+                                                        s>>>(ka);
+          return;
+        }
+      }
       k_walker_rev<float, N, A, false, true><<<dim3(prop_blocks(nconf, RevWpb<float, true>::value)),
                                               dim3(64 * RevWpb<float, true>::value),
                                               RevWpb<float, true>::value * SmemRev<float, N, A, kFwdReg>::bytes, s>>>(ka);
+    }
     else if (mode == MODE_GRAD)
       k_walker_rev<float, N, A><<<dim3((nconf + RevWpb<float, false>::value - 1) / RevWpb<float, false>::value),
                                   dim3(64 * RevWpb<float, false>::value),

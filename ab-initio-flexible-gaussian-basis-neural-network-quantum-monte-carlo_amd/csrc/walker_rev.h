@@ -73,7 +73,7 @@ constexpr bool kFwdReg = true;
 #else
 constexpr bool kFwdReg = false;
 #endif
-template <typename T, int N, int A, bool FWDREG = false>
+template <typename T, int N, int A, bool FWDREG = false, bool COMPACT = false>
 struct SmemRev {
   static constexpr int D0 = 4 * A;               // layer-0 h width
   static constexpr int DFM = 3 * D0 + 8;         // widest conv input (layer 0)
@@ -93,13 +93,14 @@ struct SmemRev {
   // region R, lifetimes disjoint: reuse scratch (F0..F2) -> {Phi [N][N][2], B [N][N][2]} (F5..B1)
   // -> dbar [N][N][3] (B3..B4)
   static constexpr int R = yv + N * N;
-  // FWDREG (proposals): Phi stays in registers (F5 -> B1), B alone in R, and F2's pair-patch
-  // scratch holds new - old differences [32][12] instead of the four parts [64][12]
+  // COMPACT (the 7-waves/SIMD proposal instantiation): Phi stays in registers (F5 -> B1), B alone
+  // in R, and F2's pair-patch scratch holds new - old differences [32][12] instead of the four parts
+  // [64][12]: 5.6 KB per wave for N2 (28 waves/CU fit the 160 KB)
   static constexpr int ph = R;
-  static constexpr int mx = FWDREG ? R : R + N * N * 2;
+  static constexpr int mx = COMPACT ? R : R + N * N * 2;
   static constexpr int dbar = R;
-  static constexpr int R_n = FWDREG ? cmax(cmax(2 * N * N, 3 * N * N), 4 + 32 * 12)
-                                    : cmax(cmax(4 * N * N, 3 * N * N), 4 + 64 * 12);
+  static constexpr int R_n = COMPACT ? cmax(cmax(2 * N * N, 3 * N * N), 4 + 32 * 12)
+                                     : cmax(cmax(4 * N * N, 3 * N * N), 4 + 64 * 12);
   // the walker's pivot record [2N+2] (proposals) lives in the g2 region during F5: the g2
   // values are dead after F4 and their adjoints are written from B2 on
   static constexpr int pv = g2;
@@ -412,8 +413,8 @@ __global__ __launch_bounds__(64 * MOVED_WPB) void k_moved_value(KArgs ka) {
 #ifndef AQ_PREP_WAVES
 #define AQ_PREP_WAVES 4
 #endif
-template <typename T, int N, int A, bool PREP, bool PROP> struct RevWaves {
-  static constexpr int value = PREP ? (sizeof(T) == 4 ? AQ_PREP_WAVES : 2) : ((sizeof(T) == 4 && N == 14 && A == 2) ? (PROP ? AQ_PROP_WAVES : 4) : 1);
+template <typename T, int N, int A, bool PREP, bool PROP, bool PW7 = false> struct RevWaves {
+  static constexpr int value = PW7 ? 7 : (PREP ? (sizeof(T) == 4 ? AQ_PREP_WAVES : 2) : ((sizeof(T) == 4 && N == 14 && A == 2) ? (PROP ? AQ_PROP_WAVES : 4) : 1));
 };
 
 // PREP = false: value + gradient (Metropolis walker launches and single-electron proposal / ECP
@@ -445,16 +446,21 @@ template <typename T, bool PROP, bool PREP = false> struct RevWpb {
   } while (0)
 #endif
 
-template <typename T, int N, int A, bool PREP = false, bool PROP = false>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * RevWpb<T, PROP, PREP>::value))) __attribute__((amdgpu_waves_per_eu(RevWaves<T, N, A, PREP, PROP>::value))) void
+// PW7 (proposals only): the small-batch instantiation, compiled for 7 waves/SIMD with the COMPACT
+// LDS layout, so that the B N proposals of a strong-scaling rank (512 N2 walkers: 7,168 waves) run
+// in one round instead of 1.4 (shape.hip chooses it by batch size)
+template <typename T, int N, int A, bool PREP = false, bool PROP = false, bool PW7 = false>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * RevWpb<T, PROP, PREP>::value))) __attribute__((amdgpu_waves_per_eu(RevWaves<T, N, A, PREP, PROP, PW7>::value))) void
 k_walker_rev(KArgs ka) {
+  static_assert(!PW7 || (PROP && !PREP), "PW7 is a proposal instantiation");
   using Ly = Lay<N, A>;
   constexpr bool fwd_reg = PROP && kFwdReg;
+  constexpr bool compact = PROP && PW7 && fwd_reg;
   // the lane-order weight blocks in F4 / B2: proposals only (round 4, interleaved A/B on one box:
   // proposal launch 216.3-219.0 -> 215.1-218.2 us; the same in the walker launch and the local
   // energy's adjoint pass measured +0.5 us and +7-11 us per launch, profiles/r04_s5_ab_xlane.txt)
   constexpr bool xlane = PROP && kXLane;
-  using SM = SmemRev<T, N, A, fwd_reg>;
+  using SM = SmemRev<T, N, A, fwd_reg, compact>;
   using LCc = LapCache<N, A>;
   constexpr int D0 = SM::D0;
   constexpr int WPB = RevWpb<T, PROP, PREP>::value;
@@ -559,7 +565,7 @@ k_walker_rev(KArgs ka) {
     for (int c = 0; c < 3; ++c) d[c] = (part < 2) ? xs[os * 3 + c] - xp[c] : xp[c] - xs[os * 3 + c];
     T v[3][4];
     pair_values<T, N, A>(d, P, v);
-    if constexpr (fwd_reg) {
+    if constexpr (compact) {
       // new - old: part 1 (3) sends its values to part 0 (2) sixteen lanes down; D[16 (part / 2) + o]
 #pragma unroll
       for (int l = 0; l < 3; ++l)
@@ -727,7 +733,7 @@ k_walker_rev(KArgs ka) {
 #pragma unroll
           for (int f = 0; f < 4; ++f)
             g2[((l * 2 + Gp) * N + lane) * 4 + f] +=
-                (fwd_reg ? S[lane * 12 + l * 4 + f] : S[lane * 12 + l * 4 + f] - S[(16 + lane) * 12 + l * 4 + f]) * gw;
+                (compact ? S[lane * 12 + l * 4 + f] : S[lane * 12 + l * 4 + f] - S[(16 + lane) * 12 + l * 4 + f]) * gw;
       }
     } else if (lane < 40) {
       const int t = lane - 16;
@@ -738,7 +744,7 @@ k_walker_rev(KArgs ka) {
       // issued together instead of one dependent round trip per electron of the group
 #pragma unroll
       for (int k = 0; k < N; ++k) {
-        const T dv = fwd_reg ? S[(16 + k) * 12 + l * 4 + f] : S[(32 + k) * 12 + l * 4 + f] - S[(48 + k) * 12 + l * 4 + f];
+        const T dv = compact ? S[(16 + k) * 12 + l * 4 + f] : S[(32 + k) * 12 + l * 4 + f] - S[(48 + k) * 12 + l * 4 + f];
         acc += (k >= k0 && k < k1 && k != pi) ? dv : T(0);
       }
       g2[((l * 2 + G) * N + pi) * 4 + f] += acc * (G ? ginv1 : ginv0);
@@ -1102,7 +1108,7 @@ k_walker_rev(KArgs ka) {
   // PROP: the Gauss-Jordan's register block, after it X = (P A)^{-1}: lane 16 rg + c holds
   // X[4 rg + t][c] = B[4 rg + t][rec[c]] in a2[t] (gj.h), kept for B1's Yt adjoint
   V2o a2[(N + 3) / 4];
-  // fwd_reg (compact proposal LDS): Phi[rec[rg RW + t]][c] of lane 16 rg + c, kept for B1 / fallback
+  // compact: Phi[rec[rg RW + t]][c] of lane 16 rg + c, kept for B1 / the fallback
   V2o phr4[(N + 3) / 4];
   if (reuse) {
     // the walker's pivot order (partial pivoting rerun only if a pivot comes out small)
@@ -1149,7 +1155,7 @@ k_walker_rev(KArgs ka) {
 #pragma unroll
         for (int t = 0; t < RW; ++t) {
           const bool ok = fl4[t] != 2 && cc < N;
-          if constexpr (fwd_reg) {
+          if constexpr (compact) {
             phr4[t] = pair_make<T>(pre[t], pim[t]);
           } else if (ok) {
             const int e = yo4[t] - SM::yv + cc;   // r N + c
@@ -1169,7 +1175,7 @@ k_walker_rev(KArgs ka) {
 #pragma unroll
         for (int f = 0; f < 4; ++f) acc = pair_fma<T>(sm[hd + f], w[4 + f], acc);
         const bool ok = fl != 2 && cc < N;
-        if constexpr (fwd_reg) {
+        if constexpr (compact) {
           phr4[t] = acc;
         } else if (ok) {
           const int e = yo - SM::yv + cc;   // r N + c
@@ -1202,7 +1208,7 @@ k_walker_rev(KArgs ka) {
 #ifdef AQ_PHASE_MARK
       AQ_PH(10);   // tools/isa_phases.py: the rarely taken pivoted fallback, counted apart
 #endif
-      if constexpr (fwd_reg) {
+      if constexpr (compact) {
         // compact layout: no Phi block in LDS; the pivoted inverse reads Phi from the B block it
         // then overwrites (gj_inverse loads its whole input before it writes)
         wave_sync();
@@ -1222,7 +1228,7 @@ k_walker_rev(KArgs ka) {
       } else {
         gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi);
       }
-      if constexpr (ybar_reg && !fwd_reg) {
+      if constexpr (ybar_reg && !compact) {
         // the register block of B for B1, from the pivoted inverse (natural layout in Mx)
         wave_sync();
         const int cc = lane & 15, rg = lane >> 4;
@@ -1419,7 +1425,7 @@ k_walker_rev(KArgs ka) {
     }
   }
   AQ_SYNC();   // ybar overwrites Yt
-  if constexpr (fwd_reg) {
+  if constexpr (compact) {
     // dL/dYt[r][c] = Re(B[c][r] Phi[r][c]) with Phi from F5's registers (lane 16 rg + c, slot
     // rg RW + t, r = rec[slot]) and B from LDS
     if (!AQ_ABL(8)) {
