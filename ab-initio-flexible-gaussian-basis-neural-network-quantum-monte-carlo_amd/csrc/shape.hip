@@ -301,17 +301,18 @@ static bool quad_small(const KArgs& ka, int nconf, hipStream_t s) {
 }
 
 // fp32 N2 proposals of small batches (the per-rank share of a strong-scaling run): the PW7
-// instantiation (7 waves/SIMD, compact LDS) when it needs fewer rounds of waves than the 5-wave
-// one and the batch takes at most three of those (AIQMC_PW7=0 / 1 forces it off / on)
+// instantiation (7 waves/SIMD, compact LDS; walker_rev.h) when it needs fewer rounds of waves than
+// the 5-wave one and the batch takes at most three of those.  Measured slower at every batch size
+// (N2, 512 / 1024 / 2048 walkers: proposal launch 40.3 -> 43.8, 65.9 -> 74.5, 116.0 -> 130.2 us,
+// profiles/r04_s8_ab_pw7.txt), so it is compiled only with -DAQ_PW7 (AIQMC_PW7=0 / 1 forces it
+// off / on there).
+#ifdef AQ_PW7
 static bool use_pw7(int nconf) {
   static const int force = [] {
     const char* e = std::getenv("AIQMC_PW7");
     return e ? (e[0] == '0' ? 0 : 1) : -1;
   }();
   if (force >= 0) return force == 1;
-#ifndef AQ_PW7_DEFAULT
-  return false;   // off until measured
-#endif
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
@@ -320,6 +321,7 @@ static bool use_pw7(int nconf) {
   const long r5 = (nconf + s5 - 1) / s5, r7 = (nconf + s7 - 1) / s7;
   return r7 < r5 && r5 <= 3;
 }
+#endif
 
 template <int N, int A>
 static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStream_t s) {
@@ -329,6 +331,7 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
     if (mode == MODE_LAP)
       k_walker<float, N, A, MODE_LAP><<<dim3(nconf), dim3(64), Smem<float, N, true>::bytes, s>>>(ka);
     else if (mode == MODE_GRAD && ka.proposal && ka.ecache) {   // proposals from the walker cache
+#ifdef AQ_PW7
       if constexpr (N == 14 && A == 2) {
         if (use_pw7(nconf)) {
           k_walker_rev<float, N, A, false, true, true><<<dim3(prop_blocks(nconf, RevWpb<float, true>::value)),
@@ -338,6 +341,7 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
           return;
         }
       }
+#endif
       k_walker_rev<float, N, A, false, true><<<dim3(prop_blocks(nconf, RevWpb<float, true>::value)),
                                               dim3(64 * RevWpb<float, true>::value),
                                               RevWpb<float, true>::value * SmemRev<float, N, A, kFwdReg>::bytes, s>>>(ka);

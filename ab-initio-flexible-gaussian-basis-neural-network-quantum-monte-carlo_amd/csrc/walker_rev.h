@@ -446,7 +446,7 @@ template <typename T, bool PROP, bool PREP = false> struct RevWpb {
   } while (0)
 #endif
 
-// PW7 (proposals only): the small-batch instantiation, compiled for 7 waves/SIMD with the COMPACT
+// PW7 (proposals only, -DAQ_PW7 builds: measured slower, shape.hip): the small-batch instantiation, compiled for 7 waves/SIMD with the COMPACT
 // LDS layout, so that the B N proposals of a strong-scaling rank (512 N2 walkers: 7,168 waves) run
 // in one round instead of 1.4 (shape.hip chooses it by batch size)
 template <typename T, int N, int A, bool PREP = false, bool PROP = false, bool PW7 = false>

@@ -19,4 +19,8 @@ for B in 512 1024 2048; do
     echo "pw7=$t events $r" | tee -a $out
   done
 done
+for rep in 1 2; do
+  echo "philox $(AIQMC_NOPROF=1 timeout -k 10 120 python tools/mc_loop.py 20 N2 512)" | tee -a $out || exit 1
+  echo "host   $(AIQMC_NOPROF=1 AIQMC_HOST_DRAWS=1 timeout -k 10 120 python tools/mc_loop.py 20 N2 512)" | tee -a $out || exit 1
+done
 AIQMC_PW7=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_mc_fp32.py tests/test_precision_fp32.py tests/test_gpu_parity.py -m gpu -q -rf --timeout 180 --timeout-method thread > gpurun_out/parity_pw7.log 2>&1; echo "parity rc=$?"; tail -3 gpurun_out/parity_pw7.log
