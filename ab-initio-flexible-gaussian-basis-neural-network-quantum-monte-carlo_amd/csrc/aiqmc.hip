@@ -829,7 +829,7 @@ int aiqmc_debug_local_energy_forward(aiqmc_ctx* c, const void* pos, int32_t B, v
 static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double tstep, int rng_mode, const void* gauss1,
                     const void* gauss2, const void* u, int st, uint64_t seed, uint64_t step, int32_t* accept_out,
                     double* dmc, hipStream_t s, AccArgs* pending = nullptr, bool defer = false,
-                    unsigned long long* tacc = nullptr, unsigned long long* tpart = nullptr) {
+                    unsigned long long* tacc = nullptr, unsigned long long* tpart = nullptr, bool pvok = false) {
   const int N = c->N;
   if (dmc) tacc = nullptr;
   if (dmc || tacc || c->dtype != AIQMC_F32) tpart = nullptr;
@@ -857,6 +857,7 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
   ka.sumsq = c->d_sq;
   ka.tacc = tacc;
   ka.wcache = c->d_wc;
+  ka.pvok = (pvok && c->walker_fixed_gj) ? 1 : 0;
   ka.tstep = tstep;
   ka.seed = seed;
   ka.step = step;
@@ -1015,7 +1016,7 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
   for (int st = 0; st < nsteps; ++st) {
     rc = mc_sweep(c, ops, pos, B, tstep, rng_mode, gauss1, gauss2, u, st, seed, offset + (uint64_t)st, accept_out,
                   nullptr, s, &pending, c->fuse_accept && st + 1 < nsteps, tacc ? tacc + 2 * TACC_STRIDE * st : nullptr,
-                  tpart ? tpart + 2 * TPART_KIND * st : nullptr);
+                  tpart ? tpart + 2 * TPART_KIND * st : nullptr, st > 0);
     if (rc) return rc;
   }
   HIPCHK(hipGetLastError());
@@ -1543,6 +1544,12 @@ int aiqmc_debug_set_lap_waves(aiqmc_ctx* c, int32_t waves) {
 int aiqmc_debug_set_fuse_accept(aiqmc_ctx* c, int32_t on) {
   if (!c) return fail(AIQMC_EINVAL, "null context");
   c->fuse_accept = on != 0;
+  return AIQMC_OK;
+}
+
+int aiqmc_debug_set_walker_pivots(aiqmc_ctx* c, int32_t reuse) {
+  if (!c) return fail(AIQMC_EINVAL, "null context");
+  c->walker_fixed_gj = reuse != 0;
   return AIQMC_OK;
 }
 

@@ -202,9 +202,14 @@ __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, in
 // rec: the walker's record written by gj_inverse (LDS copy).
 // The elimination of gj_inverse_fixed on a matrix already in its register layout:
 // a2[t] = A[rec[rg RW + t]][c] for lane 16 rg + c (zero outside the N x N block).
+// rec_out (optional; a walker launch re-using its previous sweep's order): log|det A| is formed
+// from this matrix's own pivots (gj_inverse's mantissa / exponent product, so that it does not
+// drift from sweep to sweep through the relative form) and, unless bad, the record's magnitudes
+// and log|det| are rewritten for this matrix (rec_out[N + k], rec_out[2N + 1]; the order and
+// its parity are unchanged), so that the walker's proposals are relative to it.
 template <typename T, int N>
 __device__ __forceinline__ void gj_fixed_regs(typename Pair<T>::type* a2, T* Bout, int lane, const T* rec,
-                                              T& logdet, T& phr, T& phi, bool& bad) {
+                                              T& logdet, T& phr, T& phi, bool& bad, T* rec_out = nullptr) {
   constexpr int RW = (N + 3) / 4;
   using V2 = typename Pair<T>::type;
   const int c = lane & 15;
@@ -294,11 +299,34 @@ __device__ __forceinline__ void gj_fixed_regs(typename Pair<T>::type* a2, T* Bou
   phr = zr * sg;
   phi = zi * sg;
   bad = small || !zok;
+  if (rec_out) {
+    const bool pl = lane < N;
+    const T den = pkr * pkr + pki * pki;
+    int e = 0;
+    T m = pl ? f_frexp(den, e) : T(1);
+    T ef = pl ? T(e) : T(0);
+    // product of the mantissas (each in [1/2, 1): no underflow for N <= 16) and sum of the
+    // exponents over lanes 0..15 by the row_ror tree above
+    m *= dpp<0x128>(m);
+    ef += dpp<0x128>(ef);
+    m *= dpp<0x124>(m);
+    ef += dpp<0x124>(ef);
+    m *= dpp<0x122>(m);
+    ef += dpp<0x122>(ef);
+    m *= dpp<0x121>(m);
+    ef += dpp<0x121>(ef);
+    const T ld = T(0.5) * (f_log(rdlane(m, 0)) + rdlane(ef, 0) * T(0.69314718055994531));
+    logdet = ld;
+    if (!bad) {
+      if (pl) rec_out[N + lane] = f_sqrt(f_rcp(den));
+      if (lane == 0) rec_out[2 * N + 1] = ld;
+    }
+  }
 }
 
 template <typename T, int N>
 __device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bout, int lane, const T* rec,
-                                                 T& logdet, T& phr, T& phi, bool& bad) {
+                                                 T& logdet, T& phr, T& phi, bool& bad, T* rec_out = nullptr) {
   constexpr int RW = (N + 3) / 4;
   using V2 = typename Pair<T>::type;
   const int c = lane & 15;
@@ -317,7 +345,7 @@ __device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bo
     }
     a2[t] = pair_make<T>(a, b);
   }
-  gj_fixed_regs<T, N>(a2, Bout, lane, rec, logdet, phr, phi, bad);
+  gj_fixed_regs<T, N>(a2, Bout, lane, rec, logdet, phr, phi, bad, rec_out);
 }
 
 }  // namespace aq

@@ -259,6 +259,10 @@ struct KArgs {
   // walker launch of a Metropolis sweep: acc.lpn != nullptr: first apply the PREVIOUS sweep's
   // acceptance to walker conf (fused k_accept; one launch fewer per sweep)
   AccArgs acc;
+  // walker launch of a Metropolis sweep after the first of an mc_step call: the walker cache holds
+  // this walker's pivot record of the previous sweep; the Gauss-Jordan re-uses that order (the
+  // pivoted elimination only if a pivot comes out small)
+  int pvok;
   // Metropolis caches (walker_rev.h WCache / ECache); nullptr outside aiqmc_mc_step
   void* wcache;
   void* ecache;

@@ -541,6 +541,8 @@ k_walker_rev(KArgs ka) {
   // the cached path is compiled there only (the general one serves walker launches, reuse-off
   // proposals and plain value+gradient calls)
   const bool reuse = !PREP && PROP;
+  // walker launch re-using its previous sweep's pivot order (F5; KArgs::pvok)
+  const bool wfix = !PREP && !PROP && !isprop && ka.pvok != 0;
   T* Wc = (T*)ka.wcache + (size_t)(reuse ? pb : conf) * WC::size;
   T* Lw = PREP ? (T*)ka.lapcache + (size_t)conf * LCc::size : nullptr;
   const T* Eq = reuse ? (const T*)ka.ecache + (size_t)conf * EC::size : nullptr;
@@ -673,6 +675,7 @@ k_walker_rev(KArgs ka) {
     for (int t = 0; t < NG; ++t)
       if (lane + 64 * t < 3 * 2 * N * 4) g2[lane + 64 * t] = rg[t];
   } else {
+    if (wfix) pvr = Wc[WC::pv + (lane < 2 * N + 2 ? lane : 2 * N + 1)];   // to LDS after F4, before F5's write
     ElecOut<T, A> eo;
     electron_stage<T, N, A>(P, xs + le * 3, le, lc, eo);
     // d(Yt row)/dx and d(ae features)/dx of this lane's electron -> walker cache (read in B4)
@@ -1053,7 +1056,7 @@ k_walker_rev(KArgs ka) {
   }
   if (ilive) hl[SM::hoff(3) + ic * 4 + ff] = hreg;
   AQ_SYNC();
-  if (reuse && lane < 2 * N + 2) sm[SM::pv + lane] = pvr;   // read by the Gauss-Jordan after the Phi barrier
+  if ((reuse || wfix) && lane < 2 * N + 2) sm[SM::pv + lane] = pvr;   // read by the Gauss-Jordan after the Phi barrier
   if constexpr (PROP) {
     // F5's slot table: slot k (pivot step k) holds row r = rec[k]; it records the offsets of
     // that row's Yt row and of its h^3 row (electron rowsrc[r]) in the half of the
@@ -1245,7 +1248,13 @@ k_walker_rev(KArgs ka) {
 #endif
     }
   } else {
-    gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi, (!PREP && !isprop) ? Wc + WC::pv : nullptr);
+    // walker launches after an mc_step's first sweep: the previous sweep's pivot order (no pivot
+    // search: gj_inverse's per-step argmax over the column is most of its latency), log|det| from
+    // this matrix's own pivots, the record's magnitudes refreshed for the proposals; the pivoted
+    // elimination if a pivot comes out below 0.1 of the previous one (it then rewrites the record)
+    bool bad = true;
+    if (wfix) gj_inverse_fixed<T, N>(Ph, Yv, Mx, lane, sm + SM::pv, logdet, phr, phi, bad, Wc + WC::pv);
+    if (bad) gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi, (!PREP && !isprop) ? Wc + WC::pv : nullptr);
   }
   if constexpr (!PREP) {
     if (ka.value_only) {   // ECP quadrature configurations: log|psi| and phase only

@@ -270,6 +270,12 @@ int aiqmc_debug_set_lap_waves(aiqmc_ctx* ctx, int32_t waves);
  * sweep.  Both are bitwise identical (same arithmetic, same order). */
 int aiqmc_debug_set_fuse_accept(aiqmc_ctx* ctx, int32_t on);
 
+/* Diagnostics: from the second sweep of an aiqmc_mc_step call on, the walker launch's
+ * Gauss-Jordan elimination takes the walker's pivot order of the previous sweep (default,
+ * reuse = 1; partial pivoting only when a pivot comes out below 0.1 of the previous one);
+ * reuse = 0 runs partial pivoting in every sweep.  Results agree to rounding. */
+int aiqmc_debug_set_walker_pivots(aiqmc_ctx* ctx, int32_t reuse);
+
 /* Diagnostics: in fp32, aiqmc_mc_step can sum the two limdrift reductions of each sweep
  * (|grad|^2 over the walkers, over the proposals; VMCmcstep.py:11-14) inside the walker and
  * proposal launches, as exact 64-bit integer sums of |grad|^2 in units of 2^-16: no reduction

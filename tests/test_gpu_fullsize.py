@@ -172,6 +172,38 @@ def test_fused_acceptance_is_bitwise_identical(dtype, draws):
     assert int(acc_a.sum()) > 0 and not torch.equal(a, x0)
 
 
+@pytest.mark.parametrize("name,dtype", [("N2", torch.float64), ("C", torch.float64), ("N2", torch.float32)])
+def test_walker_pivot_reuse_matches_partial_pivoting(name, dtype):
+    """From an mc_step's second sweep on, the walker launch eliminates in its previous sweep's
+    pivot order (partial pivoting only when a pivot shrinks below 0.1 of the previous one) and
+    refreshes the pivot record its proposals are relative to.  Against partial pivoting in every
+    sweep (aiqmc_debug_set_walker_pivots(0)), six host-draw sweeps: fp64 positions to 1e-10 with
+    equal accept counts; fp32 positions to 1e-5 except where rounding flips a near-tie acceptance."""
+    s, ctx = _ctx(name, dtype)
+    B, NS, N = 4096, 6, s.nelectrons
+    x0 = torch.tensor(_walkers(s, B, seed=21), dtype=dtype, device="cuda")
+    g = torch.Generator().manual_seed(5)
+    kw = dict(gauss1=torch.randn(NS, B, 3 * N, generator=g, dtype=torch.float64),
+              gauss2=torch.randn(NS, B, N, 3, generator=g, dtype=torch.float64),
+              u=torch.rand(NS, B, N, generator=g, dtype=torch.float64))
+    a = x0.clone().contiguous()
+    b = x0.clone().contiguous()
+    acc_a = ctx.mc_step(a, NS, 0.05, count_accepts=True, **kw)
+    ctx.set_walker_pivots(False)
+    acc_b = ctx.mc_step(b, NS, 0.05, count_accepts=True, **kw)
+    ctx.set_walker_pivots(True)
+    torch.cuda.synchronize()
+    assert int(acc_a.sum()) > 0 and not torch.equal(a, x0)
+    dw = (a - b).abs().reshape(B, -1).amax(1)
+    if dtype == torch.float64:
+        assert float(dw.max()) < 1e-10, float(dw.max())
+        assert torch.equal(acc_a, acc_b)
+    else:
+        flipped = dw > 1e-4
+        assert float(flipped.float().mean()) < 2e-3, float(flipped.float().mean())
+        assert float(dw[~flipped].max()) < 1e-5, float(dw[~flipped].max())
+
+
 def test_proposal_reuse_matches_recompute_f32_4096():
     s, ctx = _ctx("N2", torch.float32)
     x0 = torch.tensor(_walkers(s, 4096, seed=10), dtype=torch.float32, device="cuda")

@@ -19,6 +19,8 @@ if os.environ.get("AIQMC_FUSE_REDUCE"):     # 0: integer reduction launches, 1: 
     ctx.set_fuse_reduce(int(os.environ["AIQMC_FUSE_REDUCE"]))
 if os.environ.get("AIQMC_LAPW"):      # waves per walker of the local energy's second launch
     ctx.set_lap_waves(int(os.environ["AIQMC_LAPW"]))
+if os.environ.get("AIQMC_WPIV") == "0":   # walker launches: partial pivoting every sweep
+    ctx.set_walker_pivots(False)
 if os.environ.get("AIQMC_NOREUSE"):   # every proposal from scratch (PMC comparison of the two paths)
     ctx.set_proposal_reuse(False)
 pos = init_electrons(1000, None, s.atoms, s.charges, s.spins, B, 1.0)[0].to("cuda", torch.float32).contiguous()
