@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_debug_set_proposal_reuse", "aiqmc_debug_phase_cycles", "aiqmc_debug_local_energy_forward",
     "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
     "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves", "aiqmc_phase_param_grad",
-    "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals", "aiqmc_debug_set_ablate", "aiqmc_debug_set_fuse_accept", "aiqmc_debug_set_walker_pivots", "aiqmc_debug_set_lap_waves",
+    "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals", "aiqmc_debug_set_ablate", "aiqmc_debug_set_fuse_accept", "aiqmc_debug_set_walker_pivots", "aiqmc_debug_set_packed_walkers", "aiqmc_debug_set_lap_waves",
     "aiqmc_debug_set_fuse_reduce", "aiqmc_energy_stats", "aiqmc_energy_stats_final",
     "aiqmc_debug_limdrift_factor",
 )
@@ -130,6 +130,8 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_debug_set_fuse_accept.restype = ctypes.c_int
     lib.aiqmc_debug_set_walker_pivots.argtypes = [vp, i32]
     lib.aiqmc_debug_set_walker_pivots.restype = ctypes.c_int
+    lib.aiqmc_debug_set_packed_walkers.argtypes = [vp, i32]
+    lib.aiqmc_debug_set_packed_walkers.restype = ctypes.c_int
     lib.aiqmc_debug_set_fuse_reduce.argtypes = [vp, i32]
     lib.aiqmc_debug_set_fuse_reduce.restype = ctypes.c_int
     lib.aiqmc_debug_limdrift_factor.argtypes = [vp, vp, i32, ctypes.c_double, i32,
@@ -353,6 +355,10 @@ class Context:
         """Diagnostics: walker launches after an mc_step's first sweep re-use the previous sweep's
         Gauss-Jordan pivot order (default) or run partial pivoting every sweep."""
         check(self._lib.aiqmc_debug_set_walker_pivots(self._h, int(bool(reuse))), "aiqmc_debug_set_walker_pivots")
+
+    def set_packed_walkers(self, on: bool):
+        """Diagnostics: walker launches of N <= 8 several per wave (default) or one wave each."""
+        check(self._lib.aiqmc_debug_set_packed_walkers(self._h, int(bool(on))), "aiqmc_debug_set_packed_walkers")
 
     def set_fuse_reduce(self, mode):
         """Diagnostics: fp32 mc_step limdrift sums fused into the walker / proposal launches as

@@ -682,6 +682,7 @@ static KArgs base_args(const aiqmc_ctx* c) {
   ka.nup = c->nup;
   ka.rowsrc = c->d_rowsrc;
   ka.prm = c->d_prm;
+  ka.one_wave = c->packed_walkers ? 0 : 1;
   return ka;
 }
 
@@ -1544,6 +1545,12 @@ int aiqmc_debug_set_lap_waves(aiqmc_ctx* c, int32_t waves) {
 int aiqmc_debug_set_fuse_accept(aiqmc_ctx* c, int32_t on) {
   if (!c) return fail(AIQMC_EINVAL, "null context");
   c->fuse_accept = on != 0;
+  return AIQMC_OK;
+}
+
+int aiqmc_debug_set_packed_walkers(aiqmc_ctx* c, int32_t on) {
+  if (!c) return fail(AIQMC_EINVAL, "null context");
+  c->packed_walkers = on != 0;
   return AIQMC_OK;
 }
 

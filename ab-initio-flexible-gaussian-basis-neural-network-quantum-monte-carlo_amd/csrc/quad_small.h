@@ -466,7 +466,7 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
 //      Jacobians (walker cache, or the moved electron's record).
 // Outputs as the proposal path: log|psi|, |grad|^2, the moved electron's own gradient (and
 // the full gradient / phase when asked).
-template <typename T, int N, int A>
+template <typename T, int N, int A, bool WALK = false>
 struct SmemQG {
   static constexpr int D0 = 4 * A;
   static constexpr int NI = QSlot<N>::NI, SW = QSlot<N>::SW;   // electron slots, lanes per configuration
@@ -479,8 +479,8 @@ struct SmemQG {
   static constexpr int hl = yv + NI * NI;        // h^0 [NI][D0], h^3 [NI][4]; then their adjoints
   static constexpr int h3 = hl + NI * D0;
   static constexpr int g2 = h3 + NI * 4;         // [3][2][N][4] pair column means, then their adjoints
-  static constexpr int S = g2 + 24 * NI;         // [SW][12] patch pair values; then dbar [N][N][3]
-  static constexpr int cq = S + cmax(SW * 12, 3 * NI * NI);   // conv outputs [NI][QM] + [2][NI][QL]
+  static constexpr int S = g2 + 24 * NI;         // [SW][12] patch pair values (WALK: [N][N][12] all pairs); then dbar [N][N][3]
+  static constexpr int cq = S + cmax(cmax(SW * 12, 3 * NI * NI), WALK ? 12 * N * N : 0);   // conv outputs [NI][QM] + [2][NI][QL]
   static constexpr int sv = cq + NI * QM + 2 * NI * QL;      // [3][NI][4] single outputs
   static constexpr int ph = sv + 12 * NI;        // [N][N][2] Phi
   static constexpr int mx = ph + 2 * NI * NI;    // [N][N][2] B = A^{-1}
@@ -497,16 +497,18 @@ struct SmemQG {
 // spin-group class sums take one lane exchange across the slot's two 16-lane rows, the Gauss-Jordan
 // holds two matrix elements per lane (lane 4 r + g: columns g and g + 4 of row r; the pivot is the
 // packed-key max over the slot's eight row quads, as k_quad_value's LU), B3 runs the N (N - 1)
-// pairs in two passes of 32, and B4 puts direction x_{e,c} on lane 8 c + e.  The walker launches of
-// these shapes stay on k_walker_rev (WALK is N <= 4 only).
+// pairs in two passes of 32, and B4 puts direction x_{e,c} on lane 8 c + e.  WALK for these shapes
+// (round 4, second session): the walker launches two per wave as well -- F1's electron stage on
+// lane 8 c + e (B4's lane, so the local Jacobians stay in registers), the N^2 pair stream in two
+// passes of 32 lanes into a [N][N][12] block, and the pivot record written by the two-element
+// Gauss-Jordan.
 template <typename T, int N, int A, bool WALK = false>
 __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
   static_assert(N <= 8, "k_quad_grad: several configurations per wave need N <= 8");
-  static_assert(!WALK || N <= 4, "k_quad_grad: the packed walker launch is built for N <= 4");
   using Ly = Lay<N, A>;
   using WC = WCache<N, A>;
   using EC = ECache<N, A>;
-  using SQ = SmemQG<T, N, A>;
+  using SQ = SmemQG<T, N, A, WALK>;
   constexpr int D0 = 4 * A;
   constexpr int QM = SQ::QM;
   constexpr int SW = QSlot<N>::SW, NI = QSlot<N>::NI, NSL = QSlot<N>::NSL;
@@ -536,7 +538,7 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
   const T ginv0 = T(1) / T(nup), ginv1 = T(1) / T(N - nup);
   T* Wc = (T*)ka.wcache + (size_t)pb * WC::size;
   const T* Eq = WALK ? nullptr : (const T*)ka.ecache + (size_t)conf * EC::size;
-  T lv[N + D0];      // WALK: d(Yt row e, ae features of e) / d x_{e,c} of lane 4c + e
+  T lv[N + D0];      // WALK: d(Yt row e, ae features of e) / d x_{e,c} of lane NI c + e
   T jd1w = T(0);     // WALK: d J_ae / d x_{e,c}
   T jsum = T(0);
   if constexpr (WALK) {
@@ -559,9 +561,9 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
       xs[sl] = ((const T*)ka.pos)[(size_t)conf * 3 * N + sl];
     }
     wave_sync();
-    // ---------------------------------------------------------------- F1 electron stage, lane 4c + e
+    // ---------------------------------------------------------------- F1 electron stage, lane NI c + e
     {
-      const int c = sl >> 2, e = sl & 3;
+      const int c = sl / NI, e = sl % NI;
       const int ee = e < N ? e : N - 1;
       const bool elive = e < N, ev = c == 3;
       ElecOut<T, A> eo;
@@ -599,9 +601,13 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
       }
     }
     // ---------------------------------------------------------------- F2 pair stream, lane k N + i
-    {
-      const bool pl = sl < N * N;
-      const int k = pl ? sl / N : 0, i = pl ? sl - (sl / N) * N : 0;
+    // (N^2 > SW: passes of SW pairs)
+    T jl = T(0);
+#pragma unroll
+    for (int it0 = 0; it0 < N * N; it0 += SW) {
+      const int it = it0 + sl;
+      const bool pl = it < N * N;
+      const int k = pl ? it / N : 0, i = pl ? it - (it / N) * N : 0;
       const bool diag = k == i;
       T d[3];
 #pragma unroll
@@ -609,13 +615,14 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
       const T r2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
       const T r = f_sqrt(diag ? T(1) : r2);
       T pp[4] = {diag ? T(0) : r, diag ? T(0) : d[0], diag ? T(0) : d[1], diag ? T(0) : d[2]};
-      T jl = T(0);
       if (pl && k < i) {   // Pade e-e Jastrow, each pair once (Jastrow.py:51-52)
         const T cusp = P[Ly::jee_c + k * N + i], al = P[Ly::jee_a + k * N + i];
-        jl = f_div(cusp * r, al * r + T(1));
+        jl += f_div(cusp * r, al * r + T(1));
       }
+      if (pl) {
 #pragma unroll
-      for (int f = 0; f < 4; ++f) S[sl * 12 + f] = pp[f];
+        for (int f = 0; f < 4; ++f) S[it * 12 + f] = pp[f];
+      }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const cptr<T> dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
@@ -635,16 +642,18 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
 #pragma unroll
         for (int o = 0; o < 4; ++o) {
           pp[o] = (pp[o] + q[o]) * RSQ2;
-          S[sl * 12 + (j + 1) * 4 + o] = pp[o];
+          if (pl) S[it * 12 + (j + 1) * 4 + o] = pp[o];
         }
       }
+    }
+    {
       jsum += jl;
-      const T jee = row16_sum(jl);
+      const T jee = slot_sum<SW>(jl);
       if (sl == 0 && act) Wc[WC::jee] = jee;
     }
     wave_sync();
     // spin-group column means g2[l][G][i][f] = sum_{k in G} h2^l[k, i][f] / |G| (nn.py:151)
-    for (int t = sl; t < 24 * N; t += 16) {
+    for (int t = sl; t < 24 * N; t += SW) {
       const int f = t & 3, ci = (t >> 2) % N, lg = (t >> 2) / N;
       const int l = lg >> 1, G = lg & 1;
       const int k0 = G ? nup : 0, k1 = G ? N : nup;
@@ -954,6 +963,10 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
         ur = nr;
         ui = ni;
       }
+      if (WALK && sl == 0 && act) {   // pivot record (gj.h: row of step k, 1 / |pivot_k|)
+        Wc[WC::pv + k] = T(p);
+        Wc[WC::pv + N + k] = f_sqrt(rden);
+      }
       const T ir = pr * rden, ii = -pim * rden;   // 1 / pivot
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -976,6 +989,10 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
         Mx[(stepk * N + pc[h]) * 2 + 0] = a[h];
         Mx[(stepk * N + pc[h]) * 2 + 1] = b[h];
       }
+    }
+    if (WALK && sl == 0 && act) {
+      Wc[WC::pv + 2 * N] = T(inv & 1);
+      Wc[WC::pv + 2 * N + 1] = T(0.5) * lsum;
     }
   }
   wave_sync();
@@ -1147,7 +1164,7 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
   const int gcc = gc < 3 ? gc : 0, gee = ge < N ? ge : N - 1;
   T g = T(0);
   if constexpr (WALK) {
-    // lane 4c + e: the same lane as in F1, whose local Jacobians are in registers
+    // lane NI c + e: the same lane as in F1, whose local Jacobians are in registers
     g = jd1w;
 #pragma unroll
     for (int k = 0; k < N; ++k)

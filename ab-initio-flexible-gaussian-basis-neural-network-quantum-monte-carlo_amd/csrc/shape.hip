@@ -291,9 +291,9 @@ static bool quad_small(const KArgs& ka, int nconf, hipStream_t s) {
       return true;
     }
   }
-  if constexpr (N <= 4) {
-    if (!ka.proposal && ka.wcache && !ka.value_only && !ka.orb && !ka.lapcache) {   // walker launches
-      k_quad_grad<T, N, A, true><<<dim3((nconf + 3) / 4), dim3(64), 0, s>>>(ka);
+  if constexpr (N <= 8) {   // walker launches: 4 (N <= 4) or 2 (N <= 8) per wave
+    if (!ka.proposal && ka.wcache && !ka.value_only && !ka.orb && !ka.lapcache && !ka.one_wave) {
+      k_quad_grad<T, N, A, true><<<dim3((nconf + QSlot<N>::NSL - 1) / QSlot<N>::NSL), dim3(64), 0, s>>>(ka);
       return true;
     }
   }

@@ -263,6 +263,9 @@ struct KArgs {
   // this walker's pivot record of the previous sweep; the Gauss-Jordan re-uses that order (the
   // pivoted elimination only if a pivot comes out small)
   int pvok;
+  // walker launches of N <= 8 on k_walker_rev (one wave per walker) instead of the packed
+  // k_quad_grad (aiqmc_debug_set_packed_walkers; A/B and parity)
+  int one_wave;
   // Metropolis caches (walker_rev.h WCache / ECache); nullptr outside aiqmc_mc_step
   void* wcache;
   void* ecache;

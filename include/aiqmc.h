@@ -276,6 +276,11 @@ int aiqmc_debug_set_fuse_accept(aiqmc_ctx* ctx, int32_t on);
  * reuse = 0 runs partial pivoting in every sweep.  Results agree to rounding. */
 int aiqmc_debug_set_walker_pivots(aiqmc_ctx* ctx, int32_t reuse);
 
+/* Diagnostics: walker launches of systems with N <= 8 electrons run several walkers per wave
+ * (default, on = 1: four for N <= 4, two for N <= 8); on = 0 runs one wave per walker.
+ * Results agree to rounding. */
+int aiqmc_debug_set_packed_walkers(aiqmc_ctx* ctx, int32_t on);
+
 /* Diagnostics: in fp32, aiqmc_mc_step can sum the two limdrift reductions of each sweep
  * (|grad|^2 over the walkers, over the proposals; VMCmcstep.py:11-14) inside the walker and
  * proposal launches, as exact 64-bit integer sums of |grad|^2 in units of 2^-16: no reduction

@@ -307,6 +307,37 @@ def test_small_n_packed_proposals_match_one_wave_path(name, dtype):
         assert float(differ) < 5e-3, float(differ)
 
 
+@pytest.mark.parametrize("name", ["Be", "H2", "C", "C2_ecp"])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_small_n_packed_walkers_match_one_wave_path(name, dtype):
+    """N <= 8: the walker launches of a sweep (value, gradient, the walker cache the proposals read,
+    the fused acceptance) run several walkers per wave (quad_small.h k_quad_grad<WALK>: four for
+    N <= 4, two in 32-lane slots for 5 <= N <= 8, round 4) against one wave per walker
+    (k_walker_rev, aiqmc_debug_set_packed_walkers(0)).  Same host draws -> same trajectory (fp64:
+    to 1e-10, identical accept counts; fp32: all but rounding-level acceptance flips)."""
+    s, ctx = _ctx(name, dtype)
+    B, NS, N = 1001, 4, s.nelectrons    # odd B: the last wave of the walker launch is partial
+    x0 = torch.tensor(_walkers(s, B, seed=8), dtype=dtype, device="cuda")
+    g = torch.Generator().manual_seed(2)
+    kw = dict(gauss1=torch.randn(NS, B, 3 * N, generator=g, dtype=torch.float64),
+              gauss2=torch.randn(NS, B, N, 3, generator=g, dtype=torch.float64),
+              u=torch.rand(NS, B, N, generator=g, dtype=torch.float64))
+    a = x0.clone().contiguous()
+    b = x0.clone().contiguous()
+    acc_a = ctx.mc_step(a, NS, 0.05, count_accepts=True, **kw)
+    ctx.set_packed_walkers(False)
+    acc_b = ctx.mc_step(b, NS, 0.05, count_accepts=True, **kw)
+    ctx.set_packed_walkers(True)
+    torch.cuda.synchronize()
+    assert int(acc_a.sum()) > 0 and not torch.equal(a, x0)
+    if dtype == torch.float64:
+        assert torch.allclose(a, b, rtol=0, atol=1e-10), float((a - b).abs().max())
+        assert torch.equal(acc_a, acc_b)
+    else:
+        differ = ((a - b).abs().reshape(B, -1).amax(1) > 1e-4).float().mean()
+        assert float(differ) < 5e-3, float(differ)
+
+
 @pytest.mark.parametrize("name", ["N2", "Be"])
 def test_fused_limdrift_reduction_matches_reduction_launches(name):
     """fp32 mc_step sums the two limdrift reductions of a sweep (VMCmcstep.py:11-14) inside the

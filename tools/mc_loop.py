@@ -21,6 +21,8 @@ if os.environ.get("AIQMC_LAPW"):      # waves per walker of the local energy's s
     ctx.set_lap_waves(int(os.environ["AIQMC_LAPW"]))
 if os.environ.get("AIQMC_WPIV") == "0":   # walker launches: partial pivoting every sweep
     ctx.set_walker_pivots(False)
+if os.environ.get("AIQMC_PACKW") == "0":   # N <= 8 walker launches one wave each
+    ctx.set_packed_walkers(False)
 if os.environ.get("AIQMC_NOREUSE"):   # every proposal from scratch (PMC comparison of the two paths)
     ctx.set_proposal_reuse(False)
 pos = init_electrons(1000, None, s.atoms, s.charges, s.spins, B, 1.0)[0].to("cuda", torch.float32).contiguous()

@@ -1,0 +1,70 @@
+"""Does overlapping iteration k's local energy (on a snapshot of the positions, side stream) with
+iteration k+1's mc_step pay?  N2 fp32, `iters` VMC iterations (mc_step of 10 sweeps + local energy
++ energy stats) sequential vs pipelined, interleaved reps; checks that both give the same E_L.
+usage: python tools/pipe_probe.py [iters] [walkers]"""
+import os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ab-initio-flexible-gaussian-basis-neural-network-quantum-monte-carlo_amd"))
+import torch
+from aiqmc import systems, constants
+from aiqmc.initial_electrons_positions.init import init_electrons
+from aiqmc.wavefunction_Ynlm.nn import flatten_params
+iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+s = systems.make_system("N2")
+ctx = s.context(dtype=torch.float32)
+ctx.set_params(flatten_params(s.make_network().init(1)))
+pos0 = init_electrons(1000, None, s.atoms, s.charges, s.spins, B, 1.0)[0].to("cuda", torch.float32).contiguous()
+main = torch.cuda.current_stream()
+side = torch.cuda.Stream()
+
+
+def sequential(n, pos, off):
+    els = []
+    for k in range(n):
+        ctx.mc_step(pos, 10, 0.05, seed=1, offset=off + 10 * k)
+        el, _, _ = ctx.local_energy(pos)
+        constants.pmean_stats(el)
+        els.append(el)
+    return els
+
+
+def pipelined(n, pos, off):
+    snaps = [torch.empty_like(pos) for _ in range(2)]
+    done = [None, None]
+    els = []
+    for k in range(n):
+        ctx.mc_step(pos, 10, 0.05, seed=1, offset=off + 10 * k)
+        sn = snaps[k & 1]
+        if done[k & 1] is not None:
+            main.wait_event(done[k & 1])       # the E_L that read this snapshot two iterations ago
+        sn.copy_(pos)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        side.wait_event(ready)
+        with torch.cuda.stream(side):
+            el, _, _ = ctx.local_energy(sn)
+            constants.pmean_stats(el)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        done[k & 1] = ev
+        els.append(el)
+    main.wait_stream(side)
+    return els
+
+
+pa = pos0.clone(); pb = pos0.clone()
+ea = sequential(3, pa, 0); eb = pipelined(3, pb, 0)
+torch.cuda.synchronize()
+same = all(torch.equal(x, y) for x, y in zip(ea, eb)) and torch.equal(pa, pb)
+print(f"B={B} warm-up E_L and positions equal: {same}", flush=True)
+for rep in range(3):
+    for name, fn in (("sequential", sequential), ("pipelined", pipelined)):
+        pos = pos0.clone()
+        fn(2, pos, 1000)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn(iters, pos, 2000)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / iters
+        print(f"rep{rep} {name:10s} B={B}: {1e3 * dt:.3f} ms/iter", flush=True)
