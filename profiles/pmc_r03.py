@@ -15,9 +15,9 @@ import os
 import sys
 
 KERNELS = {
-    "proposal": "k_walker_rev<float, 14, 2, false, true>",
-    "walker": "k_walker_rev<float, 14, 2, false, false>",
-    "prep": "k_walker_rev<float, 14, 2, true, false>",
+    "proposal": "k_walker_rev<float, 14, 2, false, true",   # (a trailing PW7 template flag since round 4)
+    "walker": "k_walker_rev<float, 14, 2, false, false",
+    "prep": "k_walker_rev<float, 14, 2, true, false",
     "lap": "k_walker_lap<float, 14, 2",
     "moved_electron": "k_moved_electron<float, 14, 2>",
 }
