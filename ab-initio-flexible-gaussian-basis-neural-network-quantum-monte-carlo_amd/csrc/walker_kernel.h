@@ -123,10 +123,30 @@ __device__ __forceinline__ double tacc_v2(unsigned long long lo, unsigned long l
   if (bad) return __builtin_nan("");
   return (double)lo * (1.0 / TACC_SCALE) + (double)mid * 0x1p24 + (double)hi * 0x1p64;
 }
+// Exact (mod 2^64) sum over the wave, every lane active: the two 32-bit halves rotate inside each
+// 16-lane row by DPP (row_ror 8, 4, 2, 1; the carry by the 64-bit add), then the four row totals
+// are read into scalar registers and added there.  Round 4: replaces six dependent 64-bit
+// ds_bpermute exchanges (12 LDS-crossbar round trips) on the critical path of every walker,
+// moved-electron and acceptance wave that reads a limdrift sum; removing that read altogether
+// took 1.5 / 1.0 us off the 512-walker walker / moved-electron launches (a timing probe).
+template <int CTL> __device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)v, CTL, 0xF, 0xF, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(v >> 32), CTL, 0xF, 0xF, false);
+  return ((unsigned long long)hi << 32) | lo;
+}
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+  v += dpp_u64<0x128>(v);
+  v += dpp_u64<0x124>(v);
+  v += dpp_u64<0x122>(v);
+  v += dpp_u64<0x121>(v);
+  unsigned long long t = 0;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
+  for (int r = 0; r < 4; ++r) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, 16 * r);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), 16 * r);
+    t += ((unsigned long long)hi << 32) | lo;
+  }
+  return t;
 }
 __device__ __forceinline__ unsigned long long wave_sum_sat_u64(unsigned long long v) {
 #pragma unroll

@@ -1624,85 +1624,134 @@ k_walker_rev(KArgs ka) {
   if constexpr (PREP) {
     // ---------------------------------------------------------------- local-energy adjoint pass: tail
     for (int idx = lane; idx < N * D0; idx += 64) Lw[LCc::h0b + idx] = hbar[idx];
-    // Pair stream in the direction-lane layout: lane (c, i) runs over k and propagates h2[k,i]
-    // with its first and second derivatives along d_c, d = x_i - x_k, through the double layers.
+    // Pair stream, lane 4 i + kq: column i, the pairs (k, i) with k = kq mod 4 of one spin group at
+    // a time; each pair's forward values through the double layers once, with the first and second
+    // derivatives along the three components d_c of d = x_i - x_k carried together.
     //  * sd[l][G][i][c][f] = sum_{k in G, k != i} d h2^{(l)}[k,i][f] / d d_c  (k_walker_lap: the
-    //    derivative of the column mean g2 along x_{i,c});
+    //    derivative of the column mean g2 along x_{i,c}), summed over the four lanes of column i;
     //  * pair-local Laplacian: sum over the pair terms of g2 of their adjoint (g2b, already
     //    scaled by 1/|G|) times their Laplacian in (x_k, x_i) = 2 sum_c d^2/d d_c^2.
-    const int qc = lane >> 4, qi = lane & 15;
-    const bool plive = qc < 3 && qi < N;
-    const int ii = qi < N ? qi : N - 1;
-    const int c3 = qc < 3 ? qc : 0;
+    // Round 4: the (direction, column) lane layout ran the 14 pairs of a column serially on each
+    // direction lane and recomputed the forward values per direction (≈ 3,000 of the launch's
+    // 7,765 VALU instructions per wave).
+    const int ci = lane >> 2, kq = lane & 3;
+    const bool ilv = ci < N;
+    const int ii = ilv ? ci : N - 1;
     T pcurv = T(0);
-    T sdv[3][2][4];
-#pragma unroll
-    for (int l = 0; l < 3; ++l)
-#pragma unroll
-      for (int G = 0; G < 2; ++G)
-#pragma unroll
-        for (int f = 0; f < 4; ++f) sdv[l][G][f] = T(0);
-#pragma unroll
-    for (int G = 0; G < 2; ++G) {
-      const int k0 = G ? nup : 0, k1 = G ? N : nup;
-      const T* gb = g2b + (G * N + ii) * 4;        // level l at + l * 2 * N * 4
+    // directions C0 .. C0 + NC - 1 together (two passes, {0, 1} and {2}: the three together spill
+    // at the 4-waves/SIMD register budget)
+    auto pair_pass = [&](auto c0_, auto nc_) {
+      constexpr int C0 = decltype(c0_)::value, NC = decltype(nc_)::value;
 #pragma unroll 1
-      for (int k = k0; k < k1; ++k) {
-        const bool dg = (k == ii);
-        const T m = (plive && !dg) ? T(1) : T(0);
-        T d[3];
+      for (int G = 0; G < 2; ++G) {
+        const int k0 = G ? nup : 0, k1 = G ? N : nup;
+        const T* gb = g2b + (G * N + ii) * 4;        // level l at + l * 2 * N * 4
+        T s0[NC];           // level 0: sum of u_c = d_c / r (the other three features count the pairs)
+        T s1[2][NC][4];     // levels 1, 2
 #pragma unroll
-        for (int c = 0; c < 3; ++c) d[c] = xs[ii * 3 + c] - xs[k * 3 + c];
-        const T r = f_sqrt(dg ? T(1) : d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
-        const T ir = f_rcp(r);
-        const T u = (c3 == 0 ? d[0] : (c3 == 1 ? d[1] : d[2])) * ir;
-        T pv[4] = {r, d[0], d[1], d[2]};
-        T p1[4] = {u, c3 == 0 ? T(1) : T(0), c3 == 1 ? T(1) : T(0), c3 == 2 ? T(1) : T(0)};
-        T p2[4] = {(T(1) - u * u) * ir, T(0), T(0), T(0)};
+        for (int c = 0; c < NC; ++c) {
+          s0[c] = T(0);
 #pragma unroll
-        for (int f = 0; f < 4; ++f) sdv[0][G][f] += m * p1[f];
-        pcurv += m * gb[0] * p2[0];                 // level 0: only r has curvature
+          for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const cptr<T> dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
-          const cptr<T> db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
-          T tv[4], z1[4], z2[4];
+            for (int f = 0; f < 4; ++f) s1[j][c][f] = T(0);
+        }
+#pragma unroll 1
+        for (int k = k0 + ((kq - k0) & 3); k < k1; k += 4) {
+          const bool dg = (k == ii);
+          const T m = (ilv && !dg) ? T(1) : T(0);
+          T d[3];
 #pragma unroll
-          for (int o = 0; o < 4; ++o) {
-            T zv = db[o], a1 = T(0), a2 = (j == 0) ? p2[0] * dw[o] : T(0);
+          for (int c = 0; c < 3; ++c) d[c] = xs[ii * 3 + c] - xs[k * 3 + c];
+          const T r = f_sqrt(dg ? T(1) : d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+          const T ir = f_rcp(r);
+          T pv[4] = {r, d[0], d[1], d[2]};
+          T p1[NC][4], p2[NC][4];
 #pragma unroll
-            for (int mm = 0; mm < 4; ++mm) {
-              zv += pv[mm] * dw[mm * 4 + o];
-              a1 += p1[mm] * dw[mm * 4 + o];
-              if (j > 0) a2 += p2[mm] * dw[mm * 4 + o];
-            }
-            tv[o] = f_tanh(zv);
-            z1[o] = a1;
-            z2[o] = a2;
+          for (int c = 0; c < NC; ++c) {
+            const T u = d[C0 + c] * ir;
+            p1[c][0] = u;
+#pragma unroll
+            for (int f = 1; f < 4; ++f) p1[c][f] = (f - 1 == C0 + c) ? T(1) : T(0);
+            p2[c][0] = (T(1) - u * u) * ir;
+#pragma unroll
+            for (int f = 1; f < 4; ++f) p2[c][f] = T(0);
+            s0[c] += m * u;
+            pcurv += m * gb[0] * p2[c][0];             // level 0: only r has curvature
           }
-          const T* gl = gb + (j + 1) * 2 * N * 4;
 #pragma unroll
-          for (int o = 0; o < 4; ++o) {
-            const T s = T(1) - tv[o] * tv[o];
-            const T t1 = s * z1[o];
-            const T t2 = s * (z2[o] - T(2) * tv[o] * z1[o] * z1[o]);
-            pv[o] = (pv[o] + tv[o]) * RSQ2;
-            p1[o] = (p1[o] + t1) * RSQ2;
-            p2[o] = (p2[o] + t2) * RSQ2;
-            sdv[j + 1][G][o] += m * p1[o];
-            pcurv += m * gl[o] * p2[o];
+          for (int j = 0; j < 2; ++j) {
+            const cptr<T> dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
+            const cptr<T> db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
+            const T* gl = gb + (j + 1) * 2 * N * 4;
+            T tv[4];
+#pragma unroll
+            for (int o = 0; o < 4; ++o) {
+              T zv = db[o];
+#pragma unroll
+              for (int mm = 0; mm < 4; ++mm) zv += pv[mm] * dw[mm * 4 + o];
+              tv[o] = f_tanh(zv);
+            }
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+              T z1[4], z2[4];
+#pragma unroll
+              for (int o = 0; o < 4; ++o) {
+                T a1 = T(0), a2 = (j == 0) ? p2[c][0] * dw[o] : T(0);
+#pragma unroll
+                for (int mm = 0; mm < 4; ++mm) {
+                  a1 += p1[c][mm] * dw[mm * 4 + o];
+                  if (j > 0) a2 += p2[c][mm] * dw[mm * 4 + o];
+                }
+                z1[o] = a1;
+                z2[o] = a2;
+              }
+#pragma unroll
+              for (int o = 0; o < 4; ++o) {
+                const T sd1 = T(1) - tv[o] * tv[o];
+                const T t1 = sd1 * z1[o];
+                const T t2 = sd1 * (z2[o] - T(2) * tv[o] * z1[o] * z1[o]);
+                p1[c][o] = (p1[c][o] + t1) * RSQ2;
+                p2[c][o] = (p2[c][o] + t2) * RSQ2;
+                s1[j][c][o] += m * p1[c][o];
+                pcurv += m * gl[o] * p2[c][o];
+              }
+            }
+#pragma unroll
+            for (int o = 0; o < 4; ++o) pv[o] = (pv[o] + tv[o]) * RSQ2;
+          }
+        }
+        // column i's totals over its four lanes; lane kq stores direction C0 + kq (kq < NC)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          s0[c] += dpp<0xB1>(s0[c]);
+          s0[c] += dpp<0x4E>(s0[c]);
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+              s1[j][c][f] += dpp<0xB1>(s1[j][c][f]);
+              s1[j][c][f] += dpp<0x4E>(s1[j][c][f]);
+            }
+        }
+        if (ilv && kq < NC) {
+          const int c = C0 + kq;
+          const T cnt = T(k1 - k0 - ((ii >= k0 && ii < k1) ? 1 : 0));   // pairs (k, i), k in G, k != i
+          T* o0 = Lw + LCc::sd + ((G * N + ii) * 3 + c) * 4;
+          o0[0] = (NC == 1 || kq == 0) ? s0[0] : s0[NC - 1];
+#pragma unroll
+          for (int f = 1; f < 4; ++f) o0[f] = (f - 1 == c) ? cnt : T(0);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            T* oj = Lw + (j + 1) * LCc::layer_n + LCc::sd + ((G * N + ii) * 3 + c) * 4;
+#pragma unroll
+            for (int f = 0; f < 4; ++f) oj[f] = (NC == 1 || kq == 0) ? s1[j][0][f] : s1[j][NC - 1][f];
           }
         }
       }
-    }
-    if (plive) {
-#pragma unroll
-      for (int l = 0; l < 3; ++l)
-#pragma unroll
-        for (int G = 0; G < 2; ++G)
-#pragma unroll
-          for (int f = 0; f < 4; ++f) Lw[l * LCc::layer_n + LCc::sd + ((G * N + ii) * 3 + c3) * 4 + f] = sdv[l][G][f];
-    }
+    };
+    pair_pass(std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{});
+    pair_pass(std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
     // x2: the second derivatives along x_{k,c} equal those along x_{i,c}
     pcurv = T(2) * wave_sum(pcurv);
     const T lpsi = logdet + wave_sum(jv + jve);
