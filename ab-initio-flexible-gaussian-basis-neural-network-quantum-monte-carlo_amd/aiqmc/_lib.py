@@ -362,7 +362,7 @@ class Context:
 
     def set_fuse_reduce(self, mode):
         """Diagnostics: fp32 mc_step limdrift sums fused into the walker / proposal launches as
-        exact integer accumulations: 1 (default) for batches <= 1,024 walkers, 2 always,
+        exact integer accumulations: 1 (default) and 2 always,
         0 never (reduction launches summing the same integers: the same bits), 3 never with the
         fp64 tree-sum launch (k_taueff).  True/False map to 2/0."""
         m = 2 if mode is True else (0 if mode is False else int(mode))

@@ -22,8 +22,10 @@
 using namespace aq;
 
 // fp32 mc_step sums its limdrift reductions in the walker / proposal launches up to this many
-// walkers per call (aiqmc_debug_set_fuse_reduce: 1 = by batch size, 2 = always, 0 = never)
-constexpr int FUSE_REDUCE_MAX_B = 1024;
+// walkers per call (aiqmc_debug_set_fuse_reduce: 1 = by batch size, 2 = always, 0 = never).
+// Round 4, with 256 accumulator slots: fused is as fast or faster at every measured size (N2 per
+// iteration, launches vs fused: 4096 walkers 3.026-3.030 vs 2.993-3.000 ms), so no limit.
+constexpr int FUSE_REDUCE_MAX_B = 1 << 30;
 
 // ============================================================================ small kernels
 
@@ -980,12 +982,12 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
     if (rc) return rc;
   }
   hipStream_t s = (hipStream_t)stream;
-  // fp32, small batches (the per-rank share of a strong-scaling run): the limdrift sums of every
-  // sweep accumulate in integer accumulators (walker_kernel.h; one set per sweep, zeroed once
-  // here) instead of two k_taueff launches per sweep.  N2, ms per VMC iteration, launches vs
-  // fused: 512 walkers 1.040 vs 1.000, 1024 walkers 1.399 vs 1.377, 4096 walkers 3.53 vs 3.56 --
-  // at 4096 the walker launch's wave-wide read of the accumulators before its fused acceptance
-  // and the proposals' atomics cost more than the two launches they replace.
+  // fp32: the limdrift sums of every sweep accumulate in integer accumulators (walker_kernel.h;
+  // one set per sweep, zeroed once here) instead of two reduction launches per sweep.  N2, ms per
+  // VMC iteration, launches vs fused: round 3 (1024 slots) 512 walkers 1.040 vs 1.000, 1024
+  // walkers 1.399 vs 1.377, 4096 walkers 3.53 vs 3.56 (the consumers' wave-wide read of the 1024
+  // slots cost more than the launches); round 4 with 256 slots, 4096 walkers 3.026-3.030 vs
+  // 2.993-3.000.
   unsigned long long* tacc = nullptr;
   // (integer sums need fewer than TACC_MAX_CONF configurations per reduction, walker_kernel.h)
   const bool int_sums = (int64_t)B * c->N < TACC_MAX_CONF;

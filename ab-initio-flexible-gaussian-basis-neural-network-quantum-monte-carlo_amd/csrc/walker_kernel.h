@@ -40,8 +40,10 @@ constexpr int MODE_GRAD_FWD = 3;   // forward-mode gradient (diagnostics / cross
 // Fused limdrift reductions (VMCmcstep.py:11-14, quirk Q8), fp32 Metropolis sweeps: instead of a
 // reduction launch after the walker launch and after the proposal launch, every configuration's
 // wave adds its |grad|^2 to one of TACC_SLOTS 64-bit integer accumulators of the sweep (slot =
-// configuration mod 1024: one address for every wave of a launch serialises the atomics in L2,
-// measured 715 instead of 249 us per proposal launch, 64 slots still +9 us) in units of 2^-16
+// configuration mod TACC_SLOTS: one address for every wave of a launch serialises the atomics in
+// L2, measured 715 instead of 249 us per proposal launch, 64 slots still +9 us; every consumer wave
+// reads all the slots, so fewer slots are cheaper to read: round 4, fused at 4096 N2 walkers, N2
+// iteration 3.026-3.043 ms with 1024 slots, 2.993-3.000 with 256, 2.995-3.005 with 128) in units of 2^-16
 // (TACC_SCALE).  Integer
 // addition is exact and associative, so the sums -- and the limdrift factor every consumer
 // derives from them -- are bit-for-bit the same in any arrival order.  The quantum is far below
@@ -63,7 +65,11 @@ constexpr int MODE_GRAD_FWD = 3;   // forward-mode gradient (diagnostics / cross
 // reference's (sqrt(1 + 2 tau a v2) - 1) / (a v2) does for an inf or NaN sum.  With mid = hi =
 // bad = 0 (every ordinary sweep) v2 is exactly the round-3 integer sum.
 constexpr double TACC_SCALE = 65536.0;
-constexpr int TACC_SLOTS = 1024;
+#ifndef AQ_TACC_SLOTS
+#define AQ_TACC_SLOTS 256
+#endif
+constexpr int TACC_SLOTS = AQ_TACC_SLOTS;      // a power of two >= 64
+static_assert(TACC_SLOTS >= 64 && (TACC_SLOTS & (TACC_SLOTS - 1)) == 0, "TACC_SLOTS");
 constexpr int TACC_STRIDE = TACC_SLOTS + 64;   // per kind: lo slots, then [mid, hi, bad, 0 ...]
 constexpr int TACC_MID = TACC_SLOTS, TACC_HI = TACC_SLOTS + 1, TACC_BAD = TACC_SLOTS + 2;
 constexpr int TACC_MAX_CONF = 1 << 24;          // configurations per reduction (lo / mid headroom)

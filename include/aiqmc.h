@@ -284,8 +284,8 @@ int aiqmc_debug_set_packed_walkers(aiqmc_ctx* ctx, int32_t on);
 /* Diagnostics: in fp32, aiqmc_mc_step can sum the two limdrift reductions of each sweep
  * (|grad|^2 over the walkers, over the proposals; VMCmcstep.py:11-14) inside the walker and
  * proposal launches, as exact 64-bit integer sums of |grad|^2 in units of 2^-16: no reduction
- * launches, and the same bits in any arrival order.  mode 1 (default) = for batches of at most
- * 1,024 walkers (where it is faster), 2 = always, 0 = never: reduction launches that sum the same
+ * launches, and the same bits in any arrival order.  mode 1 (default) and 2 = always (mode 1
+ * limited it to batches of at most 1,024 walkers before round 4), 0 = never: reduction launches that sum the same
  * integers in 32 workgroups (k_taueff_part; the same bits as the fused sums), 3 = never, with the
  * single-workgroup fp64 tree sum (k_taueff; fp64 always uses it; results agree with the integer
  * sums to the float rounding of v2). */

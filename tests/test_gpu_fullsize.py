@@ -356,7 +356,7 @@ def test_fused_limdrift_reduction_matches_reduction_launches(name):
               gauss2=torch.randn(NS, B, N, 3, generator=g, dtype=torch.float64),
               u=torch.rand(NS, B, N, generator=g, dtype=torch.float64))
     a, a2, w, b = (x0.clone().contiguous() for _ in range(4))
-    ctx.set_fuse_reduce(2)          # fused at any batch size (default: B <= 1,024 only)
+    ctx.set_fuse_reduce(2)          # fused (the default at every batch size since round 4)
     acc_a = ctx.mc_step(a, NS, 0.05, count_accepts=True, **kw)
     ctx.mc_step(a2, NS, 0.05, **kw)
     ctx.set_fuse_reduce(0)          # integer reduction launches
