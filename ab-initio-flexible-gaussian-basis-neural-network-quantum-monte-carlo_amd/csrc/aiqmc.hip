@@ -70,7 +70,7 @@ __global__ __launch_bounds__(1024) void k_taueff(const T* __restrict__ x, int n,
   }
 }
 
-// fp32 limdrift reduction of an unfused sweep (batches above FUSE_REDUCE_MAX_B): TPART
+// fp32 limdrift reduction of an unfused sweep (aiqmc_debug_set_fuse_reduce(0)): TPART
 // workgroups, every element entering as tacc_fix(x) -- the fused accumulators' arithmetic --
 // each workgroup writing its exact integer partial sum to part[blockIdx.x]; the consumers
 // (taueff_wave) add the TPART partials with one load per lane and form the factor themselves.

@@ -127,7 +127,7 @@ def test_fp32_sweep_matches_oracle(golden_dir, B, sweep):
     ratio = g[f"ratio32_{sweep}_{B}"].astype(np.float64)
     cond = g[f"cond32_{sweep}_{B}"]
     u = g[f"u_{B}"][sweep].astype(np.float64)
-    for fuse in (1, 0, 3):   # fused integer sums (<= 1,024 walkers), k_taueff_part, fp64 tree sum
+    for fuse in (1, 0, 3):   # fused integer sums (the default), k_taueff_part, fp64 tree sum
         x1, acc = _sweep(ctx, g, B, x0, [sweep], fuse_reduce=fuse)
         moved = _moved(x0, x1, B)
         assert np.array_equal(acc, moved.sum(1))
