@@ -194,3 +194,45 @@ def test_fp32_walker_limdrift_factor_matches_float_sum(golden_dir, B):
         print(B, m, te, "oracle fp32", te_ref, "fp64", te64)
         assert abs(te - te_ref) <= 2e-5 * te_ref
         assert abs(te - te64) <= 2e-5 * te64
+
+
+def test_fp32_sweep_matches_oracle_at_benched_size(golden_dir):
+    """The benched configuration itself (N2, 4096 walkers, fp32, default fused limdrift sums): one
+    sweep with injected draws against oracle/mcstep.py run in float32/complex64
+    (tests/golden/N2_mc_fp32_4096.npz; the inputs are regenerated from the fixture script's seed):
+    decisions equal except within fp32 rounding of a tie, positions of agreeing walkers to fp32
+    rounding, and the walker limdrift factor of the HIP gradients equal to the oracle's."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location("mk4096", os.path.join(golden_dir, "make_golden_mc_fp32_4096.py"))
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    s, params, pos0, g1, g2d, u = mk.inputs_4096()
+    g = np.load(os.path.join(golden_dir, "N2_mc_fp32_4096.npz"))
+    B, N = mk.B, s.nelectrons
+    _, ctx = _ctx(flat=g["params_flat"])
+    pos = torch.tensor(pos0.astype(np.float32), device="cuda").contiguous()
+    _, grad = ctx.logpsi_grad(pos)
+    te_w = ctx.limdrift_factor((grad.double() ** 2).sum(1).float(), TAU, 0)
+    acc = ctx.mc_step(pos, 1, TAU, gauss1=torch.tensor(g1[None], dtype=torch.float32),
+                      gauss2=torch.tensor(g2d[None], dtype=torch.float32),
+                      u=torch.tensor(u[None], dtype=torch.float32), count_accepts=True)
+    torch.cuda.synchronize()
+    x1 = pos.cpu().numpy().astype(np.float64)
+    moved = _moved(pos0, x1, B, N)
+    cond = g["cond32"]
+    assert np.array_equal(acc.cpu().numpy(), moved.sum(1))
+    ratio = g["ratio32"].astype(np.float64)
+    flips = moved != cond
+    gap = np.abs(ratio - u) / np.maximum(ratio, u)
+    ok = ~np.any(flips, axis=1)
+    d = np.abs(x1 - g["x32"].astype(np.float64))[ok]
+    print("4096: accepted", int(moved.sum()), "oracle", int(cond.sum()), "flips", int(flips.sum()),
+          "|x_hip - x_oracle32| max", d.max(), "p99", np.quantile(d, 0.99), "te", te_w, float(g["te32"][0]))
+    assert np.all(gap[flips] < 1e-3), gap[flips]
+    assert flips.sum() <= 8
+    assert d.max() < 1e-5
+    assert np.quantile(d, 0.99) < 5e-7
+    # v2 sums 4096 walkers' |grad|^2, dominated by a few near-node walkers whose fp32 gradients
+    # differ between the two orderings (test_precision_fp32.py's tail): measured 3.5e-5 relative
+    assert abs(te_w - float(g["te32"][0])) <= 1e-4 * float(g["te32"][0])
