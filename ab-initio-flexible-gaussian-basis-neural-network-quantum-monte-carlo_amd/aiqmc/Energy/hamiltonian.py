@@ -1,7 +1,8 @@
 """Local energy (drop-in for AIQMCrelease3/Energy/hamiltonian.py).
 
 ``local_energy(f, charges, nspins, use_scan=False, complex_output=False)``
-returns ``_e_l(params, key, data) -> (E_L, None)`` (hamiltonian.py:236-260).
+returns ``_e_l(params, key, data) -> (E_L, None)`` (hamiltonian.py:236-260); with
+complex_output=True E_L is complex (the phase terms of :110-130).
 For an AIQMC network (``f`` produced by ``make_ai_net``) the whole local
 energy -- potential + kinetic via a forward Laplacian equal to the reference's
 jvp-of-grad loop (:100-131) -- runs in ONE HIP kernel launch over the batch
@@ -54,18 +55,21 @@ def _network_of(f):
 
 
 def local_kinetic_energy(f, use_scan: bool = False, complex_output: bool = True):
-    """hamiltonian.py:77-132: returns ke(params, data) -> -1/2 (lap log|psi| + |grad log|psi||^2)."""
+    """hamiltonian.py:77-132: returns ke(params, data) -> -1/2 (lap log|psi| + |grad log|psi||^2), or
+    with complex_output (the reference's default here, :110-130) the complex
+    -1/2 [lap log|psi| + i lap theta] - 1/2 |grad log|psi||^2 + 1/2 |grad theta|^2
+    - i grad log|psi| . grad theta  (theta = arg psi; aiqmc_local_energy_complex)."""
     del use_scan
-    if complex_output:
-        raise NotImplementedError("complex_output=True (phase Laplacian) is not built; "
-                                  "the all-electron driver uses complex_output=False (SURVEY Q9)")
     net = _network_of(f)
 
     def ke(params, data):
         pos = data.positions if isinstance(data.positions, torch.Tensor) else torch.as_tensor(data.positions)
         dtype = pos.dtype if pos.dtype in (torch.float32, torch.float64) else torch.float32
         ctx = net.bind(params, data.atoms, dtype)
-        el, _, _ = ctx.local_energy(pos)
+        if complex_output:
+            el = ctx.local_energy_complex(pos)
+        else:
+            el, _, _ = ctx.local_energy(pos)
         # E_L = V + KE  ->  KE = E_L - V  (V from the same kernel would need a second output;
         # computed here from positions with the reference potential formulas)
         p = pos.to(ctx.device, dtype).reshape(-1, net.nelectrons, 3)
@@ -92,10 +96,10 @@ def local_energy(f, charges, nspins: Sequence[int], use_scan: bool = False, comp
 
     The HIP kernel takes the potential charges from the network's configuration
     (make_ai_net ``charges``); they must agree with the charges given here.
+    complex_output=True returns the complex local energy (:110-130; the phase's Laplacian and
+    gradient from a second launch pair, aiqmc_local_energy_complex).
     """
     del nspins, use_scan
-    if complex_output:
-        raise NotImplementedError("complex_output=True is not built (SURVEY Q9)")
     net = _network_of(f)
     c = np.asarray(charges.detach().cpu() if isinstance(charges, torch.Tensor) else charges, dtype=np.float64)
     if c.shape != net.charges.shape or not np.allclose(c, net.charges):
@@ -107,7 +111,10 @@ def local_energy(f, charges, nspins: Sequence[int], use_scan: bool = False, comp
             np.asarray(data.positions))
         dtype = pos.dtype if pos.dtype in (torch.float32, torch.float64) else torch.float32
         ctx = net.bind(params, data.atoms, dtype)
-        el, _, _ = ctx.local_energy(pos)
+        if complex_output:
+            el = ctx.local_energy_complex(pos)
+        else:
+            el, _, _ = ctx.local_energy(pos)
         return el.reshape(pos.shape[:-1]), None
     _e_l._aiqmc_network = net
     return _e_l

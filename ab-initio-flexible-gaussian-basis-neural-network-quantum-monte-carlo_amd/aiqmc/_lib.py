@@ -26,7 +26,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
 
 EXPORTED_SYMBOLS = (
     "aiqmc_create", "aiqmc_destroy", "aiqmc_param_count", "aiqmc_set_params",
-    "aiqmc_logpsi", "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_mc_step",
+    "aiqmc_logpsi", "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_local_energy_complex", "aiqmc_mc_step",
     "aiqmc_workspace_bytes", "aiqmc_last_error", "aiqmc_supported_shapes",
     "aiqmc_profile_enable", "aiqmc_profile_read", "aiqmc_debug_logpsi_grad_forward",
     "aiqmc_debug_set_proposal_reuse", "aiqmc_debug_phase_cycles", "aiqmc_debug_local_energy_forward",
@@ -118,6 +118,7 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_logpsi_grad.argtypes = [vp, vp, i32, vp, vp, vp]
     lib.aiqmc_orbitals.argtypes = [vp, vp, i32, vp, vp, vp, vp]
     lib.aiqmc_local_energy.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+    lib.aiqmc_local_energy_complex.argtypes = [vp, vp, i32, vp, vp, vp]
     lib.aiqmc_mc_step.argtypes = [vp, vp, i32, i32, ctypes.c_double, i32, vp, vp, vp,
                                   ctypes.c_uint64, ctypes.c_uint64, vp, vp]
     lib.aiqmc_debug_logpsi_grad_forward.argtypes = [vp, vp, i32, vp, vp, vp]
@@ -162,7 +163,7 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_last_error.restype = ctypes.c_char_p
     lib.aiqmc_supported_shapes.restype = ctypes.c_char_p
     for name in ("aiqmc_create", "aiqmc_destroy", "aiqmc_set_params", "aiqmc_logpsi",
-                 "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_mc_step", "aiqmc_profile_enable",
+                 "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_local_energy_complex", "aiqmc_mc_step", "aiqmc_profile_enable",
                  "aiqmc_profile_read", "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
                  "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves",
                  "aiqmc_phase_param_grad", "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals",
@@ -406,6 +407,18 @@ class Context:
         check(self._lib.aiqmc_local_energy(self._h, _ptr(p), B, _ptr(el), _ptr(logabs), _ptr(grad),
                                            _stream(self.device)), "aiqmc_local_energy")
         return el, logabs, grad
+
+    def local_energy_complex(self, pos: torch.Tensor) -> torch.Tensor:
+        """complex_output=True local energy (hamiltonian.py:110-130): V - 1/2 [lap log|psi| + i lap theta
+        + |grad log|psi||^2 - |grad theta|^2 + 2 i grad log|psi| . grad theta], theta = arg psi; a
+        complex tensor [B] (complex64 for a float32 context)."""
+        p = self._pos(pos)
+        B = p.shape[0]
+        re = torch.empty(B, dtype=self.dtype, device=self.device)
+        im = torch.empty(B, dtype=self.dtype, device=self.device)
+        check(self._lib.aiqmc_local_energy_complex(self._h, _ptr(p), B, _ptr(re), _ptr(im), _stream(self.device)),
+              "aiqmc_local_energy_complex")
+        return torch.complex(re, im)
 
     def local_energy_forward_mode(self, pos: torch.Tensor, want_logabs: bool = False, want_grad: bool = False):
         """Diagnostics: the same quantity through the single-launch forward-Laplacian kernel."""

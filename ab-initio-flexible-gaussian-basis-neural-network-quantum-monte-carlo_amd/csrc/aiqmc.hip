@@ -29,6 +29,24 @@ constexpr int FUSE_REDUCE_MAX_B = 1 << 30;
 
 // ============================================================================ small kernels
 
+// complex_output=True local energy from the log|psi| pass (e_re = E_L = V - (lap log|psi| +
+// |grad log|psi||^2) / 2, ga = grad log|psi|) and the phase pass (gp = grad theta, lp = lap theta):
+// hamiltonian.py:110-130,  KE = -1/2 [lap log|psi| + i lap theta] - 1/2 |ga|^2 + 1/2 |gp|^2 - i ga.gp
+template <typename T>
+__global__ __launch_bounds__(256) void k_complex_el(int B, int n3, const T* __restrict__ ga, const T* __restrict__ gp,
+                                                    const T* __restrict__ lp, T* __restrict__ e_re, T* __restrict__ e_im) {
+  const int b = blockIdx.x * 256 + (int)threadIdx.x;
+  if (b >= B) return;
+  T pp = T(0), ap = T(0);
+  for (int k = 0; k < n3; ++k) {
+    const T p = gp[(size_t)b * n3 + k];
+    pp += p * p;
+    ap += ga[(size_t)b * n3 + k] * p;
+  }
+  e_re[b] += T(0.5) * pp;
+  e_im[b] = T(-0.5) * lp[b] - ap;
+}
+
 // v2 = sum(x[0..n)) ; taueff = (sqrt(1 + 2 tau a v2) - 1)/(a v2), a = 0.25  (VMCmcstep.py:11-14)
 // One 1024-thread block; thread t sums x[t + 1024 j] in 8 independent partial sums, 32 loads in
 // flight per thread (n = B N = 57,344 takes two rounds; with 8 in flight it took 7 and the
@@ -625,6 +643,7 @@ int aiqmc_destroy(aiqmc_ctx* c) {
     if (p) (void)hipFree(p);
   if (c->d_wcp) (void)hipFree(c->d_wcp);
   if (c->d_lc) (void)hipFree(c->d_lc);
+  if (c->d_cx) (void)hipFree(c->d_cx);
   for (auto& v : c->ev_used)
     for (auto& p : v) {
       (void)hipEventDestroy(p.first);
@@ -759,12 +778,10 @@ int aiqmc_logpsi_grad(aiqmc_ctx* c, const void* pos, int32_t B, void* logabs, vo
   return AIQMC_OK;
 }
 
-int aiqmc_local_energy(aiqmc_ctx* c, const void* pos, int32_t B, void* e_l, void* logabs, void* grad,
-                       void* stream) {
-  int rc = check_call(c, pos, B);
-  if (rc) return rc;
-  if (B == 0) return AIQMC_OK;
-  if (!e_l) return fail(AIQMC_EINVAL, "null e_l");
+// the local-energy launch pair for log|psi| (phase = 0: e_l = E_L) or theta = arg psi (phase = 1:
+// e_l = the phase Laplacian, grad = grad theta)
+static int local_energy_pass(aiqmc_ctx* c, const void* pos, int32_t B, void* e_l, void* logabs, void* grad, int phase,
+                             void* stream) {
   ShapeOps ops;
   shape_ops(c->N, c->A, &ops);
   HIPCHK(hipSetDevice(c->device));
@@ -795,7 +812,50 @@ int aiqmc_local_energy(aiqmc_ctx* c, const void* pos, int32_t B, void* e_l, void
     const int64_t want = 8 * (int64_t)c->ncu;
     lw = (int64_t)B >= want ? 1 : ((int64_t)B * 2 >= want ? 2 : 4);
   }
-  timed(c, 2, (hipStream_t)stream, [&] { ops.lap(c->dtype, k1, k2, B, lw, (hipStream_t)stream); });
+  timed(c, 2, (hipStream_t)stream, [&] { ops.lap(c->dtype, k1, k2, B, lw, phase, (hipStream_t)stream); });
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_local_energy(aiqmc_ctx* c, const void* pos, int32_t B, void* e_l, void* logabs, void* grad,
+                       void* stream) {
+  int rc = check_call(c, pos, B);
+  if (rc) return rc;
+  if (B == 0) return AIQMC_OK;
+  if (!e_l) return fail(AIQMC_EINVAL, "null e_l");
+  return local_energy_pass(c, pos, B, e_l, logabs, grad, 0, stream);
+}
+
+int aiqmc_local_energy_complex(aiqmc_ctx* c, const void* pos, int32_t B, void* e_re, void* e_im, void* stream) {
+  int rc = check_call(c, pos, B);
+  if (rc) return rc;
+  if (B == 0) return AIQMC_OK;
+  if (!e_re || !e_im) return fail(AIQMC_EINVAL, "null e_re / e_im");
+  HIPCHK(hipSetDevice(c->device));
+  const int N = c->N;
+  const size_t es = c->dtype == AIQMC_F32 ? 4 : 8;
+  if (c->cx_B < B) {
+    if (c->d_cx) (void)hipFree(c->d_cx);
+    c->d_cx = nullptr;
+    c->cx_B = 0;
+    HIPCHK(hipMalloc(&c->d_cx, (size_t)B * (6 * N + 1) * es));
+    c->cx_B = B;
+  }
+  char* gabs = (char*)c->d_cx;
+  char* gph = gabs + (size_t)B * 3 * N * es;
+  char* lph = gph + (size_t)B * 3 * N * es;
+  rc = local_energy_pass(c, pos, B, e_re, nullptr, gabs, 0, stream);
+  if (rc) return rc;
+  rc = local_energy_pass(c, pos, B, lph, nullptr, gph, 1, stream);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g((B + 255) / 256), b(256);
+  if (c->dtype == AIQMC_F32)
+    k_complex_el<float><<<g, b, 0, s>>>(B, 3 * N, (const float*)gabs, (const float*)gph, (const float*)lph,
+                                         (float*)e_re, (float*)e_im);
+  else
+    k_complex_el<double><<<g, b, 0, s>>>(B, 3 * N, (const double*)gabs, (const double*)gph, (const double*)lph,
+                                          (double*)e_re, (double*)e_im);
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
 }

@@ -41,6 +41,8 @@ struct aiqmc_ctx {
   int64_t wcp_n = 0;                                        // its capacity in configurations
   void* d_lc = nullptr;                                     // local-energy LapCache [B][lcache_n]
   int lc_B = 0, lc_n = 0;
+  void* d_cx = nullptr;                                     // complex E_L scratch [B][6N+1]: grad log|psi|, grad theta, lap theta
+  int cx_B = 0;
   bool reuse = true;                                        // proposals reuse the walker's cached stage
   int ablate = 0;                                           // AQ_ABLATE development builds (walker_rev.h)
   int fuse_accept = 1;                                      // acceptance fused into the next walker launch
@@ -86,7 +88,7 @@ struct ShapeOps {
   void (*accept)(int dtype, void* pos, const aq::AccArgs& a, int B, hipStream_t s);
   void (*moved)(int dtype, const KArgs& ka, hipStream_t s);   // k_moved_electron over ka.nconf proposals
   // local energy: adjoint pass (k1) + first-derivative pass (k2), walker_lap.h
-  void (*lap)(int dtype, const KArgs& k1, const KArgs& k2, int nconf, int waves, hipStream_t s);
+  void (*lap)(int dtype, const KArgs& k1, const KArgs& k2, int nconf, int waves, int phase, hipStream_t s);
   void (*phase_read)(unsigned long long* out32);               // AQ_PHASE_PROF builds only
   int wcache_n, ecache_n;                                      // cache entries per walker / per proposal
   int lcache_n;                                                // LapCache entries per walker

@@ -367,21 +367,24 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
 }
 
 // Local energy: adjoint pass (k_walker_rev<PREP>) then first-derivative pass (k_walker_lap).
-template <int N, int A>
-static void lap_impl(int dtype, const KArgs& k1, const KArgs& k2, int nconf, int waves, hipStream_t s) {
+// phase: the same pair for theta = arg psi (the PH instantiations, complex_output=True)
+template <typename T, int N, int A, bool PH>
+static void lap_launch(const KArgs& k1, const KArgs& k2, int nconf, int waves, hipStream_t s) {
   const dim3 wg(64 * waves);   // waves per walker in the first-derivative pass: 1, 2 or 4
+  k_walker_rev<T, N, A, true, false, false, PH><<<dim3(nconf), dim3(64), SmemRev<T, N, A>::bytes, s>>>(k1);
+  if (waves == 1)
+    k_walker_lap<T, N, A, 1, PH><<<dim3(nconf), wg, SmemLap<T, N, A>::bytes, s>>>(k2);
+  else
+    k_walker_lap<T, N, A, 4, PH><<<dim3(nconf), wg, SmemLap<T, N, A>::bytes, s>>>(k2);
+}
+template <int N, int A>
+static void lap_impl(int dtype, const KArgs& k1, const KArgs& k2, int nconf, int waves, int phase, hipStream_t s) {
   if (dtype == AIQMC_F32) {
-    k_walker_rev<float, N, A, true><<<dim3(nconf), dim3(64), SmemRev<float, N, A>::bytes, s>>>(k1);
-    if (waves == 1)
-      k_walker_lap<float, N, A, 1><<<dim3(nconf), wg, SmemLap<float, N, A>::bytes, s>>>(k2);
-    else
-      k_walker_lap<float, N, A, 4><<<dim3(nconf), wg, SmemLap<float, N, A>::bytes, s>>>(k2);
+    if (phase) lap_launch<float, N, A, true>(k1, k2, nconf, waves, s);
+    else lap_launch<float, N, A, false>(k1, k2, nconf, waves, s);
   } else {
-    k_walker_rev<double, N, A, true><<<dim3(nconf), dim3(64), SmemRev<double, N, A>::bytes, s>>>(k1);
-    if (waves == 1)
-      k_walker_lap<double, N, A, 1><<<dim3(nconf), wg, SmemLap<double, N, A>::bytes, s>>>(k2);
-    else
-      k_walker_lap<double, N, A, 4><<<dim3(nconf), wg, SmemLap<double, N, A>::bytes, s>>>(k2);
+    if (phase) lap_launch<double, N, A, true>(k1, k2, nconf, waves, s);
+    else lap_launch<double, N, A, false>(k1, k2, nconf, waves, s);
   }
 }
 

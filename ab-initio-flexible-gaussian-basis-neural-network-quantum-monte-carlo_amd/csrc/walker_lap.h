@@ -302,7 +302,12 @@ __device__ __forceinline__ T ss_mfma(const T* Qs, const T* hb, const int* rowsrc
 // fixed order.  W = 1 is the single-wave kernel (same arithmetic, same order).
 // WMAX: the instantiation's largest W (1: the single-wave kernel, compiled as before for 64
 // threads; 4: W = 2 or 4 at run time).
-template <typename T, int N, int A, int WMAX>
+// PH: the phase theta = arg psi instead of log|psi| (complex_output=True, hamiltonian.py:110-130):
+// with the LapCache of the PH adjoint pass, every determinant term takes the imaginary part of the
+// complex quantity whose real part the log|psi| pass takes (d^2 log det = tr(B d^2A) - tr(B dA B dA)
+// is complex; theta = Im log det); the Jastrow factors are real and drop out.  Outputs: el[conf] =
+// sum_dir d^2 theta / dx^2 (no potential, no |grad|^2), grad = grad theta.
+template <typename T, int N, int A, int WMAX, bool PH = false>
 __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) void k_walker_lap(KArgs ka) {
   using Ly = Lay<N, A>;
   using LC = LapCache<N, A>;
@@ -341,7 +346,7 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
   // ------------------------------------------------------------------ per-electron stage (electron.h)
   ElecOut<T, A> eo;
   electron_stage<T, N, A>(P, xs + le * 3, le, lc, eo);
-  T vv = (w0 && val && live) ? eo.ven : T(0);
+  T vv = (!PH && w0 && val && live) ? eo.ven : T(0);
   T acc = T(0);   // curvature sources, per direction lane
 #pragma unroll
   for (int m = 0; m < D0; ++m) acc += h0b[m] * eo.hf[m].d2;   // ae features as leaves
@@ -358,11 +363,14 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
       yd[(N + col) * 49 + l49] = yt.d2;
     }
   }
-  T jd1 = (w0 && dir) ? eo.jae.d1 : T(0);
-  T jd2 = (w0 && dir) ? eo.jae.d2 : T(0);
+  T jd1 = (!PH && w0 && dir) ? eo.jae.d1 : T(0);
+  T jd2 = (!PH && w0 && dir) ? eo.jae.d2 : T(0);
 
   // ------------------------------------------------------------------ h stream, first derivatives
   lap_layer<T, N, A, 0>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W);
+  if constexpr (PH) {   // the e-e Jastrow terms and V_ee of layer 0's column loop: not part of theta
+    jd1 = jd2 = vv = T(0);
+  }
   __syncthreads();
   stage_copy<T>(ly, Lc + LC::layer_n, LC::layer_n);
   __syncthreads();
@@ -435,15 +443,15 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
     const T dpr = spe ? d1r : d0r, dpi = spe ? d1i : d0i;
     const T xr = T(2) * dpr * Yd1[col] + pr * Yd2[col];
     const T xi = T(2) * dpi * Yd1[col] + pm * Yd2[col];
-    t2 += xr * br - xi * bi;
+    t2 += PH ? xr * bi + xi * br : xr * br - xi * bi;
   }
   __builtin_amdgcn_sched_barrier(0);
   // E3: gradient: sum_{r,f} U Re Q_f[r,r] + Re(w . b_e) + Jastrow  (rows r = wv, wv + W, ...)
-  T g = w0 ? jd1 + wbr : jd1;
+  T g = w0 ? jd1 + (PH ? wbi : wbr) : jd1;
 #pragma unroll 2
   for (int r = wv; r < N; r += W)
 #pragma unroll
-    for (int f = 0; f < NH; ++f) g += UH(r, f) * Qs[((r * N + r) * NH + f) * 2];
+    for (int f = 0; f < NH; ++f) g += UH(r, f) * Qs[((r * N + r) * NH + f) * 2 + (PH ? 1 : 0)];
   // E4: cross = Re sum_r z_r S_re (z = B^T w);  ss = Re sum_{r,s} S_rs S_sr,  S_rs = sum_f U_rf Q_f[r,s]
   // (row r costs N - r: wave wv takes rows wv, 2W-1-wv, 2W+wv, ... so the shares balance)
   T cross = T(0), ss = T(0);
@@ -467,15 +475,20 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
       sr += ur[f] * Qs[((r * N + le) * NH + f) * 2];
       si += ur[f] * Qs[((r * N + le) * NH + f) * 2 + 1];
     }
-    cross += zr * sr - zi * si;
+    cross += PH ? zr * si + zi * sr : zr * sr - zi * si;
 #ifndef AQ_LAP_MFMA_SS
+    constexpr bool vss = true;
+#else
+    constexpr bool vss = PH;   // the MFMA form of ss is built for the real part only
+#endif
+    if constexpr (vss) {
     T dr = T(0), di = T(0);
 #pragma unroll
     for (int f = 0; f < NH; ++f) {
       dr += ur[f] * Qs[((r * N + r) * NH + f) * 2];
       di += ur[f] * Qs[((r * N + r) * NH + f) * 2 + 1];
     }
-    ss += dr * dr - di * di;
+    ss += PH ? T(2) * dr * di : dr * dr - di * di;
 #pragma unroll 1
     for (int s = r + 1; s < N; ++s) {
       T ar = T(0), ai = T(0), br = T(0), bi = T(0);
@@ -487,16 +500,20 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
         br += us * Qs[((s * N + r) * NH + f) * 2];
         bi += us * Qs[((s * N + r) * NH + f) * 2 + 1];
       }
-      ss += T(2) * (ar * br - ai * bi);
+      ss += T(2) * (PH ? ar * bi + ai * br : ar * br - ai * bi);
     }
-#endif
+    }
   }
 #ifdef AQ_LAP_MFMA_SS
-  __builtin_amdgcn_sched_barrier(0);
-  ss = ss_mfma<T, N>(Qs, hb, rowsrc, lane, wv, W);
+  if constexpr (!PH) {
+    __builtin_amdgcn_sched_barrier(0);
+    ss = ss_mfma<T, N>(Qs, hb, rowsrc, lane, wv, W);
+  }
 #endif
 #undef UH
-  T lap = (w0 ? t2 : T(0)) - (ss + T(2) * cross + (w0 ? wbr * wbr - wbi * wbi : T(0))) + jd2 + acc;
+  // (w.b_e)^2: its real part, or (PH) its imaginary part 2 Re Im
+  const T wb2 = PH ? T(2) * wbr * wbi : wbr * wbr - wbi * wbi;
+  T lap = (w0 ? t2 : T(0)) - (ss + T(2) * cross + (w0 ? wb2 : T(0))) + jd2 + acc;
   if (W > 1) {
     // partial sums of waves 1..W-1 -> wave 0, added in wave order (the ly block is free now)
     __syncthreads();
@@ -518,6 +535,13 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
 
   // ------------------------------------------------------------------ outputs
   const T gd = dir ? g : T(0);
+  if constexpr (PH) {
+    // the phase Laplacian sum_dir d^2 theta / dx^2 (incl. the adjoint pass's pair-local part) and grad theta
+    const T lsum = wave_sum(dir ? lap : T(0)) + Lc[LC::scal];
+    if (ka.grad && dir) ((T*)ka.grad)[(size_t)conf * 3 * N + 3 * le + lc] = g;
+    if (lane == 0 && ka.el) ((T*)ka.el)[conf] = lsum;
+    return;
+  }
   const T sumsq = wave_sum(gd * gd);
   if (ka.grad && dir) ((T*)ka.grad)[(size_t)conf * 3 * N + 3 * le + lc] = g;
   const T kin = T(-0.5) * (wave_sum(dir ? lap : T(0)) + Lc[LC::scal] + sumsq);   // hamiltonian.py:126-127

@@ -449,10 +449,14 @@ template <typename T, bool PROP, bool PREP = false> struct RevWpb {
 // PW7 (proposals only, -DAQ_PW7 builds: measured slower, shape.hip): the small-batch instantiation, compiled for 7 waves/SIMD with the COMPACT
 // LDS layout, so that the B N proposals of a strong-scaling rank (512 N2 walkers: 7,168 waves) run
 // in one round instead of 1.4 (shape.hip chooses it by batch size)
-template <typename T, int N, int A, bool PREP = false, bool PROP = false, bool PW7 = false>
+// PH (PREP only): the adjoint pass of the PHASE -- seeded by Im d log det / dH instead of Re, so
+// that the LapCache's node weights, feature adjoints and pair-local curvature are those of
+// theta = arg psi (the complex_output=True kinetic energy, hamiltonian.py:110-130)
+template <typename T, int N, int A, bool PREP = false, bool PROP = false, bool PW7 = false, bool PH = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * RevWpb<T, PROP, PREP>::value))) __attribute__((amdgpu_waves_per_eu(RevWaves<T, N, A, PREP, PROP, PW7>::value))) void
 k_walker_rev(KArgs ka) {
   static_assert(!PW7 || (PROP && !PREP), "PW7 is a proposal instantiation");
+  static_assert(!PH || PREP, "PH is an adjoint-pass instantiation");
   using Ly = Lay<N, A>;
   constexpr bool fwd_reg = PROP && kFwdReg;
   constexpr bool compact = PROP && PW7 && fwd_reg;
@@ -1348,8 +1352,10 @@ k_walker_rev(KArgs ka) {
       const T yv = Yv[r * N + c];
       const T wr = P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2] * yv;
       const T wi = P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 1] * yv;
-      if (c & 1) q1 += wr * BRE(c, r) - wi * BIM(c, r);
-      else q += wr * BRE(c, r) - wi * BIM(c, r);
+      // Re Q_f[r,r] (PH: Im Q_f[r,r])
+      const T qc = PH ? wr * BIM(c, r) + wi * BRE(c, r) : wr * BRE(c, r) - wi * BIM(c, r);
+      if (c & 1) q1 += qc;
+      else q += qc;
     }
     q += q1;
     hbar[SM::hoff(3) + rowsrc[r] * 4 + f] = q;
@@ -1411,7 +1417,7 @@ k_walker_rev(KArgs ka) {
           }
           if (e == rr && !AQ_ABL(8)) {
 #pragma unroll
-            for (int v = 0; v < 4; ++v) hbar[SM::hoff(3) + rowsrc[rr] * 4 + v] = qre[v];
+            for (int v = 0; v < 4; ++v) hbar[SM::hoff(3) + rowsrc[rr] * 4 + v] = PH ? qim[v] : qre[v];
           }
         }
       }

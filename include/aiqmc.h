@@ -91,6 +91,15 @@ int aiqmc_logpsi_grad(aiqmc_ctx* ctx, const void* pos, int32_t B, void* logabs, 
 int aiqmc_local_energy(aiqmc_ctx* ctx, const void* pos, int32_t B, void* e_l, void* logabs,
                        void* grad, void* stream);
 
+/* complex_output=True local energy (replaces Energy/hamiltonian.py:100-131 with complex_output
+ * True, i.e. local_kinetic_energy's phase branch :110-130, + the potential :236-260):
+ * pos[B*3N] -> e_re[B], e_im[B] with
+ *   KE = -1/2 [lap log|psi| + i lap theta] - 1/2 |grad log|psi||^2 + 1/2 |grad theta|^2
+ *        - i grad log|psi| . grad theta,   theta = arg psi,
+ * E_L = V + KE.  Two local-energy launch pairs (log|psi| and theta) and one combining launch. */
+int aiqmc_local_energy_complex(aiqmc_ctx* ctx, const void* pos, int32_t B, void* e_re, void* e_im,
+                               void* stream);
+
 /* nsteps drift-diffusion Metropolis steps on pos_inout[B*3N] (in place; the
  * donate_argnums=1 analogue).  B is the per-device batch: limdrift's v2 is
  * summed over exactly these B walkers (VMCmcstep.py:12).

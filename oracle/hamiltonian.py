@@ -75,6 +75,48 @@ def kinetic_jvp_of_grad(logabs: Callable[[torch.Tensor], torch.Tensor]):
     return ke
 
 
+def kinetic_complex_jvp_of_grad(logabs: Callable[[torch.Tensor], torch.Tensor],
+                                phase: Callable[[torch.Tensor], torch.Tensor]):
+    """hamiltonian.py:100-131 with complex_output=True (:110-130): single walker x[3N] ->
+    [Re KE, Im KE] of -1/2 sum_i (d_i grad log|psi| + i d_i grad theta)_i - 1/2 |grad log|psi||^2
+    + 1/2 |grad theta|^2 - i grad log|psi| . grad theta  (theta = the phase output of f)."""
+    g = grad(logabs)
+    gp = grad(phase)
+
+    def ke(x):
+        n = x.shape[0]
+        eye = torch.eye(n, dtype=x.dtype)
+        primal = g(x)
+        pprimal = gp(x)
+        d_re = torch.zeros((), dtype=x.dtype)
+        d_im = torch.zeros((), dtype=x.dtype)
+        for i in range(n):                                   # lax.fori_loop(0, n, ...)
+            _, t = jvp(g, (x,), (eye[i],))
+            _, tp = jvp(gp, (x,), (eye[i],))
+            d_re = d_re + t[i]
+            d_im = d_im + tp[i]
+        re = -0.5 * d_re - 0.5 * torch.sum(primal ** 2) + 0.5 * torch.sum(pprimal ** 2)
+        im = -0.5 * d_im - torch.sum(primal * pprimal)
+        return torch.stack([re, im])
+    return ke
+
+
+def batch_local_energy_complex(net, params, pos: torch.Tensor, chunk: int = 32) -> torch.Tensor:
+    """complex_output=True local energy (hamiltonian.py:236-260 with :110-130) of a batch pos[B,3N]:
+    a complex tensor [B] (potential real)."""
+    atoms = net.atoms.to(pos.dtype)
+    charges = net.charges.to(pos.dtype)
+    ke = kinetic_complex_jvp_of_grad(lambda x: net.logabs(params, x), lambda x: net.apply(params, x)[0])
+
+    def e_l(x):
+        r_ae, r_ee = construct_r(x, atoms)
+        k = ke(x)
+        return torch.stack([potential_energy(r_ae, r_ee, atoms, charges) + k[0], k[1]])
+    f = vmap(e_l)
+    out = torch.cat([f(pos[s:s + chunk]) for s in range(0, pos.shape[0], chunk)])
+    return torch.complex(out[:, 0], out[:, 1])
+
+
 def kinetic_hessian(logabs: Callable[[torch.Tensor], torch.Tensor]):
     """ferminet/tests/hamiltonian_test.py:50-58 (kinetic_from_hessian_log)."""
     def ke(x):

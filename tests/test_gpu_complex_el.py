@@ -1,0 +1,91 @@
+"""complex_output=True local energy (Energy/hamiltonian.py:100-131 with the phase branch :110-130)
+on the GPU against the CPU oracle (oracle/hamiltonian.batch_local_energy_complex, itself pinned by
+finite differences in test_oracle_complex_el.py): aiqmc_local_energy_complex = the log|psi| launch
+pair + the theta = arg psi launch pair (PH instantiations of the adjoint and first-derivative
+passes) + one combining launch."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx_and_oracle(name, dtype, B, seed):
+    from oracle import network, system
+    from aiqmc import _lib
+    s = system.make_system(name)
+    t = s.tables()
+    rng = np.random.default_rng(seed)
+    params = system.init_params(rng, s, randomize_aux=True)
+    pos = system.init_electrons(rng, s.atoms, s.charges, B, 1.0)
+    ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
+                       t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"], dtype=dtype,
+                       device=0)
+    ctx.set_params(system.flatten_params(params))
+    return s, ctx, network.Network(s), params, pos
+
+
+@pytest.mark.parametrize("name", ["H2", "Be", "C", "Ne", "N2"])
+def test_complex_local_energy_matches_oracle_fp64(name):
+    from oracle import hamiltonian, network
+    s, ctx, net, params, pos = _ctx_and_oracle(name, torch.float64, 16, 31)
+    x = torch.tensor(pos, device="cuda")
+    ec = ctx.local_energy_complex(x)
+    e_re, _, _ = ctx.local_energy(x)
+    torch.cuda.synchronize()
+    ref = hamiltonian.batch_local_energy_complex(net, network.to_torch(params), torch.tensor(pos))
+    got = ec.cpu().numpy()
+    print(name, "max |d re|", np.abs(got.real - ref.real.numpy()).max(), "max |d im|",
+          np.abs(got.imag - ref.imag.numpy()).max(), "max |im|", np.abs(ref.imag.numpy()).max())
+    assert np.abs(ref.imag.numpy()).max() > 1e-3          # a genuinely complex wavefunction
+    np.testing.assert_allclose(got.real, ref.real.numpy(), rtol=1e-8, atol=1e-6)
+    np.testing.assert_allclose(got.imag, ref.imag.numpy(), rtol=1e-8, atol=1e-6)
+    # Re = E_L + |grad theta|^2 / 2 >= E_L
+    assert np.all(got.real >= e_re.cpu().numpy() - 1e-9)
+
+
+def test_complex_local_energy_fp32_vs_oracle():
+    """fp32 N2 (the reference's dtype): errors against the float64 oracle at fp32 level (the
+    determinant terms cancel as in the real E_L; bounds as test_precision_fp32's quantiles)."""
+    from oracle import hamiltonian, network
+    s, ctx, net, params, pos = _ctx_and_oracle("N2", torch.float32, 64, 33)
+    pos32 = pos.astype(np.float32)
+    ec = ctx.local_energy_complex(torch.tensor(pos32, device="cuda"))
+    torch.cuda.synchronize()
+    ref = hamiltonian.batch_local_energy_complex(net, network.to_torch(params), torch.tensor(pos32.astype(np.float64)))
+    got = ec.cpu().numpy().astype(np.complex128)
+    r = ref.numpy()
+    scale = np.maximum(1.0, np.abs(r))
+    err = np.abs(got - r) / scale
+    print("fp32 complex E_L: rel err median", np.median(err), "p90", np.quantile(err, 0.9), "max", err.max())
+    assert np.median(err) < 1e-4
+    assert np.quantile(err, 0.9) < 2e-3
+
+
+def test_drop_in_complex_output():
+    """hamiltonian.local_energy / local_kinetic_energy with complex_output=True through the drop-in
+    API (make_ai_net apply), as the reference's drivers would call it."""
+    from oracle import hamiltonian as oh, network as onet, system
+    from aiqmc import spin_indices
+    from aiqmc.Energy import hamiltonian as H
+    from aiqmc.wavefunction_Ynlm import nn
+    s = system.make_system("Be")
+    par, anti, npar, nanti = spin_indices.jastrow_indices_ee(spins=s.spins, nelectrons=s.nelectrons)
+    up, dn = spin_indices.spin_indices_h(s.spins)
+    network = nn.make_ai_net(ndim=3, nelectrons=s.nelectrons, natoms=s.natoms, nspins=s.nspins, determinants=1,
+                             charges=s.charges, parallel_indices=par, antiparallel_indices=anti,
+                             n_parallel=npar, n_antiparallel=nanti, spin_up_indices=up, spin_down_indices=dn)
+    params = system.init_params(np.random.default_rng(35), s, randomize_aux=True)
+    pos = system.init_electrons(np.random.default_rng(36), s.atoms, s.charges, 8, 1.0)
+    data = nn.AINetData(positions=torch.tensor(pos, device="cuda"), spins=s.spins, atoms=s.atoms, charges=s.charges)
+    e, mat = H.local_energy(f=network.apply, charges=s.charges, nspins=s.spins, complex_output=True)(params, None, data)
+    ke = H.local_kinetic_energy(network.apply, complex_output=True)(params, data)
+    e_real, _ = H.local_energy(f=network.apply, charges=s.charges, nspins=s.spins)(params, None, data)
+    torch.cuda.synchronize()
+    assert mat is None and e.is_complex() and ke.is_complex()
+    ref = oh.batch_local_energy_complex(onet.Network(s), onet.to_torch(params), torch.tensor(pos)).numpy()
+    np.testing.assert_allclose(e.cpu().numpy(), ref, rtol=1e-8, atol=1e-6)
+    # KE = E - V: same imaginary part, real parts differ by the (real) potential
+    np.testing.assert_allclose(ke.imag.cpu().numpy(), e.imag.cpu().numpy(), rtol=0, atol=1e-12)
+    v = (e_real - H.local_kinetic_energy(network.apply, complex_output=False)(params, data)).cpu().numpy()
+    np.testing.assert_allclose(e.real.cpu().numpy() - ke.real.cpu().numpy(), v, rtol=1e-9, atol=1e-9)
