@@ -89,3 +89,27 @@ def test_drop_in_complex_output():
     np.testing.assert_allclose(ke.imag.cpu().numpy(), e.imag.cpu().numpy(), rtol=0, atol=1e-12)
     v = (e_real - H.local_kinetic_energy(network.apply, complex_output=False)(params, data)).cpu().numpy()
     np.testing.assert_allclose(e.real.cpu().numpy() - ke.real.cpu().numpy(), v, rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_complex_local_energy_waves_and_ragged_batches(dtype):
+    """The theta pass in both first-derivative instantiations (one wave per walker, and the
+    2 / 4-waves split of small batches) agrees to rounding; ragged and empty batches give the rows
+    of the full batch."""
+    s, ctx, net, params, pos = _ctx_and_oracle("N2", dtype, 65, 37)
+    x = torch.tensor(pos, dtype=dtype, device="cuda").contiguous()
+    out = {}
+    for w in (1, 2, 4):
+        ctx.set_lap_waves(w)
+        out[w] = ctx.local_energy_complex(x)
+    ctx.set_lap_waves(0)
+    full = ctx.local_energy_complex(x)
+    part = ctx.local_energy_complex(x[:7])
+    empty = ctx.local_energy_complex(x[:0])
+    torch.cuda.synchronize()
+    tol = 1e-10 if dtype == torch.float64 else 2e-4
+    for w in (2, 4):
+        d = (out[w] - out[1]).abs() / out[1].abs().clamp(min=1.0)
+        assert float(d.max()) < tol, (w, float(d.max()))
+    assert torch.equal(part, full[:7])
+    assert empty.shape == (0,)
