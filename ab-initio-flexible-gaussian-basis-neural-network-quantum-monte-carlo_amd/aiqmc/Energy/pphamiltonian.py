@@ -4,7 +4,8 @@
 rn_non_local, non_local_coes, non_local_exps, natoms, nelectrons, ndim, list_l,
 use_scan=False, complex_output=False)`` returns ``_e_l(params, key, data) ->
 (E_L, None)`` (pphamiltonian.py:130-190) with E_L complex [B]:
-V_ee + V_nn + KE + local pp + nonlocal pp.  The whole batch runs on the GPU
+V_ee + V_nn + KE + local pp + nonlocal pp (complex_output=True adds the kinetic energy's phase
+terms, pphamiltonian.py:84-104, from aiqmc_local_energy_complex).  The whole batch runs on the GPU
 (aiqmc_local_energy_ecp): the all-electron local-energy kernels, then the
 N*A*50 quadrature configurations of every walker as value-only single-electron
 moves through the walker cache, then one reduction wave per walker.
@@ -37,8 +38,6 @@ def local_energy(f, lognetwork, charges, nspins, rn_local, local_coes, local_exp
                  non_local_coes, non_local_exps, natoms: int, nelectrons: int, ndim: int, list_l: int,
                  use_scan: bool = False, complex_output: bool = False):
     del nspins, use_scan, lognetwork
-    if complex_output:
-        raise NotImplementedError("complex_output=True (phase Laplacian) is not built (SURVEY Q9)")
     if ndim != 3:
         raise NotImplementedError("ndim must be 3")
     net = _network_of(f)
@@ -67,6 +66,12 @@ def local_energy(f, lognetwork, charges, nspins, rn_local, local_coes, local_exp
         else:
             k = key if isinstance(key, PhiloxKey) else PhiloxKey(int(key or 0), 0)
             e = ctx.local_energy_ecp(pos, seed=k.seed, offset=k.offset)
+        if complex_output:
+            # the phase terms of the kinetic energy (pphamiltonian.py:84-104 = hamiltonian.py:110-130):
+            # the complex all-electron E_L minus the real one (the potential cancels)
+            el_c = ctx.local_energy_complex(pos)
+            el_r, _, _ = ctx.local_energy(pos)
+            e = e + (el_c - el_r.to(el_c.real.dtype))
         return e.reshape(pos.shape[:-1]), None
 
     _e_l._aiqmc_network = net

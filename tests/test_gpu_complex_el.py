@@ -113,3 +113,37 @@ def test_complex_local_energy_waves_and_ragged_batches(dtype):
         assert float(d.max()) < tol, (w, float(d.max()))
     assert torch.equal(part, full[:7])
     assert empty.shape == (0,)
+
+
+def test_pp_local_energy_complex_output(golden_dir):
+    """pphamiltonian.local_energy(..., complex_output=True) (C atom ccECP, the golden walkers and
+    rotations): the real-kinetic pp E_L of the golden fixture plus the oracle's phase terms of the
+    kinetic energy (complex minus real all-electron E_L; pphamiltonian.py:84-104)."""
+    import os
+    from oracle import hamiltonian as oh, network as onet, pphamiltonian as opp, system
+    from aiqmc import spin_indices
+    from aiqmc.Energy import pphamiltonian
+    from aiqmc.wavefunction_Ynlm import nn
+    g = dict(np.load(os.path.join(golden_dir, "C_ecp.npz")))
+    s = system.make_system("C_ecp")
+    par, anti, npar, nanti = spin_indices.jastrow_indices_ee(spins=s.spins, nelectrons=s.nelectrons)
+    up, dn = spin_indices.spin_indices_h(s.spins)
+    network = nn.make_ai_net(ndim=3, nelectrons=4, natoms=1, nspins=(2, 2), determinants=1, charges=s.charges,
+                             parallel_indices=par, antiparallel_indices=anti, n_parallel=npar,
+                             n_antiparallel=nanti, spin_up_indices=up, spin_down_indices=dn)
+    params = system.unflatten_params(system.init_params(np.random.default_rng(0), s), g["params_flat"])
+    e = opp.c_atom_ccecp()
+    kw = dict(f=network.apply, lognetwork=None, charges=s.charges, nspins=s.spins, rn_local=e.rn_local,
+              local_coes=e.local_coes, local_exps=e.local_exps, rn_non_local=e.rn_non_local,
+              non_local_coes=e.non_local_coes, non_local_exps=e.non_local_exps, natoms=1, nelectrons=4, ndim=3,
+              list_l=2)
+    data = nn.AINetData(positions=torch.tensor(g["pos"], device="cuda"), spins=s.spins, atoms=s.atoms,
+                        charges=s.charges)
+    rot = pphamiltonian.HostRotations(torch.tensor(g["rot"]))
+    out_c, _ = pphamiltonian.local_energy(complex_output=True, **kw)(params, rot, data)
+    torch.cuda.synchronize()
+    net, pt, x = onet.Network(s), onet.to_torch(params), torch.tensor(g["pos"])
+    corr = oh.batch_local_energy_complex(net, pt, x).numpy() - oh.batch_local_energy(net, pt, x)[0].numpy()
+    ref = g["e_re"] + 1j * g["e_im"] + corr
+    assert np.abs(corr.imag).max() > 1e-3
+    np.testing.assert_allclose(out_c.cpu().numpy(), ref, rtol=1e-8, atol=1e-6)
