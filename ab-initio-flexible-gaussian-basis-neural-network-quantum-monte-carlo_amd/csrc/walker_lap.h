@@ -108,7 +108,13 @@ __device__ __forceinline__ void lap_layer(cptr<T> P, const T* xs, T* hb, const T
   }
 
   // multi-wave mode: wave wv of the walker's workgroup takes columns i = wv, wv + W, ...
-#pragma unroll 1
+  // Unrolled by two (round 4, N2 4096 walkers, local-energy pair 195.9-196.6 -> 193.5-193.9 us at
+  // the same 191 VGPRs; by four, or E4's (r, s) loop by two / four as well: no further gain,
+  // profiles/r04_s9_ab_lap_unroll.txt)
+#ifndef AQ_LAP_COL_UNROLL
+#define AQ_LAP_COL_UNROLL 2
+#endif
+#pragma unroll AQ_LAP_COL_UNROLL
   for (int i = wv; i < N; i += W) {
     const bool diag = (le == i);
     T d[3];
@@ -489,7 +495,10 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
       di += ur[f] * Qs[((r * N + r) * NH + f) * 2 + 1];
     }
     ss += PH ? T(2) * dr * di : dr * dr - di * di;
-#pragma unroll 1
+#ifndef AQ_LAP_E4_UNROLL
+#define AQ_LAP_E4_UNROLL 1
+#endif
+#pragma unroll AQ_LAP_E4_UNROLL
     for (int s = r + 1; s < N; ++s) {
       T ar = T(0), ai = T(0), br = T(0), bi = T(0);
 #pragma unroll
