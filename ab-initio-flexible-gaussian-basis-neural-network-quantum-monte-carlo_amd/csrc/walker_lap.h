@@ -461,7 +461,10 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
   // E4: cross = Re sum_r z_r S_re (z = B^T w);  ss = Re sum_{r,s} S_rs S_sr,  S_rs = sum_f U_rf Q_f[r,s]
   // (row r costs N - r: wave wv takes rows wv, 2W-1-wv, 2W+wv, ... so the shares balance)
   T cross = T(0), ss = T(0);
-#pragma unroll 1
+#ifndef AQ_LAP_E4R_UNROLL
+#define AQ_LAP_E4R_UNROLL 1
+#endif
+#pragma unroll AQ_LAP_E4R_UNROLL
   for (int t = 0; t * W < N; ++t) {
     const int r = t * W + ((t & 1) ? W - 1 - wv : wv);
     if (r >= N) continue;
