@@ -302,7 +302,12 @@ __device__ __forceinline__ int xcd_major(int blk, int n) {
 // with coalesced stores (direct per-lane stores scatter over 16 records x 4 lanes).
 // MOVED_WPB independent waves (16 proposals each) per workgroup: the launch pays per workgroup
 // (see AQ_PROP_WPB); the grid is padded to a multiple of 8 and the padding waves exit.
-constexpr int MOVED_WPB = 4;
+// (round 4: 2 per workgroup, N2 iteration at 512 walkers 0.780-0.784 -> 0.770-0.777 ms, 4096 equal;
+// 8: no better; profiles/r04_s9_ab_prop_wpb.txt)
+#ifndef AQ_MOVED_WPB
+#define AQ_MOVED_WPB 2
+#endif
+constexpr int MOVED_WPB = AQ_MOVED_WPB;
 template <typename T, int N, int A>
 __global__ __launch_bounds__(64 * MOVED_WPB) void k_moved_electron(KArgs ka) {
   using Ly = Lay<N, A>;
@@ -427,8 +432,11 @@ template <typename T, int N, int A, bool PREP, bool PROP, bool PW7 = false> stru
 //   the walker's LapCache; no gradient (B3/B4) and no Metropolis cache.
 // Proposal launches: AQ_PROP_WPB configurations (one wave each) per workgroup; the waves share
 // nothing, so their LDS regions are disjoint and every barrier is wave-local.
+// (round 4, re-measured on the final code: 2 per workgroup beats 4 at 4096 N2 walkers, proposal
+// launch 222.3-224.9 -> 219.1-222.0 us, iteration 2.990-3.019 -> 2.962-2.997 ms; 1 and 8 are slower,
+// 512 walkers equal; profiles/r04_s9_ab_prop_wpb.txt)
 #ifndef AQ_PROP_WPB
-#define AQ_PROP_WPB 4
+#define AQ_PROP_WPB 2
 #endif
 #ifndef AQ_WALK_WPB
 #define AQ_WALK_WPB 1
