@@ -253,7 +253,11 @@ def make_ai_net(nspins, charges, parallel_indices, antiparallel_indices, spin_up
     (nn.py:531-539), whose orbital layer always carries its bias."""
     del determinants, bias_orbitals
     if rescale_inputs:
-        raise NotImplementedError("rescale_inputs=True is not built (reference default False)")
+        raise NotImplementedError(
+            "rescale_inputs=True: the reference's rescaled e-e features are ee*log(1+r_ee)/r_ee with "
+            "r_ee masked to 0 on the diagonal (nn.py:115,130-131), i.e. 0/0 = NaN, and the g_two means "
+            "(nn.py:151) spread it to every electron, so its log|psi| is NaN for every configuration "
+            "(tests/test_oracle_rescale_inputs.py); the drop-in refuses the option instead")
     if tuple(tuple(h) for h in hidden_dims) != DEFAULT_HIDDEN_DIMS or \
             tuple(hidden_dims_Ynlm) != DEFAULT_HIDDEN_DIMS_YNLM:
         raise NotImplementedError("only the default hidden dims are built")

@@ -97,8 +97,9 @@ def convolu_layer(n, x, w, b):
 class Network:
     """make_ai_net (nn.py:511-553) with the closure tables of a System."""
 
-    def __init__(self, system: System):
+    def __init__(self, system: System, rescale_inputs: bool = False):
         self.system = system
+        self.rescale_inputs = rescale_inputs
         t = system.tables()
         self.N = system.nelectrons
         self.A = system.natoms
@@ -117,8 +118,17 @@ class Network:
         charges = self.charges.to(pos.dtype)
         ae, ee, r_ae, r_ee = construct_input_features(pos, atoms)
         # make_ai_net_layers.apply (nn.py:321-352)
-        ae_features = torch.cat([r_ae, ae], dim=2).reshape(N, -1)
-        ee_features = torch.cat([r_ee, ee], dim=2)
+        if self.rescale_inputs:
+            # nn.py:126-131: log(1 + r) and the vector times log(1 + r)/r.  On the r_ee diagonal
+            # (masked to exactly 0 at nn.py:115) that is (0 * 0)/0 = NaN, and the NaN reaches every
+            # electron through the g_two means of construct_symmetric_features (nn.py:151).
+            lr_ae = torch.log(1 + r_ae)
+            ae_features = torch.cat([lr_ae, ae * lr_ae / r_ae], dim=2).reshape(N, -1)
+            lr_ee = torch.log(1 + r_ee)
+            ee_features = torch.cat([lr_ee, ee * lr_ee / r_ee], dim=2)
+        else:
+            ae_features = torch.cat([r_ae, ae], dim=2).reshape(N, -1)
+            ee_features = torch.cat([r_ee, ee], dim=2)
         temp = ae / r_ae
         y_sp = y_l_real(temp).reshape(N, -1)
         y_df = y_l_real_high(temp, r_ae).reshape(N, -1)
