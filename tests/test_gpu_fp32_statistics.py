@@ -1,0 +1,125 @@
+"""The benched fp32 Metropolis path samples the same distribution as the fp64 path (a
+size-independent property at the benchmark size, N2 and Be at 4,096 walkers).
+
+VMC is a Markov chain: the fp32 and fp64 chains start from the same walkers with the same
+on-device Philox draws (seed, offset), follow each other while their rounding differences stay
+small and decorrelate afterwards, but both must sample |psi|^2 of the same network.  We run
+warm-up + measured VMC iterations (mc_step with nsteps=10, tstep=0.05, then the local energy:
+the bench's iteration, VMCmcstep.py:121-140 + hamiltonian.py:236-260) in each precision and
+compare, per iteration, robust walker statistics (the median and the 1 %-trimmed mean of E_L,
+the mean electron-nucleus distance) and the acceptance rate.  STATUS (round 4): both cases are
+xfail -- with Gaussian-only envelopes the fp32 kernels meet far-out electrons whose rows are
+~1e-19 and return NaN gradients / E_L there (pinned by the last test), which the fp32 oracle does
+not; found by this test, open for round 5.  The bound is 5 combined standard
+errors of the block means (blocks of 5 iterations) plus a small absolute floor; the oracle does
+not enter (it is far too slow at this size), the fp64 kernels are pinned against it elsewhere
+(tests/test_gpu_parity.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+B, WARM, ITERS, NSTEPS, TSTEP = 4096, 20, 40, 10, 0.05
+
+
+def _ctx(name, dtype):
+    from oracle import system
+    from aiqmc import _lib
+    s = system.make_system(name)
+    t = s.tables()
+    ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
+                       t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"], dtype=dtype,
+                       device=0)
+    p = system.init_params(np.random.default_rng(1), s)
+    # sigma = 0 drops the envelope's signed exp(-pi * ae) term (envelope.py:26-30), which grows
+    # without bound along negative ae: with it |psi|^2 is not normalisable and the chains drift
+    # outwards for ever (measured with it: mean r_ae 21 bohr after 600 steps and rising, block
+    # errors dominated by the drift, acceptance 0.997 in fp64 vs 0.959 +- 0.016 in fp32).  What
+    # remains, sum_a alpha exp(-beta r^2) times the network and Jastrows, is a proper distribution.
+    for env in p["envelope"]:
+        env["sigma"] = np.zeros_like(env["sigma"])
+    ctx.set_params(system.flatten_params(p))
+    return s, ctx
+
+
+def _chain(name, dtype):
+    from oracle import system
+    s, ctx = _ctx(name, dtype)
+    x = system.init_electrons(np.random.default_rng(0), s.atoms, s.charges, B, 1.0)
+    pos = torch.tensor(x, dtype=dtype, device="cuda").contiguous()
+    atoms = torch.tensor(np.asarray(s.atoms), dtype=torch.float64, device="cuda")
+    rows = []
+    for it in range(WARM + ITERS):
+        acc = ctx.mc_step(pos, NSTEPS, TSTEP, seed=7, offset=it, count_accepts=True)
+        el, _, _ = ctx.local_energy(pos)
+        if it < WARM:
+            continue
+        e = el.double()
+        assert torch.isfinite(e).all()
+        es = torch.sort(e).values
+        k = B // 100
+        r = torch.linalg.norm(pos.double().reshape(B, s.nelectrons, 1, 3) - atoms.reshape(1, 1, -1, 3), dim=-1)
+        rows.append([float(es[B // 2]), float(es[k:B - k].mean()), float(r.mean()),
+                     float(acc.double().sum()) / (B * s.nelectrons * NSTEPS)])
+    torch.cuda.synchronize()
+    return np.array(rows)
+
+
+def _block_stats(v, bs=5):
+    nb = len(v) // bs
+    m = v[:nb * bs].reshape(nb, bs).mean(1)
+    return m.mean(), m.std(ddof=1) / np.sqrt(nb)
+
+
+@pytest.mark.parametrize("name", [
+    pytest.param("N2", marks=pytest.mark.xfail(strict=False, reason=(
+        "open (round 4): the fp32 N2 chain stops accepting after ~10 iterations; the cause is the "
+        "NaN fp32 gradient pinned by test_fp32_gradient_finite_with_a_far_electron"))),
+    pytest.param("Be", marks=pytest.mark.xfail(strict=False, reason=(
+        "open (round 4): the fp32 Be chain reaches a walker with a non-finite fp32 E_L within 60 "
+        "iterations (fp64 finite throughout); same Gaussian-envelope far-electron regime")))])
+def test_fp32_chain_samples_fp64_distribution(name):
+    c64 = _chain(name, torch.float64)
+    c32 = _chain(name, torch.float32)
+    labels = ["E_L median", "E_L trimmed mean", "mean r_ae", "acceptance"]
+    floors = [1e-3, 1e-3, 1e-4, 1e-3]
+    for j, (lab, floor) in enumerate(zip(labels, floors)):
+        m64, s64 = _block_stats(c64[:, j])
+        m32, s32 = _block_stats(c32[:, j])
+        bound = 5.0 * np.hypot(s64, s32) + floor * max(1.0, abs(m64))
+        print(f"{name} {lab}: fp64 {m64:.6f} +- {s64:.2e}, fp32 {m32:.6f} +- {s32:.2e}, "
+              f"diff {m32 - m64:+.2e}, bound {bound:.2e}")
+        assert abs(m32 - m64) <= bound, (lab, m32, m64, bound)
+    # the acceptance rate of the measured iterations is a genuine rate (the chains move)
+    assert 0.05 < c32[:, 3].mean() < 0.999
+
+
+@pytest.mark.xfail(strict=False, reason=(
+    "open (round 4): with one electron 6.6 bohr out (row envelope ~1e-19) the fp32 value+gradient "
+    "kernels (reverse and forward mode alike) return a NaN gradient for 7 of the 14 single-electron "
+    "proposals while log|psi| is right; the fp32 oracle (torch float32/complex64) and the fp64 "
+    "kernels are finite there; one NaN poisons limdrift's batch sum, so the whole batch rejects"))
+def test_fp32_gradient_finite_with_a_far_electron(golden_dir):
+    """The walker the fp32 N2 chain above froze on (tests/golden/N2_fp32_far_electron.npz, made by
+    tools/freeze_probe.py; params = _ctx's) and its 14 proposal configurations (the drifted move
+    of VMCmcstep.py:58-76 with the fixture's gauss1): finite gradients in fp32 as in fp64."""
+    import os
+    d = np.load(os.path.join(golden_dir, "N2_fp32_far_electron.npz"))
+    s, c32 = _ctx("N2", torch.float32)
+    _, c64 = _ctx("N2", torch.float64)
+    N = s.nelectrons
+    x = torch.tensor(d["frozen"][0], dtype=torch.float64)
+    la, g = c64.logpsi_grad(x.reshape(1, -1).cuda().contiguous())
+    v2 = float((g ** 2).sum())
+    f = (np.sqrt(1 + 2 * TSTEP * 0.25 * v2) - 1) / (0.25 * v2)
+    step = g.cpu().reshape(N, 3) * f * TSTEP + np.sqrt(TSTEP) * torch.tensor(d["g1"][0, 0], dtype=torch.float64).reshape(N, 3)
+    xs = x.reshape(1, N, 3).repeat(N + 1, 1, 1)
+    xs[torch.arange(N), torch.arange(N)] += step
+    xs = xs.reshape(N + 1, 3 * N)
+    l64, g64 = c64.logpsi_grad(xs.cuda().contiguous())
+    l32, g32 = c32.logpsi_grad(xs.float().cuda().contiguous())
+    assert torch.isfinite(g64).all()
+    np.testing.assert_allclose(l32.double().cpu().numpy(), l64.cpu().numpy(), rtol=1e-5, atol=1e-3)
+    assert torch.isfinite(g32).all(), (~torch.isfinite(g32).all(1)).nonzero().flatten().tolist()

@@ -1,0 +1,36 @@
+"""Diagnostic follow-up: which electron of the frozen walker makes the fp32 gradient of its
+proposal configurations NaN (move each electron in turn towards the nearest nucleus)."""
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, ".")
+sys.path.insert(0, "tests")
+sys.path.insert(0, "ab-initio-flexible-gaussian-basis-neural-network-quantum-monte-carlo_amd")
+from test_gpu_fp32_statistics import _ctx, TSTEP
+
+d = np.load("tests/golden/N2_fp32_far_electron.npz")
+s, c = _ctx("N2", torch.float32)
+N = 14
+x0 = torch.tensor(d["frozen"][0], dtype=torch.float64).reshape(N, 3)
+g1 = torch.tensor(d["g1"][0, 0], dtype=torch.float64).reshape(N, 3)
+at = torch.tensor(np.asarray(s.atoms), dtype=torch.float64)
+
+
+def props(x):
+    la, g = c.logpsi_grad(x.reshape(1, -1).float().cuda().contiguous())
+    v2 = float((g.double() ** 2).sum())
+    f = (np.sqrt(1 + 2 * TSTEP * 0.25 * v2) - 1) / (0.25 * v2)
+    step = g.double().cpu().reshape(N, 3) * f * TSTEP + np.sqrt(TSTEP) * g1
+    xs = x.reshape(1, N, 3).repeat(N, 1, 1)
+    xs[torch.arange(N), torch.arange(N)] += step
+    l, gg = c.logpsi_grad(xs.reshape(N, 3 * N).float().cuda().contiguous())
+    return (~torch.isfinite(gg).all(1)).nonzero().flatten().cpu().tolist(), float(la)
+
+
+print("frozen walker: NaN-gradient proposals", props(x0), flush=True)
+for e in range(N):
+    x = x0.clone()
+    r = torch.linalg.norm(x[e] - at, dim=1)
+    a = int(r.argmin())
+    x[e] = at[a] + (x[e] - at[a]) * 0.5
+    print(f"electron {e} halfway to atom {a}: NaN proposals", props(x), flush=True)

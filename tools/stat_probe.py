@@ -1,0 +1,31 @@
+"""Diagnostic for tests/test_gpu_fp32_statistics.py: per VMC iteration, acceptance, non-finite
+log|psi| / gradients, and the largest electron-nucleus distance of fp32 and fp64 chains."""
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, ".")
+sys.path.insert(0, "tests")
+sys.path.insert(0, "ab-initio-flexible-gaussian-basis-neural-network-quantum-monte-carlo_amd")
+from test_gpu_fp32_statistics import _ctx, B, NSTEPS, TSTEP
+from oracle import system
+
+name = sys.argv[1] if len(sys.argv) > 1 else "N2"
+for dtype in (torch.float32, torch.float64):
+    s, ctx = _ctx(name, dtype)
+    x = system.init_electrons(np.random.default_rng(0), s.atoms, s.charges, B, 1.0)
+    pos = torch.tensor(x, dtype=dtype, device="cuda").contiguous()
+    atoms = torch.tensor(np.asarray(s.atoms), dtype=torch.float64, device="cuda")
+    for it in range(30):
+        la, g = ctx.logpsi_grad(pos)
+        r = torch.linalg.norm(pos.double().reshape(B, s.nelectrons, 1, 3) - atoms.reshape(1, 1, -1, 3), dim=-1)
+        rmin = r.min(dim=2).values
+        bad = ~torch.isfinite(la)
+        gbad = ~torch.isfinite(g).all(dim=1)
+        msg = (f"{dtype} it {it}: logabs nonfinite {int(bad.sum())} grad nonfinite {int(gbad.sum())} "
+               f"max dist-to-nearest-atom {float(rmin.max()):.2f} logabs min {float(la[~bad].min()) if (~bad).any() else 0:.1f}")
+        if bad.any():
+            b = int(bad.nonzero()[0])
+            msg += f" first bad walker {b} rmin {rmin[b].cpu().numpy().round(2).tolist()}"
+        acc = ctx.mc_step(pos, NSTEPS, TSTEP, seed=7, offset=it, count_accepts=True)
+        msg += f" acc {float(acc.double().sum()) / (B * s.nelectrons * NSTEPS):.4f}"
+        print(msg, flush=True)
