@@ -119,24 +119,23 @@ __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, in
     const T pr = rdlane(sr, 16 * g + k);
     const T pim = rdlane(si, 16 * g + k);
     const T den = pr * pr + pim * pim;
+    T ir, ii, rm, lden_;
+    pivot_recip(pr, pim, den, ir, ii, rm, lden_);
     if (rec && lane == 0) {
       rec[k] = T(p);
-      rec[N + k] = f_sqrt(f_rcp(den));
+      rec[N + k] = rm;
     }
-    const T rden = f_rcp(den);
     {
       int e;
       pm *= f_frexp(den, e);
       pe += e;
     }
     {
-      const T rm = f_sqrt(rden);
       const T ur = pr * rm, ui = pim * rm;
       const T nr = pr_ * ur - pi_ * ui, ni = pr_ * ui + pi_ * ur;
       pr_ = nr;
       pi_ = ni;
     }
-    const T ir = pr * rden, ii = -pim * rden;   // 1 / pivot
     const T q0r = __shfl(sr, 16 * g + c), q0i = __shfl(si, 16 * g + c);
     const bool ck = (c == k);
     const T qr = ck ? ir : q0r * ir - q0i * ii;
@@ -228,8 +227,8 @@ __device__ __forceinline__ void gj_fixed_regs(typename Pair<T>::type* a2, T* Bou
       pkr = pr;
       pki = pim;
     }
-    const T rden = f_rcp(den);
-    const T ir = pr * rden, ii = -pim * rden;   // 1 / pivot
+    T ir, ii, rabs_, lden_;   // 1 / pivot
+    pivot_recip(pr, pim, den, ir, ii, rabs_, lden_);
     const T q0r = __shfl(pair_re<T>(a2[ts]), 16 * g + c), q0i = __shfl(pair_im<T>(a2[ts]), 16 * g + c);
     const bool ck = (c == k);
     const T qr = ck ? ir : q0r * ir - q0i * ii;
@@ -318,7 +317,11 @@ __device__ __forceinline__ void gj_fixed_regs(typename Pair<T>::type* a2, T* Bou
     const T ld = T(0.5) * (f_log(rdlane(m, 0)) + rdlane(ef, 0) * T(0.69314718055994531));
     logdet = ld;
     if (!bad) {
-      if (pl) rec_out[N + lane] = f_sqrt(f_rcp(den));
+      if (pl) {
+        T ir_, ii_, rabs_, lden_;
+        pivot_recip(pkr, pki, den, ir_, ii_, rabs_, lden_);
+        rec_out[N + lane] = rabs_;
+      }
       if (lane == 0) rec_out[2 * N + 1] = ld;
     }
   }

@@ -67,6 +67,32 @@ __device__ __forceinline__ double f_frexp(double x, int& e) { return frexp(x, &e
 template <typename T> __device__ __forceinline__ T f_abs(T x);
 template <> __device__ __forceinline__ float f_abs(float x) { return fabsf(x); }
 template <> __device__ __forceinline__ double f_abs(double x) { return fabs(x); }
+
+// 1 / pivot (ir, ii), 1 / |pivot| (rabs) and log |pivot|^2 (lden) of a complex pivot pr + i pim,
+// den = pr^2 + pim^2 already formed.  fp32: below |pivot| ~ 1e-15 (a row scaled by a far-out
+// electron's Gaussian envelope, ~1e-19) 1 / den overflows to inf and inf - inf turns the inverse
+// into NaN; that (rare) case scales by the larger component first.  Ordinary pivots take the
+// plain formulas, bit for bit as before.
+template <typename T>
+__device__ __forceinline__ void pivot_recip(T pr, T pim, T den, T& ir, T& ii, T& rabs, T& lden) {
+  if (sizeof(T) == 4 && den < T(1e-30)) {
+    const T s = f_abs(pr) > f_abs(pim) ? f_abs(pr) : f_abs(pim);
+    const T rs = f_rcp(s);
+    const T a = pr * rs, b = pim * rs;
+    const T d1 = a * a + b * b;
+    const T rd = f_rcp(d1);
+    ir = a * rd * rs;
+    ii = -b * rd * rs;
+    rabs = rs * f_sqrt(rd);
+    lden = T(2) * f_log(s) + f_log(d1);
+  } else {
+    const T rden = f_rcp(den);
+    ir = pr * rden;
+    ii = -pim * rden;
+    rabs = f_sqrt(rden);
+    lden = f_log(den);
+  }
+}
 __device__ __forceinline__ float f_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 __device__ __forceinline__ double f_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 template <typename T> __device__ __forceinline__ T f_hypot(T x, T y);

@@ -345,16 +345,17 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
       inv += __builtin_popcount(used >> p);
       used |= 1u << p;
       const T den = pr * pr + pim * pim;
-      const T rden = f_rcp(den);
-      lsum += f_log(den);
+      T ipr_, ipi_, rabs_, lden_;
+      pivot_recip(pr, pim, den, ipr_, ipi_, rabs_, lden_);
+      lsum += lden_;
       {
-        const T rm = f_sqrt(rden);
+        const T rm = rabs_;
         const T xr = pr * rm, xi = pim * rm;
         const T nr = ur * xr - ui * xi, ni = ur * xi + ui * xr;
         ur = nr;
         ui = ni;
       }
-      const T ipr = pr * rden, ipi = -pim * rden;   // 1 / pivot
+      const T ipr = ipr_, ipi = ipi_;   // 1 / pivot
       if (rl && !((used >> r) & 1u)) {   // rows still open: A[r][:] -= (A[r][k] / pivot) A[p][:]
         const T mr = akr * ipr - aki * ipi, mi = akr * ipi + aki * ipr;
         a -= mr * er - mi * ei;
@@ -425,16 +426,17 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
       inv += __builtin_popcount(used >> p);   // earlier pivots below p in the row order
       used |= 1u << p;
       const T den = pr * pr + pim * pim;
-      const T rden = f_rcp(den);
-      lsum += f_log(den);
+      T ipr_, ipi_, rabs_, lden_;
+      pivot_recip(pr, pim, den, ipr_, ipi_, rabs_, lden_);
+      lsum += lden_;
       {
-        const T rm = f_sqrt(rden);
+        const T rm = rabs_;
         const T xr = pr * rm, xi = pim * rm;
         const T nr = ur * xr - ui * xi, ni = ur * xi + ui * xr;
         ur = nr;
         ui = ni;
       }
-      const T ipr = pr * rden, ipi = -pim * rden;   // 1 / pivot
+      const T ipr = ipr_, ipi = ipi_;   // 1 / pivot
       if (rl && !((used >> r) & 1u)) {   // rows still open: A[r][:] -= (A[r][k] / pivot) A[p][:]
         const T mr = akr * ipr - aki * ipi, mi = akr * ipi + aki * ipr;
         a[0] -= mr * er0 - mi * ei0;
@@ -848,10 +850,11 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
       inv += __builtin_popcount(used >> p);
       used |= 1u << p;
       const T den = pr * pr + pim * pim;
-      const T rden = f_rcp(den);
-      lsum += f_log(den);
+      T ipr_, ipi_, rabs_, lden_;
+      pivot_recip(pr, pim, den, ipr_, ipi_, rabs_, lden_);
+      lsum += lden_;
       {
-        const T rm = f_sqrt(rden);
+        const T rm = rabs_;
         const T xr = pr * rm, xi = pim * rm;
         const T nr = ur * xr - ui * xi, ni = ur * xi + ui * xr;
         ur = nr;
@@ -859,9 +862,9 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
       }
       if (WALK && sl == 0 && act) {   // pivot record (gj.h: row of step k, 1 / |pivot_k|)
         Wc[WC::pv + k] = T(p);
-        Wc[WC::pv + N + k] = f_sqrt(rden);
+        Wc[WC::pv + N + k] = rabs_;
       }
-      const T ir = pr * rden, ii = -pim * rden;   // 1 / pivot
+      const T ir = ipr_, ii = ipi_;   // 1 / pivot
       const bool ck = (c == k);
       const T qr = ck ? ir : spr * ir - spi * ii;
       const T qi = ck ? ii : spr * ii + spi * ir;
@@ -954,10 +957,11 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
       inv += __builtin_popcount(used >> p);
       used |= 1u << p;
       const T den = pr * pr + pim * pim;
-      const T rden = f_rcp(den);
-      lsum += f_log(den);
+      T ipr_, ipi_, rabs_, lden_;
+      pivot_recip(pr, pim, den, ipr_, ipi_, rabs_, lden_);
+      lsum += lden_;
       {
-        const T rm = f_sqrt(rden);
+        const T rm = rabs_;
         const T xr = pr * rm, xi = pim * rm;
         const T nr = ur * xr - ui * xi, ni = ur * xi + ui * xr;
         ur = nr;
@@ -965,9 +969,9 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
       }
       if (WALK && sl == 0 && act) {   // pivot record (gj.h: row of step k, 1 / |pivot_k|)
         Wc[WC::pv + k] = T(p);
-        Wc[WC::pv + N + k] = f_sqrt(rden);
+        Wc[WC::pv + N + k] = rabs_;
       }
-      const T ir = pr * rden, ii = -pim * rden;   // 1 / pivot
+      const T ir = ipr_, ii = ipi_;   // 1 / pivot
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const bool ck = (g + 4 * h == k);

@@ -7,11 +7,11 @@ small and decorrelate afterwards, but both must sample |psi|^2 of the same netwo
 warm-up + measured VMC iterations (mc_step with nsteps=10, tstep=0.05, then the local energy:
 the bench's iteration, VMCmcstep.py:121-140 + hamiltonian.py:236-260) in each precision and
 compare, per iteration, robust walker statistics (the median and the 1 %-trimmed mean of E_L,
-the mean electron-nucleus distance) and the acceptance rate.  STATUS (round 4): both cases are
-xfail -- with Gaussian-only envelopes the fp32 kernels meet far-out electrons whose rows are
-~1e-19 and return NaN gradients / E_L there (pinned by the last test), which the fp32 oracle does
-not; found by this test, open for round 5.  The bound is 5 combined standard
-errors of the block means (blocks of 5 iterations) plus a small absolute floor; the oracle does
+the mean electron-nucleus distance) and the acceptance rate.  History (round 4): this test found
+that with Gaussian-only envelopes the fp32 kernels returned NaN gradients / E_L for far-out
+electrons (a row ~1e-19: 1/|pivot|^2 overflowed in the Gauss-Jordan / LU steps), which the fp32
+oracle does not; fixed by jets.h pivot_recip, pinned by the last test.  The
+bound is 5 combined standard errors of the block means (blocks of 5 iterations) plus a small absolute floor; the oracle does
 not enter (it is far too slow at this size), the fp64 kernels are pinned against it elsewhere
 (tests/test_gpu_parity.py).
 """
@@ -73,13 +73,7 @@ def _block_stats(v, bs=5):
     return m.mean(), m.std(ddof=1) / np.sqrt(nb)
 
 
-@pytest.mark.parametrize("name", [
-    pytest.param("N2", marks=pytest.mark.xfail(strict=False, reason=(
-        "open (round 4): the fp32 N2 chain stops accepting after ~10 iterations; the cause is the "
-        "NaN fp32 gradient pinned by test_fp32_gradient_finite_with_a_far_electron"))),
-    pytest.param("Be", marks=pytest.mark.xfail(strict=False, reason=(
-        "open (round 4): the fp32 Be chain reaches a walker with a non-finite fp32 E_L within 60 "
-        "iterations (fp64 finite throughout); same Gaussian-envelope far-electron regime")))])
+@pytest.mark.parametrize("name", ["N2", "Be"])
 def test_fp32_chain_samples_fp64_distribution(name):
     c64 = _chain(name, torch.float64)
     c32 = _chain(name, torch.float32)
@@ -96,11 +90,6 @@ def test_fp32_chain_samples_fp64_distribution(name):
     assert 0.05 < c32[:, 3].mean() < 0.999
 
 
-@pytest.mark.xfail(strict=False, reason=(
-    "open (round 4): with one electron 6.6 bohr out (row envelope ~1e-19) the fp32 value+gradient "
-    "kernels (reverse and forward mode alike) return a NaN gradient for 7 of the 14 single-electron "
-    "proposals while log|psi| is right; the fp32 oracle (torch float32/complex64) and the fp64 "
-    "kernels are finite there; one NaN poisons limdrift's batch sum, so the whole batch rejects"))
 def test_fp32_gradient_finite_with_a_far_electron(golden_dir):
     """The walker the fp32 N2 chain above froze on (tests/golden/N2_fp32_far_electron.npz, made by
     tools/freeze_probe.py; params = _ctx's) and its 14 proposal configurations (the drifted move
