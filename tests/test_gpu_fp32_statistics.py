@@ -10,7 +10,7 @@ compare, per iteration, robust walker statistics (the median and the 1 %-trimmed
 the mean electron-nucleus distance) and the acceptance rate.  History (round 4): this test found
 that with Gaussian-only envelopes the fp32 kernels returned NaN gradients / E_L for far-out
 electrons (a row ~1e-19: 1/|pivot|^2 overflowed in the Gauss-Jordan / LU steps), which the fp32
-oracle does not; fixed by jets.h pivot_recip, pinned by the last test.  The
+oracle does not; fixed by jets.h pivot_recip, pinned by the two far-electron tests.  The
 bound is 5 combined standard errors of the block means (blocks of 5 iterations) plus a small absolute floor; the oracle does
 not enter (it is far too slow at this size), the fp64 kernels are pinned against it elsewhere
 (tests/test_gpu_parity.py).
@@ -112,3 +112,18 @@ def test_fp32_gradient_finite_with_a_far_electron(golden_dir):
     assert torch.isfinite(g64).all()
     np.testing.assert_allclose(l32.double().cpu().numpy(), l64.cpu().numpy(), rtol=1e-5, atol=1e-3)
     assert torch.isfinite(g32).all(), (~torch.isfinite(g32).all(1)).nonzero().flatten().tolist()
+
+
+def test_fp32_local_energy_finite_with_a_far_electron(golden_dir):
+    """The same walker through the fp32 local-energy launch pair (adjoint pass + first-derivative
+    pass, both on the Gauss-Jordan inverse): finite, and log|psi| / gradient as in fp64."""
+    import os
+    d = np.load(os.path.join(golden_dir, "N2_fp32_far_electron.npz"))
+    _, c32 = _ctx("N2", torch.float32)
+    _, c64 = _ctx("N2", torch.float64)
+    x = torch.tensor(d["frozen"], dtype=torch.float64).cuda().contiguous()
+    e64, l64, g64 = c64.local_energy(x, want_logabs=True, want_grad=True)
+    e32, l32, g32 = c32.local_energy(x.float().contiguous(), want_logabs=True, want_grad=True)
+    assert torch.isfinite(e64).all() and torch.isfinite(e32).all() and torch.isfinite(g32).all()
+    np.testing.assert_allclose(l32.double().cpu().numpy(), l64.cpu().numpy(), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(g32.double().cpu().numpy(), g64.cpu().numpy(), rtol=1e-3, atol=1e-2)
