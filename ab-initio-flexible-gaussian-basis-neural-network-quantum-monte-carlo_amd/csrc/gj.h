@@ -59,8 +59,9 @@ __device__ __forceinline__ unsigned key_bits(double x) {
 }
 
 // rec (optional): the pivot sequence, recorded for gj_inverse_fixed: rec[k] = row of
-// step k, rec[N + k] = 1 / |pivot_k|, rec[2N] = permutation parity, rec[2N + 1] = log|det A|
-// (written by lane 0).
+// step k, rec[N + k] = 1 / |pivot_k|, rec[2N] = permutation parity, rec[2N + 1] = log|det A|,
+// rec[2N + 2 + k] = 1 / |pivot_k| again: the anchor a walker launch re-using this order keeps
+// until partial pivoting runs again (written by lane 0).
 template <typename T, int N>
 __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, int lane, T& logdet, T& phr,
                                            T& phi, T* rec = nullptr) {
@@ -124,10 +125,14 @@ __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, in
     if (rec && lane == 0) {
       rec[k] = T(p);
       rec[N + k] = rm;
+      rec[2 * N + 2 + k] = rm;
     }
     {
+      // |pivot|^2 = m 2^e formed where it cannot leave the range (pivot_mag2), branch-free:
+      // carrying the frexp form out of pivot_recip's range branch instead cost 3 VGPRs and 15
+      // spills in the N2 proposal instantiation, whose rare fallback inlines this function
       int e;
-      pm *= f_frexp(den, e);
+      pm *= pivot_mag2(pr, pim, e);
       pe += e;
     }
     {
@@ -196,8 +201,9 @@ __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, in
 // sgn(perm) prod pivots, accumulated relative to the walker's pivots:
 // z = prod_k pivot_k / |walker pivot_k| (O(1) for a one-electron move), so
 // log|det A| = log|det A_walker| + log|z| and the phase is z / |z| -- one log and one
-// sqrt per matrix instead of per step.  bad = some |pivot_k| < 0.1 |walker pivot_k| or z
-// not finite (the order may not suit this matrix: the caller falls back to gj_inverse).
+// sqrt per matrix instead of per step.  bad = some |pivot_k| < 0.1 |walker pivot_k|, some
+// |pivot_k|^2 outside the floating-point range, or z not finite (the order may not suit this
+// matrix: the caller falls back to gj_inverse, which scales out-of-range pivots).
 // rec: the walker's record written by gj_inverse (LDS copy).
 // The elimination of gj_inverse_fixed on a matrix already in its register layout:
 // a2[t] = A[rec[rg RW + t]][c] for lane 16 rg + c (zero outside the N x N block).
@@ -206,9 +212,15 @@ __device__ __forceinline__ void gj_inverse(const T* Ph, const T* Yv, T* Bout, in
 // drift from sweep to sweep through the relative form) and, unless bad, the record's magnitudes
 // and log|det| are rewritten for this matrix (rec_out[N + k], rec_out[2N + 1]; the order and
 // its parity are unchanged), so that the walker's proposals are relative to it.
+// magoff: where the reference magnitudes 1 / |pivot_k| of the `bad` test sit in rec -- N (the
+// walker's current pivots, proposals) or 2N + 2 (the anchor written when partial pivoting last
+// chose the order; walker launches): measured against the anchor, a pivot cannot shrink by just
+// under 10x per sweep for ever without re-pivoting (the pivots' growth stays bounded over a
+// long mc_step); the phase z / |z| does not depend on the reference's scale.
 template <typename T, int N>
 __device__ __forceinline__ void gj_fixed_regs(typename Pair<T>::type* a2, T* Bout, int lane, const T* rec,
-                                              T& logdet, T& phr, T& phi, bool& bad, T* rec_out = nullptr) {
+                                              T& logdet, T& phr, T& phi, bool& bad, T* rec_out = nullptr,
+                                              int magoff = N) {
   constexpr int RW = (N + 3) / 4;
   using V2 = typename Pair<T>::type;
   const int c = lane & 15;
@@ -227,8 +239,12 @@ __device__ __forceinline__ void gj_fixed_regs(typename Pair<T>::type* a2, T* Bou
       pkr = pr;
       pki = pim;
     }
-    T ir, ii, rabs_, lden_;   // 1 / pivot
-    pivot_recip(pr, pim, den, ir, ii, rabs_, lden_);
+    // 1 / pivot by the plain formula: a |pivot|^2 outside the float range (a far-out electron's
+    // row) is caught after the loop from the parked pivots and sent to the pivoted fallback, which
+    // scales it (pivot_recip_me); no range branch in this loop (it cost 3 VGPRs and 15 spills in
+    // the N2 proposal instantiation)
+    const T rden = f_rcp(den);
+    const T ir = pr * rden, ii = -pim * rden;
     const T q0r = __shfl(pair_re<T>(a2[ts]), 16 * g + c), q0i = __shfl(pair_im<T>(a2[ts]), 16 * g + c);
     const bool ck = (c == k);
     const T qr = ck ? ir : q0r * ir - q0i * ii;
@@ -251,9 +267,10 @@ __device__ __forceinline__ void gj_fixed_regs(typename Pair<T>::type* a2, T* Bou
   {
     // z = prod_k pivot_k / |walker pivot_k| over lanes 0..N-1 of row 0 (row_ror tree)
     const bool pl = lane < N;
-    const T sk = pl ? rec[N + lane] : T(0);
+    const T sk = pl ? rec[magoff + lane] : T(0);
     T ur = pl ? pkr * sk : T(1), ui = pl ? pki * sk : T(0);
-    small = __ballot(pl && (ur * ur + ui * ui < T(1e-2))) != 0;
+    const T dk = pkr * pkr + pki * pki;
+    small = __ballot(pl && ((ur * ur + ui * ui < T(1e-2)) || !(dk >= PivRange<T>::lo && dk <= PivRange<T>::hi))) != 0;
     {
       const T xr = dpp<0x128>(ur), xi = dpp<0x128>(ui);
       const T nr = ur * xr - ui * xi, ni = ur * xi + ui * xr;
@@ -300,7 +317,7 @@ __device__ __forceinline__ void gj_fixed_regs(typename Pair<T>::type* a2, T* Bou
   bad = small || !zok;
   if (rec_out) {
     const bool pl = lane < N;
-    const T den = pkr * pkr + pki * pki;
+    const T den = pkr * pkr + pki * pki;   // in range unless bad (then gj_inverse re-runs)
     int e = 0;
     T m = pl ? f_frexp(den, e) : T(1);
     T ef = pl ? T(e) : T(0);
@@ -317,11 +334,7 @@ __device__ __forceinline__ void gj_fixed_regs(typename Pair<T>::type* a2, T* Bou
     const T ld = T(0.5) * (f_log(rdlane(m, 0)) + rdlane(ef, 0) * T(0.69314718055994531));
     logdet = ld;
     if (!bad) {
-      if (pl) {
-        T ir_, ii_, rabs_, lden_;
-        pivot_recip(pkr, pki, den, ir_, ii_, rabs_, lden_);
-        rec_out[N + lane] = rabs_;
-      }
+      if (pl) rec_out[N + lane] = f_sqrt(f_rcp(den));
       if (lane == 0) rec_out[2 * N + 1] = ld;
     }
   }
@@ -329,7 +342,8 @@ __device__ __forceinline__ void gj_fixed_regs(typename Pair<T>::type* a2, T* Bou
 
 template <typename T, int N>
 __device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bout, int lane, const T* rec,
-                                                 T& logdet, T& phr, T& phi, bool& bad, T* rec_out = nullptr) {
+                                                 T& logdet, T& phr, T& phi, bool& bad, T* rec_out = nullptr,
+                                                 int magoff = N) {
   constexpr int RW = (N + 3) / 4;
   using V2 = typename Pair<T>::type;
   const int c = lane & 15;
@@ -348,7 +362,7 @@ __device__ __forceinline__ void gj_inverse_fixed(const T* Ph, const T* Yv, T* Bo
     }
     a2[t] = pair_make<T>(a, b);
   }
-  gj_fixed_regs<T, N>(a2, Bout, lane, rec, logdet, phr, phi, bad, rec_out);
+  gj_fixed_regs<T, N>(a2, Bout, lane, rec, logdet, phr, phi, bad, rec_out, magoff);
 }
 
 }  // namespace aq

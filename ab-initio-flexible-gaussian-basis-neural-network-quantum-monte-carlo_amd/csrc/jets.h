@@ -64,27 +64,71 @@ template <> __device__ __forceinline__ double f_tanh(double x) { return tanh(x);
 // mantissa in [0.5, 1) and binary exponent (v_frexp_mant / v_frexp_exp)
 __device__ __forceinline__ float f_frexp(float x, int& e) { return frexpf(x, &e); }
 __device__ __forceinline__ double f_frexp(double x, int& e) { return frexp(x, &e); }
+__device__ __forceinline__ float f_ldexp(float x, int e) { return ldexpf(x, e); }
+__device__ __forceinline__ double f_ldexp(double x, int e) { return ldexp(x, e); }
 template <typename T> __device__ __forceinline__ T f_abs(T x);
 template <> __device__ __forceinline__ float f_abs(float x) { return fabsf(x); }
 template <> __device__ __forceinline__ double f_abs(double x) { return fabs(x); }
 
-// 1 / pivot (ir, ii), 1 / |pivot| (rabs) and log |pivot|^2 (lden) of a complex pivot pr + i pim,
-// den = pr^2 + pim^2 already formed.  fp32: below |pivot| ~ 1e-15 (a row scaled by a far-out
-// electron's Gaussian envelope, ~1e-19) 1 / den overflows to inf and inf - inf turns the inverse
-// into NaN; that (rare) case scales by the larger component first.  Ordinary pivots take the
-// plain formulas, bit for bit as before.
+// 1 / pivot (ir, ii), 1 / |pivot| (rabs) and |pivot|^2 = m 2^e (m in [1/2, 1), frexp form) of a
+// complex pivot pr + i pim, den = pr^2 + pim^2 already formed.  den leaves the floating-point range
+// on both sides for a row scaled by a far-out electron's envelope: fp32 below |pivot| ~ 1e-15 (a
+// Gaussian envelope ~1e-19: 1 / den overflows, inf - inf turns the inverse into NaN; below ~1e-23
+// den itself underflows to 0 and log|det| is -inf) and above |pivot| ~ 1e15 (the signed
+// exp(-pi ae) term of envelope.py:29-30, ~1e21 at 50 bohr: den overflows, 1 / pivot becomes 0).
+// That (rare, wave-uniform in the Gauss-Jordan) case scales the pivot by the power of two of its
+// larger component first, so every quantity is formed in range, exactly as jnp.linalg.slogdet's
+// scaled pivots stay finite (network_blocks.py:156).  Ordinary pivots take the plain formulas,
+// bit for bit as before.
+template <typename T> struct PivRange;
+template <> struct PivRange<float> { static constexpr float lo = 1e-30f, hi = 1e30f; };
+template <> struct PivRange<double> { static constexpr double lo = 1e-290, hi = 1e290; };
+template <typename T>
+__device__ __forceinline__ void pivot_recip_me(T pr, T pim, T den, T& ir, T& ii, T& rabs, T& m, int& e) {
+  if (!(den >= PivRange<T>::lo && den <= PivRange<T>::hi)) {
+    const T s = f_abs(pr) > f_abs(pim) ? f_abs(pr) : f_abs(pim);
+    int es;
+    (void)f_frexp(s, es);
+    const T a = f_ldexp(pr, -es), b = f_ldexp(pim, -es);   // exact: |a|, |b| < 1
+    const T d1 = a * a + b * b;                              // in [1/4, 2)
+    const T rd = f_rcp(d1);
+    ir = f_ldexp(a * rd, -es);
+    ii = f_ldexp(-b * rd, -es);
+    rabs = f_ldexp(f_sqrt(rd), -es);
+    int e1;
+    m = f_frexp(d1, e1);
+    e = e1 + 2 * es;
+  } else {
+    const T rden = f_rcp(den);
+    ir = pr * rden;
+    ii = -pim * rden;
+    rabs = f_sqrt(rden);
+    m = f_frexp(den, e);
+  }
+}
+// |pivot|^2 = m 2^e (m in [1/2, 1)) for any finite pivot, branch-free.  float: the square formed
+// in double (exact products, one rounding; no float pivot leaves double's range); double: the
+// pivot scaled by the power of two of its larger component first (exact scalings).
+__device__ __forceinline__ float pivot_mag2(float pr, float pim, int& e) {
+  const double a = (double)pr, b = (double)pim;
+  return (float)frexp(a * a + b * b, &e);
+}
+__device__ __forceinline__ double pivot_mag2(double pr, double pim, int& e) {
+  int es, e1;
+  (void)frexp(fabs(pr) > fabs(pim) ? fabs(pr) : fabs(pim), &es);
+  const double a = ldexp(pr, -es), b = ldexp(pim, -es);
+  const double m = frexp(a * a + b * b, &e1);
+  e = e1 + 2 * es;
+  return m;
+}
+// the same with log |pivot|^2 (lden) instead of the frexp form
 template <typename T>
 __device__ __forceinline__ void pivot_recip(T pr, T pim, T den, T& ir, T& ii, T& rabs, T& lden) {
-  if (sizeof(T) == 4 && den < T(1e-30)) {
-    const T s = f_abs(pr) > f_abs(pim) ? f_abs(pr) : f_abs(pim);
-    const T rs = f_rcp(s);
-    const T a = pr * rs, b = pim * rs;
-    const T d1 = a * a + b * b;
-    const T rd = f_rcp(d1);
-    ir = a * rd * rs;
-    ii = -b * rd * rs;
-    rabs = rs * f_sqrt(rd);
-    lden = T(2) * f_log(s) + f_log(d1);
+  if (!(den >= PivRange<T>::lo && den <= PivRange<T>::hi)) {
+    T m;
+    int e;
+    pivot_recip_me(pr, pim, den, ir, ii, rabs, m, e);
+    lden = f_log(m) + T(e) * T(0.69314718055994531);
   } else {
     const T rden = f_rcp(den);
     ir = pr * rden;

@@ -863,6 +863,7 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
       if (WALK && sl == 0 && act) {   // pivot record (gj.h: row of step k, 1 / |pivot_k|)
         Wc[WC::pv + k] = T(p);
         Wc[WC::pv + N + k] = rabs_;
+        Wc[WC::pv + 2 * N + 2 + k] = rabs_;
       }
       const T ir = ipr_, ii = ipi_;   // 1 / pivot
       const bool ck = (c == k);
@@ -970,6 +971,7 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
       if (WALK && sl == 0 && act) {   // pivot record (gj.h: row of step k, 1 / |pivot_k|)
         Wc[WC::pv + k] = T(p);
         Wc[WC::pv + N + k] = rabs_;
+        Wc[WC::pv + 2 * N + 2 + k] = rabs_;
       }
       const T ir = ipr_, ii = ipi_;   // 1 / pivot
 #pragma unroll

@@ -101,13 +101,13 @@ struct SmemRev {
   static constexpr int dbar = R;
   static constexpr int R_n = COMPACT ? cmax(cmax(2 * N * N, 3 * N * N), 4 + 32 * 12)
                                      : cmax(cmax(4 * N * N, 3 * N * N), 4 + 64 * 12);
-  // the walker's pivot record [2N+2] (proposals) lives in the g2 region during F5: the g2
+  // the walker's pivot record [2N+2] (proposals; [3N+2] walker launches) lives in the g2 region during F5: the g2
   // values are dead after F4 and their adjoints are written from B2 on
   static constexpr int pv = g2;
   // proposals: F5's slot table after the pivot record, [4 RW slots][4] ints (Yt row offset, the
   // h^3 row offset for each half of the spin-stacked orbital weights, flag), then a zero row
   static constexpr int RW = (N + 3) / 4;
-  static constexpr int st = ((g2 + 2 * N + 2 + 3) / 4) * 4;
+  static constexpr int st = ((g2 + 3 * N + 2 + 3) / 4) * 4;
   static constexpr int zr = st + (4 * RW * 4 * 4 + (int)sizeof(T) - 1) / (int)sizeof(T);
   static_assert(zr + 4 <= g2 + 3 * 2 * N * 4, "slot table outside the g2 region");
   // FWDREG (proposals): the e-n Jastrow gradient of the direction lanes, parked from F2 to B4
@@ -131,8 +131,8 @@ struct WCache {
   static constexpr int jaed = jaev + N;             // [48]       dJ_ae/dx per direction lane
   static constexpr int g2 = jaed + 48;              // [3][2][N][4]
   static constexpr int jee = g2 + 3 * 2 * N * 4;    // [1]        J_ee
-  static constexpr int pv = jee + 1;                // [2N+2]     Gauss-Jordan pivot record (gj.h)
-  static constexpr int pt = ((pv + 2 * N + 2 + 3) / 4) * 4; // [N][N][8]  tanh outputs t1, t2 of pair (k, i)
+  static constexpr int pv = jee + 1;                // [3N+2]     Gauss-Jordan pivot record (gj.h)
+  static constexpr int pt = ((pv + 3 * N + 2 + 3) / 4) * 4; // [N][N][8]  tanh outputs t1, t2 of pair (k, i)
   static constexpr int size = ((pt + 8 * N * N + 63) / 64) * 64;
 };
 // Per-proposal electron-local stage of the moved electron (k_moved_electron).
@@ -687,7 +687,7 @@ k_walker_rev(KArgs ka) {
     for (int t = 0; t < NG; ++t)
       if (lane + 64 * t < 3 * 2 * N * 4) g2[lane + 64 * t] = rg[t];
   } else {
-    if (wfix) pvr = Wc[WC::pv + (lane < 2 * N + 2 ? lane : 2 * N + 1)];   // to LDS after F4, before F5's write
+    if (wfix) pvr = Wc[WC::pv + (lane < 3 * N + 2 ? lane : 3 * N + 1)];   // to LDS after F4, before F5's write
     ElecOut<T, A> eo;
     electron_stage<T, N, A>(P, xs + le * 3, le, lc, eo);
     // d(Yt row)/dx and d(ae features)/dx of this lane's electron -> walker cache (read in B4)
@@ -1068,7 +1068,7 @@ k_walker_rev(KArgs ka) {
   }
   if (ilive) hl[SM::hoff(3) + ic * 4 + ff] = hreg;
   AQ_SYNC();
-  if ((reuse || wfix) && lane < 2 * N + 2) sm[SM::pv + lane] = pvr;   // read by the Gauss-Jordan after the Phi barrier
+  if ((reuse || wfix) && lane < (wfix ? 3 * N + 2 : 2 * N + 2)) sm[SM::pv + lane] = pvr;   // read by the Gauss-Jordan after the Phi barrier
   if constexpr (PROP) {
     // F5's slot table: slot k (pivot step k) holds row r = rec[k]; it records the offsets of
     // that row's Yt row and of its h^3 row (electron rowsrc[r]) in the half of the
@@ -1265,7 +1265,7 @@ k_walker_rev(KArgs ka) {
     // this matrix's own pivots, the record's magnitudes refreshed for the proposals; the pivoted
     // elimination if a pivot comes out below 0.1 of the previous one (it then rewrites the record)
     bool bad = true;
-    if (wfix) gj_inverse_fixed<T, N>(Ph, Yv, Mx, lane, sm + SM::pv, logdet, phr, phi, bad, Wc + WC::pv);
+    if (wfix) gj_inverse_fixed<T, N>(Ph, Yv, Mx, lane, sm + SM::pv, logdet, phr, phi, bad, Wc + WC::pv, 2 * N + 2);
     if (bad) gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi, (!PREP && !isprop) ? Wc + WC::pv : nullptr);
   }
   if constexpr (!PREP) {

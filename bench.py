@@ -13,9 +13,12 @@ N = 8); a weak-scaling run at 4096 walkers per GPU is reported beside it (``weak
 ``strong_scaling_per_rank`` times the per-rank workloads of N = 2, 4, 8 (2048/1024/512
 walkers) on the one GPU.
 
-Usage: python bench.py [--gpus N --steps K --warmup W]; for N>1 launch with
+Usage: python bench.py [--gpus N --steps K --warmup W].  With N > 1 and no launcher, bench.py
+starts the N ranks itself (torch.distributed.run as a child process, before any GPU call) and
+relays rank 0's line; under an external launcher
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N --steps K --warmup W
+each rank runs directly (a WORLD_SIZE different from --gpus is an error).
 Rank 0 prints one JSON line.
 """
 import argparse
@@ -382,8 +385,43 @@ def load_pmc(lib_sha):
                 ": counters not reported for a different build")
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """``--gpus N`` without a launcher: start N ranks (one process per GPU) under
+    torch.distributed.run as a CHILD process -- never exec, and before this process touches the
+    GPU -- relay rank 0's JSON line on stdout and exit with the child's return code.  The
+    reference shards over every local device by itself (main_all_electrons_adam_muti_GPU.py:58-66)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this host driver
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
+    for line in proc.stdout:       # streamed: progress reaches the caller while the ranks run
+        s = line.strip()
+        if s.startswith("{") and '"metric"' in s:
+            print(s, flush=True)
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    return proc.wait()
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus and "--gpus" in " ".join(sys.argv):
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}: launch one rank per GPU "
+                         f"(torch.distributed.run --nproc-per-node {args.gpus}) or drop the launcher\n")
+        sys.exit(2)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -172,15 +172,21 @@ def test_fused_acceptance_is_bitwise_identical(dtype, draws):
     assert int(acc_a.sum()) > 0 and not torch.equal(a, x0)
 
 
-@pytest.mark.parametrize("name,dtype", [("N2", torch.float64), ("C", torch.float64), ("N2", torch.float32)])
-def test_walker_pivot_reuse_matches_partial_pivoting(name, dtype):
+@pytest.mark.parametrize("name,dtype,B,NS", [("N2", torch.float64, 4096, 6), ("C", torch.float64, 4096, 6),
+                                             ("N2", torch.float32, 4096, 6),
+                                             # a long mc_step (burn-in runs 50+ sweeps): the re-used
+                                             # order is checked against the pivots partial pivoting
+                                             # chose (the anchor), not the previous sweep's
+                                             ("N2", torch.float64, 1024, 50), ("C", torch.float64, 1024, 50),
+                                             ("N2", torch.float32, 1024, 50)])
+def test_walker_pivot_reuse_matches_partial_pivoting(name, dtype, B, NS):
     """From an mc_step's second sweep on, the walker launch eliminates in its previous sweep's
     pivot order (partial pivoting only when a pivot shrinks below 0.1 of the previous one) and
     refreshes the pivot record its proposals are relative to.  Against partial pivoting in every
     sweep (aiqmc_debug_set_walker_pivots(0)), six host-draw sweeps: fp64 positions to 1e-10 with
     equal accept counts; fp32 positions to 1e-5 except where rounding flips a near-tie acceptance."""
     s, ctx = _ctx(name, dtype)
-    B, NS, N = 4096, 6, s.nelectrons
+    N = s.nelectrons
     x0 = torch.tensor(_walkers(s, B, seed=21), dtype=dtype, device="cuda")
     g = torch.Generator().manual_seed(5)
     kw = dict(gauss1=torch.randn(NS, B, 3 * N, generator=g, dtype=torch.float64),
@@ -200,8 +206,10 @@ def test_walker_pivot_reuse_matches_partial_pivoting(name, dtype):
         assert torch.equal(acc_a, acc_b)
     else:
         flipped = dw > 1e-4
-        assert float(flipped.float().mean()) < 2e-3, float(flipped.float().mean())
-        assert float(dw[~flipped].max()) < 1e-5, float(dw[~flipped].max())
+        # a walker whose near-tie acceptance flipped follows its own chain from then on
+        assert float(flipped.float().mean()) < 2e-3 * max(1, NS // 6), float(flipped.float().mean())
+        # rounding differences of two elimination orders drift the chains apart slowly
+        assert float(dw[~flipped].max()) < 1e-5 * max(1, NS // 12), float(dw[~flipped].max())
 
 
 def test_proposal_reuse_matches_recompute_f32_4096():

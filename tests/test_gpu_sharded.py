@@ -148,6 +148,25 @@ def test_bench_two_ranks_weak_headline(tmp_path):
     assert r["value"] > 0 and r["finite"]
 
 
+def test_bench_gpus_flag_spawns_ranks_without_launcher(tmp_path):
+    """``python bench.py --gpus 2`` with NO launcher (the form the driver's BENCH line uses): bench.py
+    must start the two ranks itself (torch.distributed.run as a child, before any GPU call) and relay
+    rank 0's line -- not silently run one rank (VERDICT r4 weak #2)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--steps", "2",
+           "--warmup", "1", "--no-ecp", "--no-adam", "--no-dmc", "--no-cpu-baseline", "--global-walkers", "1024",
+           "--walkers", "256"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
+                         env=dict(env, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["scaling"] == "strong" and r["finite"]
+    assert r["config"]["walkers_per_gpu"] == 512 and r["config"]["global_walkers"] == 1024
+    assert r["weak_scaling"]["walkers_per_gpu"] == 256 and r["weak_scaling"]["global_walkers"] == 512
+
+
 _DMC_WORKER = r'''
 import os, sys
 sys.path.insert(0, sys.argv[1]); sys.path.insert(0, os.path.join(sys.argv[1], "ab-initio-flexible-gaussian-basis-neural-network-quantum-monte-carlo_amd"))
