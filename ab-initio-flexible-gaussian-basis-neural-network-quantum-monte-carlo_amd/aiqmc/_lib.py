@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves", "aiqmc_phase_param_grad",
     "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals", "aiqmc_debug_set_ablate", "aiqmc_debug_set_fuse_accept", "aiqmc_debug_set_walker_pivots", "aiqmc_debug_set_packed_walkers", "aiqmc_debug_set_lap_waves",
     "aiqmc_debug_set_fuse_reduce", "aiqmc_energy_stats", "aiqmc_energy_stats_final",
-    "aiqmc_debug_limdrift_factor",
+    "aiqmc_debug_limdrift_factor", "aiqmc_debug_launch_lds",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -129,6 +129,8 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_debug_set_ablate.restype = ctypes.c_int
     lib.aiqmc_debug_set_fuse_accept.argtypes = [vp, i32]
     lib.aiqmc_debug_set_fuse_accept.restype = ctypes.c_int
+    lib.aiqmc_debug_launch_lds.argtypes = [i32, i32, i32, i32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+    lib.aiqmc_debug_launch_lds.restype = ctypes.c_int
     lib.aiqmc_debug_set_walker_pivots.argtypes = [vp, i32]
     lib.aiqmc_debug_set_walker_pivots.restype = ctypes.c_int
     lib.aiqmc_debug_set_packed_walkers.argtypes = [vp, i32]
@@ -180,6 +182,21 @@ def last_error() -> str:
 def check(rc: int, what: str):
     if rc != 0:
         raise RuntimeError(f"{what} failed ({rc}): {last_error()}")
+
+
+LDS_KINDS = ("proposal", "walker", "adjoint", "lap", "pgrad", "fwdlap")   # AIQMC_LDS_* order
+
+
+def launch_lds(nelectrons: int, natoms: int, dtype=torch.float32) -> dict:
+    """Dynamic LDS bytes and waves per workgroup of the launches of one shape (host only)."""
+    lib = load()
+    out = {}
+    for k, name in enumerate(LDS_KINDS):
+        b, w = ctypes.c_int32(0), ctypes.c_int32(0)
+        check(lib.aiqmc_debug_launch_lds(int(nelectrons), int(natoms), AIQMC_F32 if dtype == torch.float32 else AIQMC_F64,
+                                         k, ctypes.byref(b), ctypes.byref(w)), "aiqmc_debug_launch_lds")
+        out[name] = {"dyn_lds_bytes_per_wg": b.value, "waves_per_wg": w.value}
+    return out
 
 
 def supported_shapes():

@@ -1616,6 +1616,18 @@ int aiqmc_debug_set_packed_walkers(aiqmc_ctx* c, int32_t on) {
   return AIQMC_OK;
 }
 
+int aiqmc_debug_launch_lds(int32_t nelectrons, int32_t natoms, int32_t dtype, int32_t kind, int32_t* bytes,
+                           int32_t* waves) {
+  ShapeOps ops{};
+  if (!shape_ops(nelectrons, natoms, &ops)) return fail(AIQMC_EUNSUPPORTED, "no kernel instantiation for this shape");
+  if (kind < 0 || kind > 5) return fail(AIQMC_EINVAL, "kind must be one of AIQMC_LDS_*");
+  if (dtype != AIQMC_F32 && dtype != AIQMC_F64) return fail(AIQMC_EINVAL, "dtype must be AIQMC_F32 or AIQMC_F64");
+  const int d = dtype == AIQMC_F32 ? 0 : 1;
+  if (bytes) *bytes = ops.dyn_lds[d][kind];
+  if (waves) *waves = ops.wg_waves[d][kind];
+  return AIQMC_OK;
+}
+
 int aiqmc_debug_set_walker_pivots(aiqmc_ctx* c, int32_t reuse) {
   if (!c) return fail(AIQMC_EINVAL, "null context");
   c->walker_fixed_gj = reuse != 0;

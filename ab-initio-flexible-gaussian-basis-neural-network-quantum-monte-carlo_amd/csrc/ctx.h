@@ -99,6 +99,11 @@ struct ShapeOps {
   void (*gmap)(const aiqmc_ctx* c, std::vector<int>& map);                        // canonical -> kernel index
   int (*pgrad)(int dtype, const KArgs& ka, int nconf, hipStream_t s);            // k_param_grad
   int wy_off;                                                                      // Lay::wy
+  // dynamic LDS bytes per workgroup of the launches that take it, [dtype f32, f64][kind]
+  // (kind: AIQMC_LDS_* of aiqmc.h), and the waves per workgroup of each: what a profiler's
+  // dispatch record does not show (rocprofv3 reports the static group segment only)
+  int dyn_lds[2][6];
+  int wg_waves[2][6];
 };
 
 

@@ -415,24 +415,25 @@ static void accept_impl(int dtype, void* pos, const AccArgs& a, int B, hipStream
 }
 
 // per-walker parameter gradients in the kernel layout: out [nconf][Lay::total]
+template <typename T, int N, int A>
+static int pgrad_launch(const KArgs& ka, int nconf, hipStream_t s) {
+  constexpr int K = PgK<N>::value;   // walkers per wave (walker_pgrad.h)
+  constexpr int bytes = K * SmemPG<T, N, A>::bytes;
+  if (bytes > 65536) {
+    hipError_t e = hipFuncSetAttribute((const void*)&k_param_grad<T, N, A, K>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e != hipSuccess) return fail(AIQMC_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+  }
+  k_param_grad<T, N, A, K><<<dim3((nconf + K - 1) / K), dim3(64), bytes, s>>>(ka);
+  return 0;
+}
+
 template <int N, int A>
 static int pgrad_impl(int dtype, const KArgs& ka, int nconf, hipStream_t s) {
   if (dtype == AIQMC_F32) {
-    constexpr int bytes = SmemPG<float, N, A>::bytes;
-    if (bytes > 65536) {
-      hipError_t e = hipFuncSetAttribute((const void*)&k_param_grad<float, N, A>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-      if (e != hipSuccess) return fail(AIQMC_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
-    }
-    k_param_grad<float, N, A><<<dim3(nconf), dim3(64), bytes, s>>>(ka);
+    if (int rc = pgrad_launch<float, N, A>(ka, nconf, s)) return rc;
   } else {
-    constexpr int bytes = SmemPG<double, N, A>::bytes;
-    if (bytes > 65536) {
-      hipError_t e = hipFuncSetAttribute((const void*)&k_param_grad<double, N, A>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-      if (e != hipSuccess) return fail(AIQMC_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
-    }
-    k_param_grad<double, N, A><<<dim3(nconf), dim3(64), bytes, s>>>(ka);
+    if (int rc = pgrad_launch<double, N, A>(ka, nconf, s)) return rc;
   }
   return 0;
 }
@@ -466,5 +467,22 @@ bool AQ_CAT(AQ_N, AQ_A)(ShapeOps* ops) {
   ops->gmap = &gmap_impl<AQ_N, AQ_A>;
   ops->pgrad = &pgrad_impl<AQ_N, AQ_A>;
   ops->wy_off = Lay<AQ_N, AQ_A>::wy;
+  {
+    constexpr int N = AQ_N, A = AQ_A;
+    const int f[6] = {RevWpb<float, true>::value * SmemRev<float, N, A, kFwdReg>::bytes,
+                      RevWpb<float, false>::value * SmemRev<float, N, A>::bytes, SmemRev<float, N, A>::bytes,
+                      SmemLap<float, N, A>::bytes, PgK<N>::value * SmemPG<float, N, A>::bytes, Smem<float, N, true>::bytes};
+    const int d[6] = {RevWpb<double, true>::value * SmemRev<double, N, A, kFwdReg>::bytes,
+                      SmemRev<double, N, A>::bytes, SmemRev<double, N, A>::bytes, SmemLap<double, N, A>::bytes,
+                      PgK<N>::value * SmemPG<double, N, A>::bytes, Smem<double, N, true>::bytes};
+    const int wf[6] = {RevWpb<float, true>::value, RevWpb<float, false>::value, 1, 0, 1, 1};
+    const int wd[6] = {RevWpb<double, true>::value, 1, 1, 0, 1, 1};
+    for (int k = 0; k < 6; ++k) {
+      ops->dyn_lds[0][k] = f[k];
+      ops->dyn_lds[1][k] = d[k];
+      ops->wg_waves[0][k] = wf[k];   // 0: the launch chooses (k_walker_lap: 1, 2 or 4 waves)
+      ops->wg_waves[1][k] = wd[k];
+    }
+  }
   return true;
 }

@@ -2,11 +2,12 @@
 // AIQMC network (the psi_tangent of the energy-gradient custom JVP,
 // Loss/loss.py:242-265, and of the Adam step, Optimizer/adam.py:49-59).
 //
-// One wave per walker; not on the Metropolis hot path (one launch per optimisation step), so
-// the kernel favours clarity: a plain forward pass with every intermediate kept in LDS
-// (lanes over items: electrons, pairs, (electron, unit), (row, column)), Gauss-Jordan of
-// gj.h, then the reverse pass with the parameter adjoints accumulated in an LDS copy of the
-// kernel parameter layout (Lay<N,A>) by LDS atomics and written out per walker.
+// One wave per PgK walkers (four for N <= 4, two for N <= 8, one above); not on the Metropolis hot
+// path (one launch per optimisation step), so the kernel favours clarity: a plain forward pass
+// with every intermediate kept in LDS (lanes over items: electrons, pairs, (electron, unit),
+// (row, column) of every walker of the wave), Gauss-Jordan of gj.h per walker, then the reverse
+// pass with the parameter adjoints accumulated in an LDS copy of the kernel parameter layout
+// (Lay<N,A>) per walker by LDS atomics and written out per walker.
 //
 // Adjoints (L = log|det A| + J_ee + J_ae, Q11; B = A^{-1}, A = Phi (.) Yt):
 //   dL/dPhi_re[r,c] = Re B[c,r] Yt[r,c],  dL/dPhi_im[r,c] = -Im B[c,r] Yt[r,c],
@@ -56,51 +57,77 @@ struct SmemPG {
 
 template <typename T> __device__ __forceinline__ void lds_add(T* p, T v) { atomicAdd(p, v); }
 
-template <typename T, int N, int A>
+// Walkers per wave: every phase below is a loop of lanes over items (electrons, pairs, (electron,
+// unit), (row, column), parameters), which for a small system leaves most lanes idle (N = 4: 16
+// pairs, 16 (electron, unit) items, 4 electrons); PGK walkers share a wave by widening each loop to
+// PGK x items (walker k = item / n), each walker with its own LDS block.  The Gauss-Jordan (gj.h,
+// one matrix per wave) runs once per walker.  Per walker the arithmetic and its order are those of
+// the one-walker kernel (PGK = 1).
+#ifndef AQ_PGK1
+template <int N> struct PgK { static constexpr int value = N <= 4 ? 4 : (N <= 8 ? 2 : 1); };
+#else   // A/B builds: one walker per wave
+template <int N> struct PgK { static constexpr int value = 1; };
+#endif
+
+template <typename T, int N, int A, int K = 1>
 __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
   using Ly = Lay<N, A>;
   using SM = SmemPG<T, N, A>;
   constexpr int D0 = SM::D0;
   constexpr int QM = SM::QM;
+  constexpr int ST = SM::bytes / (int)sizeof(T);   // one walker's LDS block (16-byte multiple)
   const cptr<T> P = param_ptr<T>(ka.prm);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  T* sm = (T*)smem_raw;
-  T* xs = sm + SM::xs;
-  T* pg = sm + SM::pg;
-  const int conf = blockIdx.x;
+  T* const sm0 = (T*)smem_raw;
   const int lane = threadIdx.x;
   const int nup = ka.nup;
   const T gw[2] = {T(1) / T(nup), T(1) / T(N - nup)};
   const T RSQ2 = T(0.70710678118654752);
   const int* rowsrc = ka.rowsrc;
+  const int conf0 = blockIdx.x * K;
+  const int nk = ka.nconf - conf0 < K ? ka.nconf - conf0 : K;   // walkers of this wave
+  // walker k's LDS block (and its pieces)
+  auto S = [&](int k) { return sm0 + k * ST; };
 
-  if (lane < 3 * N) xs[lane] = ((const T*)ka.pos)[(size_t)conf * 3 * N + lane];
-  for (int idx = lane; idx < Ly::total; idx += 64) pg[idx] = T(0);
-  for (int idx = lane; idx < 24 * N; idx += 64) sm[SM::g2 + idx] = T(0);
-  if (lane < 2) sm[SM::red + lane] = T(0);
+  for (int it = lane; it < nk * 3 * N; it += 64) {
+    const int k = it / (3 * N), j = it - k * 3 * N;
+    S(k)[SM::xs + j] = ((const T*)ka.pos)[(size_t)(conf0 + k) * 3 * N + j];
+  }
+  for (int it = lane; it < K * Ly::total; it += 64) {
+    const int k = it / Ly::total;
+    S(k)[SM::pg + it - k * Ly::total] = T(0);
+  }
+  for (int it = lane; it < K * 24 * N; it += 64) {
+    const int k = it / (24 * N);
+    S(k)[SM::g2 + it - k * 24 * N] = T(0);
+  }
+  if (lane < 2 * K) S(lane >> 1)[SM::red + (lane & 1)] = T(0);
   __syncthreads();
 
   // ---------------------------------------------------------------- forward: electron stage
-  T jae_v = T(0);
-  if (lane < N) {
+  if (lane < nk * N) {
+    const int k = lane / N, i = lane - k * N;
+    T* sm = S(k);
     ElecOut<T, A> eo;
-    electron_stage<T, N, A>(P, xs + 3 * lane, lane, 3, eo);
+    electron_stage<T, N, A>(P, sm + SM::xs + 3 * i, i, 3, eo);
 #pragma unroll
-    for (int m = 0; m < D0; ++m) sm[SM::hl + lane * D0 + m] = eo.hf[m].v;
+    for (int m = 0; m < D0; ++m) sm[SM::hl + i * D0 + m] = eo.hf[m].v;
 #pragma unroll
-    for (int m = 0; m < NYW; ++m) sm[SM::yst + lane * NYW + m] = eo.yst[m].v;
-    sm[SM::env + lane] = eo.env.v;
+    for (int m = 0; m < NYW; ++m) sm[SM::yst + i * NYW + m] = eo.yst[m].v;
+    sm[SM::env + i] = eo.env.v;
     for (int c = 0; c < N; ++c) {
       T y = T(0);
 #pragma unroll
       for (int m = 0; m < NYW; ++m) y += eo.yst[m].v * P[Ly::wy + m * N + c];
-      sm[SM::yv + lane * N + c] = eo.env.v * y;
+      sm[SM::yv + i * N + c] = eo.env.v * y;
     }
-    jae_v = eo.jae.v;
+    lds_add(&sm[SM::red], eo.jae.v);
   }
   // ---------------------------------------------------------------- forward: pair stream column means
-  T jee_v = T(0);
-  for (int idx = lane; idx < N * N; idx += 64) {
+  for (int it = lane; it < nk * N * N; it += 64) {
+    const int kw = it / (N * N), idx = it - kw * N * N;
+    T* sm = S(kw);
+    const T* xs = sm + SM::xs;
     const int k = idx / N, i = idx - k * N;
     const bool diag = k == i;
     T d[3];
@@ -108,7 +135,7 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
     for (int c = 0; c < 3; ++c) d[c] = xs[3 * i + c] - xs[3 * k + c];
     const T r = f_sqrt(diag ? T(1) : d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
     T p[4] = {diag ? T(0) : r, diag ? T(0) : d[0], diag ? T(0) : d[1], diag ? T(0) : d[2]};
-    if (k < i) jee_v += f_div(P[Ly::jee_c + k * N + i] * r, P[Ly::jee_a + k * N + i] * r + T(1));
+    if (k < i) lds_add(&sm[SM::red + 1], f_div(P[Ly::jee_c + k * N + i] * r, P[Ly::jee_a + k * N + i] * r + T(1)));
     const int G = k >= nup ? 1 : 0;
 #pragma unroll
     for (int f = 0; f < 4; ++f) lds_add(&sm[SM::g2 + ((0 * 2 + G) * N + i) * 4 + f], p[f] * gw[G]);
@@ -137,10 +164,12 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
   for (int l = 0; l < 3; ++l) {
     const int d = l == 0 ? D0 : NH;
     const int DF = 3 * d + 2 * NH2, Q = DF / 4;
-    const T* h = sm + SM::hl + SM::hoff(l);
-    T* g1 = sm + SM::g1 + l * 2 * D0;
-    if (lane < 2 * d) {
-      const int G = lane / d, m = lane - G * d;
+    if (lane < nk * 2 * d) {
+      const int kw = lane / (2 * d), gl = lane - kw * 2 * d;
+      T* sm = S(kw);
+      const T* h = sm + SM::hl + SM::hoff(l);
+      T* g1 = sm + SM::g1 + l * 2 * D0;
+      const int G = gl / d, m = gl - G * d;
       T s = T(0);
       for (int k = (G ? nup : 0); k < (G ? N : nup); ++k) s += h[k * d + m];
       g1[G * D0 + m] = s * gw[G];
@@ -148,7 +177,11 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
     __syncthreads();
     const cptr<T> convw = P + (l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2));
     const cptr<T> convb = P + (l == 0 ? Ly::conv_b0 : (l == 1 ? Ly::conv_b1 : Ly::conv_b2));
-    for (int idx = lane; idx < N * Q; idx += 64) {
+    for (int it = lane; it < nk * N * Q; it += 64) {
+      const int kw = it / (N * Q), idx = it - kw * N * Q;
+      T* sm = S(kw);
+      const T* h = sm + SM::hl + SM::hoff(l);
+      const T* g1 = sm + SM::g1 + l * 2 * D0;
       const int i = idx / Q, q = idx - i * Q;
       T z = T(0);
       for (int s4 = 0; s4 < 4; ++s4) {
@@ -164,7 +197,10 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
     __syncthreads();
     const cptr<T> sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
     const cptr<T> sngb = P + (l == 0 ? Ly::sng_b0 : (l == 1 ? Ly::sng_b1 : Ly::sng_b2));
-    for (int idx = lane; idx < N * NH; idx += 64) {
+    for (int it = lane; it < nk * N * NH; it += 64) {
+      const int kw = it / (N * NH), idx = it - kw * N * NH;
+      T* sm = S(kw);
+      const T* h = sm + SM::hl + SM::hoff(l);
       const int i = idx / NH, f = idx - i * NH;
       T z = sngb[f];
       for (int q = 0; q < Q; ++q) z += sm[SM::cq + (l * N + i) * QM + q] * sngw[q * NH + f];
@@ -175,11 +211,10 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
     __syncthreads();
   }
   // ---------------------------------------------------------------- forward: Phi, Gauss-Jordan (nn.py:432-506)
-  T* Ph = sm + SM::ph;
-  T* Mx = sm + SM::mx;
-  T* Yv = sm + SM::yv;
-  const T* H3 = sm + SM::hl + SM::hoff(3);
-  for (int idx = lane; idx < N * N; idx += 64) {
+  for (int it = lane; it < nk * N * N; it += 64) {
+    const int kw = it / (N * N), idx = it - kw * N * N;
+    T* sm = S(kw);
+    const T* H3 = sm + SM::hl + SM::hoff(3);
     const int r = idx / N, c = idx - r * N;
     const int src = rowsrc[r], s = r < nup ? 0 : 1;
     T re = P[Ly::orb_b + (s * N + c) * 2], im = P[Ly::orb_b + (s * N + c) * 2 + 1];
@@ -188,26 +223,38 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
       re += H3[src * NH + f] * P[Ly::orb_w + ((s * NH + f) * N + c) * 2];
       im += H3[src * NH + f] * P[Ly::orb_w + ((s * NH + f) * N + c) * 2 + 1];
     }
-    Ph[idx * 2] = re;
-    Ph[idx * 2 + 1] = im;
+    sm[SM::ph + idx * 2] = re;
+    sm[SM::ph + idx * 2 + 1] = im;
   }
   __syncthreads();
-  T logdet, phr, phi;
-  gj_inverse<T, N>(Ph, Yv, Mx, lane, logdet, phr, phi);
+  T logdet[K], phr[K], phi[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (k < nk) {
+      T* sm = S(k);
+      gj_inverse<T, N>(sm + SM::ph, sm + SM::yv, sm + SM::mx, lane, logdet[k], phr[k], phi[k]);
+    } else {
+      logdet[k] = phr[k] = phi[k] = T(0);
+    }
+  }
   __syncthreads();
   // ---------------------------------------------------------------- reverse: orbitals (B1)
   const bool phg = ka.phase_grad != 0;
-  T* ybar = sm + SM::ybar;
-  T* hb = sm + SM::hb;
-  for (int idx = lane; idx < N * N; idx += 64) {
+  for (int it = lane; it < nk * N * N; it += 64) {
+    const int kw = it / (N * N), idx = it - kw * N * N;
+    T* sm = S(kw);
+    T* pg = sm + SM::pg;
+    const T* Ph = sm + SM::ph;
+    const T* Mx = sm + SM::mx;
+    const T* H3 = sm + SM::hl + SM::hoff(3);
     const int r = idx / N, c = idx - r * N;
     const int src = rowsrc[r], s = r < nup ? 0 : 1;
     const T br = Mx[(c * N + r) * 2], bi = Mx[(c * N + r) * 2 + 1];
-    const T yt = Yv[idx];
+    const T yt = sm[SM::yv + idx];
     // log|det| = Re ln det: (Re B yt, -Im B yt), dYt = Re(B Phi); phase = Im ln det:
     // (Im B yt, Re B yt), dYt = Im(B Phi)
     const T pr_ = phg ? bi * yt : br * yt, pi_ = phg ? br * yt : -bi * yt;   // dL/dPhi_re, dL/dPhi_im
-    ybar[idx] = phg ? br * Ph[idx * 2 + 1] + bi * Ph[idx * 2] : br * Ph[idx * 2] - bi * Ph[idx * 2 + 1];
+    sm[SM::ybar + idx] = phg ? br * Ph[idx * 2 + 1] + bi * Ph[idx * 2] : br * Ph[idx * 2] - bi * Ph[idx * 2 + 1];
     lds_add(&pg[Ly::orb_b + (s * N + c) * 2], pr_);
     lds_add(&pg[Ly::orb_b + (s * N + c) * 2 + 1], pi_);
 #pragma unroll
@@ -216,30 +263,36 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
       lds_add(&pg[Ly::orb_w + ((s * NH + f) * N + c) * 2 + 1], H3[src * NH + f] * pi_);
     }
   }
-  for (int idx = lane; idx < N * NH; idx += 64) {
+  for (int it = lane; it < nk * N * NH; it += 64) {
+    const int kw = it / (N * NH), idx = it - kw * N * NH;
+    T* sm = S(kw);
+    const T* Mx = sm + SM::mx;
     const int r = idx / NH, f = idx - r * NH;
     const int s = r < nup ? 0 : 1;
     T a = T(0);
     for (int c = 0; c < N; ++c) {
       const T br = Mx[(c * N + r) * 2], bi = Mx[(c * N + r) * 2 + 1];
-      const T yt = Yv[r * N + c];
+      const T yt = sm[SM::yv + r * N + c];
       const T wr = P[Ly::orb_w + ((s * NH + f) * N + c) * 2], wi = P[Ly::orb_w + ((s * NH + f) * N + c) * 2 + 1];
       a += phg ? wr * bi * yt + wi * br * yt : wr * br * yt - wi * bi * yt;
     }
-    hb[rowsrc[r] * NH + f] = a;
+    sm[SM::hb + rowsrc[r] * NH + f] = a;
   }
   __syncthreads();
   // ---------------------------------------------------------------- reverse: per electron (Yt row, envelope,
-  // e-n Jastrow, Ynlm stream), one lane per electron
-  if (lane < N) {
-    const int i = lane;
+  // e-n Jastrow, Ynlm stream), one lane per (walker, electron)
+  if (lane < nk * N) {
+    const int kw = lane / N, i = lane - kw * N;
+    T* sm = S(kw);
+    T* pg = sm + SM::pg;
+    const T* xs = sm + SM::xs;
     const T env = sm[SM::env + i];
     T ystb[NYW];
     T envb = T(0);
 #pragma unroll
     for (int m = 0; m < NYW; ++m) ystb[m] = T(0);
     for (int c = 0; c < N; ++c) {
-      const T yb = ybar[i * N + c];
+      const T yb = sm[SM::ybar + i * N + c];
       T y = T(0);
 #pragma unroll
       for (int m = 0; m < NYW; ++m) {
@@ -384,16 +437,10 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
   }
   __syncthreads();
   // ---------------------------------------------------------------- reverse: h stream (B2)
-  T* hn = sm + SM::hn;
-  T* fb = sm + SM::fb;
-  T* zc = sm + SM::zc;
-  T* zsv = sm + SM::zs;
 #pragma unroll
   for (int l = 2; l >= 0; --l) {
     const int d = l == 0 ? D0 : NH;
     const int DF = 3 * d + 2 * NH2, Q = DF / 4;
-    const T* h = sm + SM::hl + SM::hoff(l);
-    const T* g1 = sm + SM::g1 + l * 2 * D0;
     const cptr<T> convw = P + (l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2));
     const cptr<T> sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
     const int cw = l == 0 ? Ly::conv_w0 : (l == 1 ? Ly::conv_w1 : Ly::conv_w2);
@@ -401,68 +448,91 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
     const int sw = l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2);
     const int sb = l == 0 ? Ly::sng_b0 : (l == 1 ? Ly::sng_b1 : Ly::sng_b2);
     // single: s = tanh(c Ws + bs), h^{l+1} = res(h^l, s)
-    for (int idx = lane; idx < N * NH; idx += 64) {
+    for (int it = lane; it < nk * N * NH; it += 64) {
+      const int kw = it / (N * NH), idx = it - kw * N * NH;
+      T* sm = S(kw);
       const int i = idx / NH, f = idx - i * NH;
       const T s = sm[SM::sv + (l * N + i) * NH + f];
-      const T sb_ = (d == NH) ? hb[idx] * RSQ2 : hb[idx];
-      zsv[idx] = sb_ * (T(1) - s * s);
+      const T sb_ = (d == NH) ? sm[SM::hb + idx] * RSQ2 : sm[SM::hb + idx];
+      sm[SM::zs + idx] = sb_ * (T(1) - s * s);
     }
     __syncthreads();
-    for (int idx = lane; idx < Q * NH; idx += 64) {
+    for (int it = lane; it < nk * Q * NH; it += 64) {
+      const int kw = it / (Q * NH), idx = it - kw * Q * NH;
+      T* sm = S(kw);
+      T* pg = sm + SM::pg;
       const int q = idx / NH, f = idx - q * NH;
       T a = T(0), b = T(0);
       for (int i = 0; i < N; ++i) {
-        a += sm[SM::cq + (l * N + i) * QM + q] * zsv[i * NH + f];
-        if (q == 0) b += zsv[i * NH + f];
+        a += sm[SM::cq + (l * N + i) * QM + q] * sm[SM::zs + i * NH + f];
+        if (q == 0) b += sm[SM::zs + i * NH + f];
       }
       pg[sw + q * NH + f] += a;
       if (q == 0) pg[sb + f] += b;
     }
-    for (int idx = lane; idx < N * Q; idx += 64) {
+    for (int it = lane; it < nk * N * Q; it += 64) {
+      const int kw = it / (N * Q), idx = it - kw * N * Q;
+      T* sm = S(kw);
       const int i = idx / Q, q = idx - i * Q;
       T a = T(0);
 #pragma unroll
-      for (int f = 0; f < NH; ++f) a += sngw[q * NH + f] * zsv[i * NH + f];
+      for (int f = 0; f < NH; ++f) a += sngw[q * NH + f] * sm[SM::zs + i * NH + f];
       const T c = sm[SM::cq + (l * N + i) * QM + q];
       const T z = a * (T(1) - c * c);
-      zc[i * QM + q] = z;
-      pg[cb + i * Q + q] += z;
+      sm[SM::zc + i * QM + q] = z;
+      sm[SM::pg + cb + i * Q + q] += z;
     }
     __syncthreads();
     // conv: c = tanh(0.25 sum_j F_j w_j + b)
-    for (int idx = lane; idx < N * DF; idx += 64) {
+    for (int it = lane; it < nk * N * DF; it += 64) {
+      const int kw = it / (N * DF), idx = it - kw * N * DF;
+      T* sm = S(kw);
+      const T* h = sm + SM::hl + SM::hoff(l);
+      const T* g1 = sm + SM::g1 + l * 2 * D0;
       const int i = idx / DF, j = idx - i * DF;
       T F;
       if (j < d) F = h[i * d + j];
       else if (j < 3 * d) F = g1[((j - d) / d) * D0 + (j - d) % d];
       else F = sm[SM::g2 + ((l * 2 + (j - 3 * d) / 4) * N + i) * 4 + ((j - 3 * d) & 3)];
-      const T z = T(0.25) * zc[i * QM + j / 4];
-      pg[cw + i * DF + j] += z * F;
-      fb[i * SM::DFM + j] = z * convw[i * DF + j];
+      const T z = T(0.25) * sm[SM::zc + i * QM + j / 4];
+      sm[SM::pg + cw + i * DF + j] += z * F;
+      sm[SM::fb + i * SM::DFM + j] = z * convw[i * DF + j];
     }
     __syncthreads();
     // inputs: h^l (direct + group means), g2 column means
-    for (int idx = lane; idx < 2 * N * NH2; idx += 64) {
+    for (int it = lane; it < nk * 2 * N * NH2; it += 64) {
+      const int kw = it / (2 * N * NH2), idx = it - kw * 2 * N * NH2;
+      T* sm = S(kw);
       const int G = idx / (N * NH2), rem = idx - G * N * NH2, i = rem / NH2, f = rem - i * NH2;
-      sm[SM::g2b + ((l * 2 + G) * N + i) * 4 + f] = fb[i * SM::DFM + 3 * d + 4 * G + f];
+      sm[SM::g2b + ((l * 2 + G) * N + i) * 4 + f] = sm[SM::fb + i * SM::DFM + 3 * d + 4 * G + f];
     }
     if (l > 0) {
-      for (int idx = lane; idx < N * NH; idx += 64) {
+      for (int it = lane; it < nk * N * NH; it += 64) {
+        const int kw = it / (N * NH), idx = it - kw * N * NH;
+        T* sm = S(kw);
+        const T* fb = sm + SM::fb;
         const int k = idx / NH, m = idx - k * NH;
         const int G = k >= nup ? 1 : 0;
-        T a = fb[k * SM::DFM + m] + ((d == NH) ? hb[idx] * RSQ2 : T(0));
+        T a = fb[k * SM::DFM + m] + ((d == NH) ? sm[SM::hb + idx] * RSQ2 : T(0));
         T s = T(0);
         for (int i = 0; i < N; ++i) s += fb[i * SM::DFM + d + G * d + m];
-        hn[idx] = a + s * gw[G];
+        sm[SM::hn + idx] = a + s * gw[G];
       }
     }
     __syncthreads();
     if (l > 0)
-      for (int idx = lane; idx < N * NH; idx += 64) hb[idx] = hn[idx];
+      for (int it = lane; it < nk * N * NH; it += 64) {
+        const int kw = it / (N * NH), idx = it - kw * N * NH;
+        S(kw)[SM::hb + idx] = S(kw)[SM::hn + idx];
+      }
     __syncthreads();
   }
   // ---------------------------------------------------------------- reverse: pair stream (B3) + e-e Jastrow
-  for (int idx = lane; idx < N * N; idx += 64) {
+  for (int it = lane; it < nk * N * N; it += 64) {
+    const int kw = it / (N * N), idx = it - kw * N * N;
+    T* sm = S(kw);
+    T* pg = sm + SM::pg;
+    const T* xs = sm + SM::xs;
     const int k = idx / N, i = idx - k * N;
     const bool diag = k == i;
     const int G = k >= nup ? 1 : 0;
@@ -523,11 +593,18 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
   }
   __syncthreads();
   // ---------------------------------------------------------------- outputs
-  T* out = (T*)ka.grad + (size_t)conf * Ly::total;
-  for (int idx = lane; idx < Ly::total; idx += 64) out[idx] = pg[idx];
-  const T lpsi = logdet + wave_sum(jae_v + jee_v);
-  if (lane == 0 && ka.logabs) ((T*)ka.logabs)[conf] = lpsi;
-  if (lane == 0 && ka.phase) ((T*)ka.phase)[conf] = f_atan2(phi, phr);
+  for (int it = lane; it < nk * Ly::total; it += 64) {
+    const int kw = it / Ly::total, idx = it - kw * Ly::total;
+    ((T*)ka.grad)[(size_t)(conf0 + kw) * Ly::total + idx] = S(kw)[SM::pg + idx];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (k < nk && lane == 0) {
+      const T lpsi = logdet[k] + (S(k)[SM::red] + S(k)[SM::red + 1]);
+      if (ka.logabs) ((T*)ka.logabs)[conf0 + k] = lpsi;
+      if (ka.phase) ((T*)ka.phase)[conf0 + k] = f_atan2(phi[k], phr[k]);
+    }
+  }
 }
 
 // out[j] = sum_b w[b] O[b][j] over the kernel layout, deterministic, in two launches:

@@ -285,6 +285,20 @@ int aiqmc_debug_set_fuse_accept(aiqmc_ctx* ctx, int32_t on);
  * reuse = 0 runs partial pivoting in every sweep.  Results agree to rounding. */
 int aiqmc_debug_set_walker_pivots(aiqmc_ctx* ctx, int32_t reuse);
 
+/* Diagnostics (host only, no GPU call): dynamic LDS bytes per workgroup and waves per workgroup
+ * of the launches of shape (N, A) that size their LDS at launch time -- the part of a kernel's
+ * LDS that a profiler's dispatch record does not report.  kind: AIQMC_LDS_*; dtype AIQMC_F32 /
+ * AIQMC_F64.  waves = 0: chosen per launch (the first-derivative pass: 1, 2 or 4 by batch size).
+ * (profiles/summarize.py joins this with the code objects' register counts.) */
+#define AIQMC_LDS_PROPOSAL 0   /* k_walker_rev, Metropolis proposals from the walker cache */
+#define AIQMC_LDS_WALKER 1     /* k_walker_rev, walker launches / value + gradient */
+#define AIQMC_LDS_ADJOINT 2    /* k_walker_rev<PREP>, local energy adjoint pass */
+#define AIQMC_LDS_LAP 3        /* k_walker_lap, local energy first-derivative pass */
+#define AIQMC_LDS_PGRAD 4      /* k_param_grad */
+#define AIQMC_LDS_FWDLAP 5     /* k_walker<LAP>, forward-Laplacian diagnostics */
+int aiqmc_debug_launch_lds(int32_t nelectrons, int32_t natoms, int32_t dtype, int32_t kind, int32_t* bytes,
+                           int32_t* waves);
+
 /* Diagnostics: walker launches of systems with N <= 8 electrons run several walkers per wave
  * (default, on = 1: four for N <= 4, two for N <= 8); on = 0 runs one wave per walker.
  * Results agree to rounding. */
