@@ -61,17 +61,13 @@ def local_energy(f, lognetwork, charges, nspins, rn_local, local_coes, local_exp
         if getattr(ctx, "_ecp_token", None) != token:
             ctx.set_ecp(*tables, list_l=int(list_l))
             ctx._ecp_token = token
+        # complex_output: the kinetic energy's phase terms (pphamiltonian.py:84-104 =
+        # hamiltonian.py:110-130) added in the same call, from the log|psi| and theta launch pairs
         if isinstance(key, HostRotations):
-            e = ctx.local_energy_ecp(pos, rot=torch.as_tensor(key.rot))
+            e = ctx.local_energy_ecp(pos, rot=torch.as_tensor(key.rot), complex_output=complex_output)
         else:
             k = key if isinstance(key, PhiloxKey) else PhiloxKey(int(key or 0), 0)
-            e = ctx.local_energy_ecp(pos, seed=k.seed, offset=k.offset)
-        if complex_output:
-            # the phase terms of the kinetic energy (pphamiltonian.py:84-104 = hamiltonian.py:110-130):
-            # the complex all-electron E_L minus the real one (the potential cancels)
-            el_c = ctx.local_energy_complex(pos)
-            el_r, _, _ = ctx.local_energy(pos)
-            e = e + (el_c - el_r.to(el_c.real.dtype))
+            e = ctx.local_energy_ecp(pos, seed=k.seed, offset=k.offset, complex_output=complex_output)
         return e.reshape(pos.shape[:-1]), None
 
     _e_l._aiqmc_network = net

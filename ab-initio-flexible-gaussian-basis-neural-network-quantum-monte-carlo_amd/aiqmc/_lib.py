@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_workspace_bytes", "aiqmc_last_error", "aiqmc_supported_shapes",
     "aiqmc_profile_enable", "aiqmc_profile_read", "aiqmc_debug_logpsi_grad_forward",
     "aiqmc_debug_set_proposal_reuse", "aiqmc_debug_phase_cycles", "aiqmc_debug_local_energy_forward",
-    "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
+    "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_local_energy_ecp_complex", "aiqmc_logpsi_param_grad",
     "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves", "aiqmc_phase_param_grad",
     "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals", "aiqmc_debug_set_ablate", "aiqmc_debug_set_fuse_accept", "aiqmc_debug_set_walker_pivots", "aiqmc_debug_set_packed_walkers", "aiqmc_debug_set_lap_waves",
     "aiqmc_debug_set_fuse_reduce", "aiqmc_energy_stats", "aiqmc_energy_stats_final",
@@ -158,6 +158,8 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_set_ecp.argtypes = [vp, ctypes.POINTER(AiqmcEcp)]
     lib.aiqmc_local_energy_ecp.argtypes = [vp, vp, i32, i32, vp, ctypes.c_uint64, ctypes.c_uint64, vp, vp, vp,
                                            vp, vp]
+    lib.aiqmc_local_energy_ecp_complex.argtypes = [vp, vp, i32, i32, vp, ctypes.c_uint64, ctypes.c_uint64, vp, vp,
+                                                   vp]
     lib.aiqmc_profile_enable.argtypes = [vp, i32]
     lib.aiqmc_profile_read.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64)]
     lib.aiqmc_energy_stats.argtypes = [vp, i32, i64, vp, i32, vp]
@@ -166,7 +168,8 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_supported_shapes.restype = ctypes.c_char_p
     for name in ("aiqmc_create", "aiqmc_destroy", "aiqmc_set_params", "aiqmc_logpsi",
                  "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_local_energy_complex", "aiqmc_mc_step", "aiqmc_profile_enable",
-                 "aiqmc_profile_read", "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_logpsi_param_grad",
+                 "aiqmc_profile_read", "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_local_energy_ecp_complex",
+                 "aiqmc_logpsi_param_grad",
                  "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves",
                  "aiqmc_phase_param_grad", "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals",
                  "aiqmc_energy_stats", "aiqmc_energy_stats_final"):
@@ -633,9 +636,10 @@ class Context:
             check(self._lib.aiqmc_set_ecp(self._h, ctypes.byref(e)), "aiqmc_set_ecp")
 
     def local_energy_ecp(self, pos: torch.Tensor, rot: Optional[torch.Tensor] = None, seed: int = 0,
-                         offset: int = 0, want_quadrature: bool = False):
+                         offset: int = 0, want_quadrature: bool = False, complex_output: bool = False):
         """Complex pseudopotential local energy [B] (pphamiltonian.py:177-188).  rot [B,3,3]:
-        injected rotations (parity mode); None: Philox Haar draws from (seed, offset)."""
+        injected rotations (parity mode); None: Philox Haar draws from (seed, offset).
+        complex_output: with the kinetic energy's phase terms (pphamiltonian.py:84-104)."""
         p = self._pos(pos)
         B = p.shape[0]
         er = torch.empty(B, dtype=self.dtype, device=self.device)
@@ -648,10 +652,17 @@ class Context:
         nq = B * self.N * self.A * ECP_NQ
         lq = torch.empty(nq, dtype=self.dtype, device=self.device) if want_quadrature else None
         pq = torch.empty(nq, dtype=self.dtype, device=self.device) if want_quadrature else None
-        check(self._lib.aiqmc_local_energy_ecp(self._h, _ptr(p), B, AIQMC_RNG_HOST if r is not None else
-                                               AIQMC_RNG_PHILOX, _ptr(r), ctypes.c_uint64(seed),
-                                               ctypes.c_uint64(offset), _ptr(er), _ptr(ei), _ptr(lq), _ptr(pq),
-                                               _stream(self.device)), "aiqmc_local_energy_ecp")
+        mode = AIQMC_RNG_HOST if r is not None else AIQMC_RNG_PHILOX
+        if complex_output:
+            if want_quadrature:
+                raise ValueError("want_quadrature is not available with complex_output")
+            check(self._lib.aiqmc_local_energy_ecp_complex(self._h, _ptr(p), B, mode, _ptr(r), ctypes.c_uint64(seed),
+                                                           ctypes.c_uint64(offset), _ptr(er), _ptr(ei),
+                                                           _stream(self.device)), "aiqmc_local_energy_ecp_complex")
+        else:
+            check(self._lib.aiqmc_local_energy_ecp(self._h, _ptr(p), B, mode, _ptr(r), ctypes.c_uint64(seed),
+                                                   ctypes.c_uint64(offset), _ptr(er), _ptr(ei), _ptr(lq), _ptr(pq),
+                                                   _stream(self.device)), "aiqmc_local_energy_ecp")
         e = torch.complex(er, ei)
         if want_quadrature:
             return e, lq.reshape(B, self.N, self.A, ECP_NQ), pq.reshape(B, self.N, self.A, ECP_NQ)

@@ -32,7 +32,9 @@ constexpr int FUSE_REDUCE_MAX_B = 1 << 30;
 // complex_output=True local energy from the log|psi| pass (e_re = E_L = V - (lap log|psi| +
 // |grad log|psi||^2) / 2, ga = grad log|psi|) and the phase pass (gp = grad theta, lp = lap theta):
 // hamiltonian.py:110-130,  KE = -1/2 [lap log|psi| + i lap theta] - 1/2 |ga|^2 + 1/2 |gp|^2 - i ga.gp
-template <typename T>
+// ADD_IM: e_im already holds a part of the energy (the pp local energy's imaginary nonlocal part):
+// the phase terms are added to it, and to e_re, directly (no complex-minus-real difference).
+template <typename T, bool ADD_IM = false>
 __global__ __launch_bounds__(256) void k_complex_el(int B, int n3, const T* __restrict__ ga, const T* __restrict__ gp,
                                                     const T* __restrict__ lp, T* __restrict__ e_re, T* __restrict__ e_im) {
   const int b = blockIdx.x * 256 + (int)threadIdx.x;
@@ -44,7 +46,8 @@ __global__ __launch_bounds__(256) void k_complex_el(int B, int n3, const T* __re
     ap += ga[(size_t)b * n3 + k] * p;
   }
   e_re[b] += T(0.5) * pp;
-  e_im[b] = T(-0.5) * lp[b] - ap;
+  if (ADD_IM) e_im[b] += T(-0.5) * lp[b] - ap;
+  else e_im[b] = T(-0.5) * lp[b] - ap;
 }
 
 // v2 = sum(x[0..n)) ; taueff = (sqrt(1 + 2 tau a v2) - 1)/(a v2), a = 0.25  (VMCmcstep.py:11-14)
@@ -826,6 +829,18 @@ int aiqmc_local_energy(aiqmc_ctx* c, const void* pos, int32_t B, void* e_l, void
   return local_energy_pass(c, pos, B, e_l, logabs, grad, 0, stream);
 }
 
+// complex-output scratch [B][6N+1]: grad log|psi|, grad theta, lap theta
+static int ensure_cx(aiqmc_ctx* c, int B) {
+  if (c->cx_B >= B) return AIQMC_OK;
+  if (c->d_cx) (void)hipFree(c->d_cx);
+  c->d_cx = nullptr;
+  c->cx_B = 0;
+  const size_t es = c->dtype == AIQMC_F32 ? 4 : 8;
+  HIPCHK(hipMalloc(&c->d_cx, (size_t)B * (6 * c->N + 1) * es));
+  c->cx_B = B;
+  return AIQMC_OK;
+}
+
 int aiqmc_local_energy_complex(aiqmc_ctx* c, const void* pos, int32_t B, void* e_re, void* e_im, void* stream) {
   int rc = check_call(c, pos, B);
   if (rc) return rc;
@@ -834,13 +849,8 @@ int aiqmc_local_energy_complex(aiqmc_ctx* c, const void* pos, int32_t B, void* e
   HIPCHK(hipSetDevice(c->device));
   const int N = c->N;
   const size_t es = c->dtype == AIQMC_F32 ? 4 : 8;
-  if (c->cx_B < B) {
-    if (c->d_cx) (void)hipFree(c->d_cx);
-    c->d_cx = nullptr;
-    c->cx_B = 0;
-    HIPCHK(hipMalloc(&c->d_cx, (size_t)B * (6 * N + 1) * es));
-    c->cx_B = B;
-  }
+  rc = ensure_cx(c, B);
+  if (rc) return rc;
   char* gabs = (char*)c->d_cx;
   char* gph = gabs + (size_t)B * 3 * N * es;
   char* lph = gph + (size_t)B * 3 * N * es;
@@ -1291,9 +1301,24 @@ static int ecp_quadrature(aiqmc_ctx* c, const void* pos, int B, int rng_mode, co
 
 extern "C" {
 
+static int local_energy_ecp_impl(aiqmc_ctx* c, const void* pos, int32_t B, int32_t rng_mode, const void* rot,
+                                 uint64_t seed, uint64_t offset, void* e_re, void* e_im, void* logabs_q,
+                                 void* phase_q, bool cplx, void* stream);
+
 int aiqmc_local_energy_ecp(aiqmc_ctx* c, const void* pos, int32_t B, int32_t rng_mode, const void* rot,
                            uint64_t seed, uint64_t offset, void* e_re, void* e_im, void* logabs_q, void* phase_q,
                            void* stream) {
+  return local_energy_ecp_impl(c, pos, B, rng_mode, rot, seed, offset, e_re, e_im, logabs_q, phase_q, false, stream);
+}
+
+int aiqmc_local_energy_ecp_complex(aiqmc_ctx* c, const void* pos, int32_t B, int32_t rng_mode, const void* rot,
+                                   uint64_t seed, uint64_t offset, void* e_re, void* e_im, void* stream) {
+  return local_energy_ecp_impl(c, pos, B, rng_mode, rot, seed, offset, e_re, e_im, nullptr, nullptr, true, stream);
+}
+
+static int local_energy_ecp_impl(aiqmc_ctx* c, const void* pos, int32_t B, int32_t rng_mode, const void* rot,
+                                 uint64_t seed, uint64_t offset, void* e_re, void* e_im, void* logabs_q,
+                                 void* phase_q, bool cplx, void* stream) {
   int rc = check_call(c, pos, B);
   if (rc) return rc;
   if (!c->ecp_set) return fail(AIQMC_ESTATE, "aiqmc_set_ecp has not been called");
@@ -1310,7 +1335,21 @@ int aiqmc_local_energy_ecp(aiqmc_ctx* c, const void* pos, int32_t B, int32_t rng
     rc = ensure_ecp_ws(c, B, ops0);
     if (rc) return rc;
   }
-  rc = aiqmc_local_energy(c, pos, B, c->d_ecp_el, nullptr, nullptr, stream);
+  const size_t es = c->dtype == AIQMC_F32 ? 4 : 8;
+  char* gabs = nullptr;
+  if (cplx) {
+    // complex_output=True (pphamiltonian.py:84-104 = hamiltonian.py:110-130): the all-electron
+    // pass also leaves grad log|psi|, and the phase pass gives grad theta and lap theta
+    rc = ensure_cx(c, B);
+    if (rc) return rc;
+    gabs = (char*)c->d_cx;
+    rc = local_energy_pass(c, pos, B, c->d_ecp_el, nullptr, gabs, 0, stream);
+    if (rc) return rc;
+    rc = local_energy_pass(c, pos, B, gabs + (size_t)2 * B * 3 * c->N * es, nullptr, gabs + (size_t)B * 3 * c->N * es,
+                           1, stream);
+  } else {
+    rc = aiqmc_local_energy(c, pos, B, c->d_ecp_el, nullptr, nullptr, stream);
+  }
   if (rc) return rc;
   // (2)-(4) rotations, quadrature positions, log psi at the walkers and the quadrature points --
   // skipped when every nonlocal coefficient is 0 (all-electron tables, "Ne + DMC"): each
@@ -1337,6 +1376,17 @@ int aiqmc_local_energy_ecp(aiqmc_ctx* c, const void* pos, int32_t B, int32_t rng
   // (5) local pp part + nonlocal quadrature sum
   if (c->dtype == AIQMC_F32) k_ecp_energy<float><<<dim3(B), dim3(64), 0, s>>>(ea);
   else k_ecp_energy<double><<<dim3(B), dim3(64), 0, s>>>(ea);
+  if (cplx) {   // + 1/2 |grad theta|^2 - i (lap theta / 2 + grad log|psi| . grad theta)
+    const char* gph = gabs + (size_t)B * 3 * c->N * es;
+    const char* lph = gph + (size_t)B * 3 * c->N * es;
+    const dim3 g((B + 255) / 256), b(256);
+    if (c->dtype == AIQMC_F32)
+      k_complex_el<float, true><<<g, b, 0, s>>>(B, 3 * c->N, (const float*)gabs, (const float*)gph,
+                                                 (const float*)lph, (float*)e_re, (float*)e_im);
+    else
+      k_complex_el<double, true><<<g, b, 0, s>>>(B, 3 * c->N, (const double*)gabs, (const double*)gph,
+                                                  (const double*)lph, (double*)e_re, (double*)e_im);
+  }
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
 }

@@ -217,6 +217,13 @@ int aiqmc_local_energy_ecp(aiqmc_ctx* ctx, const void* pos, int32_t B, int32_t r
                            uint64_t seed, uint64_t offset, void* e_re, void* e_im, void* logabs_q,
                            void* phase_q, void* stream);
 
+/* The same with complex_output=True (pphamiltonian.local_energy(..., complex_output=True),
+ * Energy/pphamiltonian.py:84-104, whose kinetic phase branch is hamiltonian.py:110-130): the
+ * kinetic energy's phase terms + 1/2 |grad theta|^2 - i (lap theta / 2 + grad log|psi| . grad theta)
+ * are added to e_re / e_im, theta = arg psi.  Two local-energy launch pairs (log|psi|, theta). */
+int aiqmc_local_energy_ecp_complex(aiqmc_ctx* ctx, const void* pos, int32_t B, int32_t rng_mode, const void* rot,
+                                   uint64_t seed, uint64_t offset, void* e_re, void* e_im, void* stream);
+
 /* DMC T-moves (DMC/Tmoves.py:32-225, called per walker by dmc.py:79 before the
  * drift-diffusion step), in place on pos_inout [B][3N]: for every electron the
  * pp quadrature configurations of aiqmc_local_energy_ecp give the amplitudes

@@ -147,3 +147,35 @@ def test_pp_local_energy_complex_output(golden_dir):
     ref = g["e_re"] + 1j * g["e_im"] + corr
     assert np.abs(corr.imag).max() > 1e-3
     np.testing.assert_allclose(out_c.cpu().numpy(), ref, rtol=1e-8, atol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_pp_complex_output_one_call_matches_composition(dtype):
+    """aiqmc_local_energy_ecp_complex (one call: the phase terms added to the pp energy directly,
+    ADVICE r4) against the composition the drop-in used before -- pp E_L + (complex all-electron
+    E_L - real all-electron E_L) -- on 512 C-atom ccECP walkers with the same Philox rotations."""
+    from aiqmc import systems
+    from aiqmc.initial_electrons_positions.init import init_electrons
+    from aiqmc.wavefunction_Ynlm.nn import flatten_params
+    s = systems.make_system("C_ecp")
+    ctx = s.context(dtype=dtype)
+    ctx.set_params(flatten_params(s.make_network().init(3)))
+    e = systems.ccecp_tables("C_ecp")
+    ctx.set_ecp(e.rn_local, e.local_coes, e.local_exps, e.rn_non_local, e.non_local_coes, e.non_local_exps, e.list_l)
+    pos = init_electrons(5, None, s.atoms, s.charges, s.spins, 512, 1.0)[0].to("cuda", dtype).contiguous()
+    one = ctx.local_energy_ecp(pos, seed=4, offset=2, complex_output=True)
+    pp = ctx.local_energy_ecp(pos, seed=4, offset=2)
+    el_c = ctx.local_energy_complex(pos)
+    el_r, _, _ = ctx.local_energy(pos)
+    comp = pp + (el_c - el_r.to(el_c.real.dtype))
+    torch.cuda.synchronize()
+    a, b = one.cpu().numpy(), comp.cpu().numpy()
+    assert np.isfinite(a).all()
+    assert np.abs(a.imag - pp.imag.cpu().numpy()).max() > 1e-3        # the phase terms are there
+    if dtype == torch.float64:
+        np.testing.assert_allclose(a, b, rtol=1e-10, atol=1e-9)
+    else:
+        # the composition carries fl(E + x) - E rounding at the scale of |E_L| (ADVICE r4); the one
+        # call adds x itself: compare at fp32 precision relative to |E_L|
+        tol = 2e-6 * np.maximum(1.0, np.abs(el_r.double().cpu().numpy()))
+        assert (np.abs(a - b) <= 4 * tol + 1e-4 * np.abs(b)).all(), np.abs(a - b).max()

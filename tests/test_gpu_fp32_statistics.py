@@ -127,3 +127,47 @@ def test_fp32_local_energy_finite_with_a_far_electron(golden_dir):
     assert torch.isfinite(e64).all() and torch.isfinite(e32).all() and torch.isfinite(g32).all()
     np.testing.assert_allclose(l32.double().cpu().numpy(), l64.cpu().numpy(), rtol=1e-5, atol=1e-3)
     np.testing.assert_allclose(g32.double().cpu().numpy(), g64.cpu().numpy(), rtol=1e-3, atol=1e-2)
+
+
+def test_fp32_chain_on_the_init_parameters_early_iterations():
+    """The same comparison on the parameters the benchmark and the drivers use (the default
+    envelope with its signed exp(-pi ae) term, sigma = 1: ADVICE r4), over the first iterations,
+    before the outward drift that term causes dominates: per iteration, the acceptance and the
+    median E_L of the fp32 chain within 5 standard errors of the fp64 chain's, with no absolute
+    floor (standard errors of two independent samples of B walkers; the chains share their draws,
+    so this is loose but not padded)."""
+    from oracle import system
+    from aiqmc import _lib
+    name, iters = "N2", 8
+    res = {}
+    for dtype in (torch.float64, torch.float32):
+        s = system.make_system(name)
+        t = s.tables()
+        ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
+                           t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"], dtype=dtype,
+                           device=0)
+        ctx.set_params(system.flatten_params(system.init_params(np.random.default_rng(1), s)))
+        x = system.init_electrons(np.random.default_rng(0), s.atoms, s.charges, B, 1.0)
+        pos = torch.tensor(x, dtype=dtype, device="cuda").contiguous()
+        rows = []
+        for it in range(iters):
+            acc = ctx.mc_step(pos, NSTEPS, TSTEP, seed=11, offset=it * NSTEPS, count_accepts=True)
+            el, _, _ = ctx.local_energy(pos)
+            e = el.double()
+            assert torch.isfinite(e).all() and torch.isfinite(pos).all()
+            med = float(e.median())
+            mad = float((e - med).abs().median()) * 1.4826
+            rows.append((float(acc.double().sum()) / (B * s.nelectrons * NSTEPS), med, mad))
+        torch.cuda.synchronize()
+        res[dtype] = np.array(rows)
+    r64, r32 = res[torch.float64], res[torch.float32]
+    n_moves = B * 14 * NSTEPS
+    for it in range(iters):
+        p = r64[it, 0]
+        se_acc = np.sqrt(2 * p * (1 - p) / n_moves)
+        se_med = np.sqrt(2) * 1.2533 * r64[it, 2] / np.sqrt(B)
+        print(f"it {it}: acceptance {r32[it, 0]:.5f} vs {r64[it, 0]:.5f} (5 SE {5 * se_acc:.1e}); "
+              f"median E_L {r32[it, 1]:.4f} vs {r64[it, 1]:.4f} (5 SE {5 * se_med:.2e})")
+        assert abs(r32[it, 0] - r64[it, 0]) <= 5 * se_acc, (it, r32[it, 0], r64[it, 0])
+        assert abs(r32[it, 1] - r64[it, 1]) <= 5 * se_med, (it, r32[it, 1], r64[it, 1])
+    assert 0.05 < r32[:, 0].mean() < 0.999
