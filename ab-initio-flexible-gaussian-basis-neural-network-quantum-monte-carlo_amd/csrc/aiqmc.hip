@@ -902,7 +902,8 @@ int aiqmc_debug_local_energy_forward(aiqmc_ctx* c, const void* pos, int32_t B, v
 static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double tstep, int rng_mode, const void* gauss1,
                     const void* gauss2, const void* u, int st, uint64_t seed, uint64_t step, int32_t* accept_out,
                     double* dmc, hipStream_t s, AccArgs* pending = nullptr, bool defer = false,
-                    unsigned long long* tacc = nullptr, unsigned long long* tpart = nullptr, bool pvok = false) {
+                    unsigned long long* tacc = nullptr, unsigned long long* tpart = nullptr, bool pvok = false,
+                    unsigned long long* zero_next = nullptr, int nzero = 0) {
   const int N = c->N;
   if (dmc) tacc = nullptr;
   if (dmc || tacc || c->dtype != AIQMC_F32) tpart = nullptr;
@@ -1018,6 +1019,8 @@ static int mc_sweep(aiqmc_ctx* c, const ShapeOps& ops, void* pos, int B, double 
     *pending = a;
     return 0;
   }
+  a.zero = zero_next;
+  a.nzero = nzero;
   ops.accept(c->dtype, pos, a, B, s);
   if (dmc) {
     if (c->dtype == AIQMC_F32)
@@ -1062,15 +1065,22 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
   // (integer sums need fewer than TACC_MAX_CONF configurations per reduction, walker_kernel.h)
   const bool int_sums = (int64_t)B * c->N < TACC_MAX_CONF;
   if (int_sums && c->fuse_reduce && c->dtype == AIQMC_F32 && (c->fuse_reduce > 1 || B <= FUSE_REDUCE_MAX_B)) {
+    // two banks of per-sweep accumulator sets: a call sums into bank p, and its last k_accept
+    // zeroes bank 1 - p for the next call (round 5: no memset launch per call);
+    // a bank not known to be clean (new allocation, an earlier call that stopped early) is
+    // memset here
     if (c->tacc_n < nsteps) {
       if (c->d_tacc) (void)hipFree(c->d_tacc);
       c->d_tacc = nullptr;
       c->tacc_n = 0;
-      HIPCHK(hipMalloc((void**)&c->d_tacc, (size_t)2 * TACC_STRIDE * nsteps * sizeof(unsigned long long)));
+      c->tacc_clean[0] = c->tacc_clean[1] = false;
+      HIPCHK(hipMalloc((void**)&c->d_tacc, (size_t)2 * 2 * TACC_STRIDE * nsteps * sizeof(unsigned long long)));
       c->tacc_n = nsteps;
     }
-    tacc = c->d_tacc;
-    HIPCHK(hipMemsetAsync(tacc, 0, (size_t)2 * TACC_STRIDE * nsteps * sizeof(unsigned long long), s));
+    const size_t bank_words = (size_t)2 * TACC_STRIDE * c->tacc_n;
+    tacc = c->d_tacc + bank_words * c->tacc_bank;
+    if (!c->tacc_clean[c->tacc_bank]) HIPCHK(hipMemsetAsync(tacc, 0, (size_t)2 * TACC_STRIDE * nsteps * sizeof(unsigned long long), s));
+    c->tacc_clean[c->tacc_bank] = false;   // in use from here on
   }
   // unfused fp32 sweeps: per-sweep partial sums of the limdrift reductions (k_taueff_part), kept
   // until the next sweep's walker launch has read them (fused acceptance)
@@ -1086,13 +1096,22 @@ int aiqmc_mc_step(aiqmc_ctx* c, void* pos, int32_t B, int32_t nsteps, double tst
     tpart = c->d_tpart;
   }
   AccArgs pending{};
+  const int other = 1 - c->tacc_bank;
+  unsigned long long* zero_next = tacc ? c->d_tacc + (size_t)2 * TACC_STRIDE * c->tacc_n * other : nullptr;
+  const int nzero = tacc ? 2 * TACC_STRIDE * c->tacc_n : 0;
   for (int st = 0; st < nsteps; ++st) {
+    const bool last = st + 1 == nsteps;
     rc = mc_sweep(c, ops, pos, B, tstep, rng_mode, gauss1, gauss2, u, st, seed, offset + (uint64_t)st, accept_out,
-                  nullptr, s, &pending, c->fuse_accept && st + 1 < nsteps, tacc ? tacc + 2 * TACC_STRIDE * st : nullptr,
-                  tpart ? tpart + 2 * TPART_KIND * st : nullptr, st > 0);
+                  nullptr, s, &pending, c->fuse_accept && !last, tacc ? tacc + 2 * TACC_STRIDE * st : nullptr,
+                  tpart ? tpart + 2 * TPART_KIND * st : nullptr, st > 0, last ? zero_next : nullptr,
+                  last ? nzero : 0);
     if (rc) return rc;
   }
   HIPCHK(hipGetLastError());
+  if (tacc) {   // the last k_accept has zeroed the other bank: the next call uses it as it is
+    c->tacc_clean[other] = true;
+    c->tacc_bank = other;
+  }
   return AIQMC_OK;
 }
 

@@ -52,8 +52,10 @@ struct aiqmc_ctx {
   int wide_reduce = 1;                                      // unfused fp32 sweeps: k_taueff_part (0: k_taueff)
   unsigned long long* d_tpart = nullptr;                    // their per-sweep partial sums [tpart_n][2][TPART]
   int tpart_n = 0;
-  unsigned long long* d_tacc = nullptr;                     // their per-sweep accumulators [tacc_n][2]
+  unsigned long long* d_tacc = nullptr;                     // their per-sweep accumulators [2 banks][tacc_n][2]
   int tacc_n = 0;
+  int tacc_bank = 0;                                        // the bank the next mc_step call uses
+  bool tacc_clean[2] = {false, false};                      // bank zeroed (by the last k_accept of a call)
   int lap_waves = 0;                                        // waves per walker of k_walker_lap (0: by batch)
   int ncu = 256;                                            // compute units of the device
   double* d_taueff = nullptr;

@@ -27,6 +27,8 @@ __global__ __launch_bounds__(256) void k_accept(T* __restrict__ pos, AccArgs a, 
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   // limdrift factors: every lane of the (full, 256-thread) block's waves before any returns
   const T te1 = taueff_wave<T>(a.taueff, a.tacc, 0, a.tstep, a.tpart), te2 = taueff_wave<T>(a.taueff, a.tacc, 1, a.tstep, a.tpart);
+  // the next mc_step call's accumulator bank (not read by this call)
+  for (int k = t; k < a.nzero; k += gridDim.x * blockDim.x) a.zero[k] = 0ull;
   if (t >= B * N) return;
   const int b = t / N, i = t - b * N;
   T xn[3];

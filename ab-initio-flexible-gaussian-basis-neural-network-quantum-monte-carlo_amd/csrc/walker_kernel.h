@@ -207,6 +207,10 @@ struct AccArgs {
   const unsigned long long* tpart;  // [2][TPART_KIND] k_taueff_part sums of the sweep (unfused fp32), or nullptr
   double tstep;
   int32_t* count;         // [B] accepted moves (optional)
+  // k_accept only (the last sweep of aiqmc_mc_step): words of the OTHER bank of fused limdrift
+  // accumulators to zero for the next call (no memset launch per call; aiqmc.hip tacc banks)
+  unsigned long long* zero = nullptr;
+  int32_t nzero = 0;
 };
 
 // Electron i of walker b: t_pro (sum over xyz, Q6), acceptance |exp(lp_i - lp)|^2 t_pro > u.
