@@ -64,18 +64,36 @@ def clip_local_values(local_values: torch.Tensor, mean_local_values: torch.Tenso
     return diff_center, clipped - diff_center
 
 
-def _unflatten_like(template, flat: np.ndarray):
-    pos = [0]
+def _unflatten_like(template, flat):
+    """The tree of `template` with leaves cut from `flat` (numpy -> numpy leaves; a device tensor
+    -> views of it on the device, so an optimiser step never leaves the GPU)."""
+    shapes = []
+
+    def collect(tree):
+        if isinstance(tree, dict):
+            for k in sorted(tree.keys()):
+                collect(tree[k])
+        elif isinstance(tree, (list, tuple)):
+            for v in tree:
+                collect(v)
+        else:
+            shapes.append(tuple(tree.shape) if hasattr(tree, "shape") else np.shape(tree))
+    collect(template)
+    sizes = [int(np.prod(sh)) if sh else 1 for sh in shapes]
+    if isinstance(flat, torch.Tensor):
+        # one split (views) + a view per leaf; each stays a view of `flat`, which nn.bind and the
+        # optimiser recognise and use whole (no gather)
+        pieces = iter([p.view(sh) for p, sh in zip(torch.split(flat, sizes), shapes)])
+    else:
+        offs = np.cumsum([0] + sizes)
+        pieces = iter([flat[offs[i]:offs[i + 1]].reshape(sh) for i, sh in enumerate(shapes)])
 
     def build(tree):
         if isinstance(tree, dict):
             return {k: build(tree[k]) for k in sorted(tree.keys())}
         if isinstance(tree, (list, tuple)):
             return [build(v) for v in tree]
-        a = np.asarray(tree.detach().cpu() if isinstance(tree, torch.Tensor) else tree)
-        out = flat[pos[0]:pos[0] + a.size].reshape(a.shape)
-        pos[0] += a.size
-        return out
+        return next(pieces)
     return build(template)
 
 

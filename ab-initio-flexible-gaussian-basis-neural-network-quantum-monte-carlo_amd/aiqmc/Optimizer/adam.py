@@ -5,7 +5,9 @@ key) -> (params, opt_state, loss, aux)``: the energy gradient of ``evaluate_loss
 Loss.make_loss, computed on the GPU), ``constants.pmean`` of the gradient (ONE RCCL
 all-reduce of the parameter vector, adam.py:55), then the optimizer (Optimizer.optax_like).
 ``make_training_step(opt_update)`` adds the NaN rollback of adam.py:74-79.  Parameters stay a
-reference-shaped pytree (numpy leaves); the optimizer runs on the flat device vector.
+reference-shaped pytree; the optimizer runs on the flat device vector and the new leaves are
+device tensors (views of it), so a training step makes no host round trip of the parameters
+(the next bind repacks them on the device, aiqmc_set_params_device).
 """
 from __future__ import annotations
 
@@ -15,7 +17,7 @@ import numpy as np
 import torch
 
 from .. import constants
-from ..wavefunction_Ynlm.nn import flatten_params
+from ..wavefunction_Ynlm.nn import flatten_params_device
 
 
 def make_opt_update_step(evaluate_loss, optimizer):
@@ -26,11 +28,13 @@ def make_opt_update_step(evaluate_loss, optimizer):
     def opt_update(params, data, opt_state, key):
         (loss, aux), grad = vg(params, key, data)
         grad = constants.pmean(grad)
-        flat = torch.as_tensor(flatten_params(params), dtype=grad.dtype, device=grad.device)
+        flat = flatten_params_device(params, grad.device).to(grad.dtype)
         if opt_state is None:
             opt_state = optimizer.init(flat)
         updates, opt_state = optimizer.update(grad, opt_state, flat)
-        new_flat = (flat + updates).detach().cpu().to(torch.float64).numpy()
+        # the new parameters stay on the device as views of one float64 vector (the reference's
+        # params are device arrays): the next bind repacks them there (aiqmc_set_params_device)
+        new_flat = (flat + updates).detach().to(torch.float64)
         return evaluate_loss.unflatten(params, new_flat), opt_state, loss, aux
     return opt_update
 

@@ -25,7 +25,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
                         "libaiqmc_hip.so" if not _VARIANT else f"libaiqmc_hip_{_VARIANT}.so")
 
 EXPORTED_SYMBOLS = (
-    "aiqmc_create", "aiqmc_destroy", "aiqmc_param_count", "aiqmc_set_params",
+    "aiqmc_create", "aiqmc_destroy", "aiqmc_param_count", "aiqmc_set_params", "aiqmc_set_params_device",
     "aiqmc_logpsi", "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_local_energy_complex", "aiqmc_mc_step",
     "aiqmc_workspace_bytes", "aiqmc_last_error", "aiqmc_supported_shapes",
     "aiqmc_profile_enable", "aiqmc_profile_read", "aiqmc_debug_logpsi_grad_forward",
@@ -114,6 +114,7 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_workspace_bytes.argtypes = [vp]
     lib.aiqmc_workspace_bytes.restype = i64
     lib.aiqmc_set_params.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i64, vp]
+    lib.aiqmc_set_params_device.argtypes = [vp, vp, i64, vp]
     lib.aiqmc_logpsi.argtypes = [vp, vp, i32, vp, vp, vp]
     lib.aiqmc_logpsi_grad.argtypes = [vp, vp, i32, vp, vp, vp]
     lib.aiqmc_orbitals.argtypes = [vp, vp, i32, vp, vp, vp, vp]
@@ -166,7 +167,7 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_energy_stats_final.argtypes = [vp, vp]
     lib.aiqmc_last_error.restype = ctypes.c_char_p
     lib.aiqmc_supported_shapes.restype = ctypes.c_char_p
-    for name in ("aiqmc_create", "aiqmc_destroy", "aiqmc_set_params", "aiqmc_logpsi",
+    for name in ("aiqmc_create", "aiqmc_destroy", "aiqmc_set_params", "aiqmc_set_params_device", "aiqmc_logpsi",
                  "aiqmc_logpsi_grad", "aiqmc_local_energy", "aiqmc_local_energy_complex", "aiqmc_mc_step", "aiqmc_profile_enable",
                  "aiqmc_profile_read", "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_local_energy_ecp_complex",
                  "aiqmc_logpsi_param_grad",
@@ -326,6 +327,19 @@ class Context:
         with torch.cuda.device(self.device):
             check(self._lib.aiqmc_set_params(self._h, flat.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
                                              flat.size, _stream(self.device)), "aiqmc_set_params")
+
+    def set_params_device(self, flat: torch.Tensor):
+        """Canonical parameters already on this context's device (float64, tree_flatten order):
+        repacked into the kernel layout on the device, stream-ordered (no host copy, no sync)."""
+        if not (isinstance(flat, torch.Tensor) and flat.is_cuda and flat.dtype == torch.float64
+                and flat.is_contiguous() and flat.device == self.device):
+            raise ValueError("set_params_device needs a contiguous float64 tensor on the context's device")
+        if flat.numel() != self.nparams:
+            raise ValueError(f"expected {self.nparams} parameters, got {flat.numel()}")
+        with torch.cuda.device(self.device):
+            check(self._lib.aiqmc_set_params_device(self._h, _ptr(flat), flat.numel(), _stream(self.device)),
+                  "aiqmc_set_params_device")
+        self._flat_keep = flat   # the repack reads it later on the stream: keep it alive until then
 
     def logpsi(self, pos: torch.Tensor, with_phase: bool = True):
         p = self._pos(pos)

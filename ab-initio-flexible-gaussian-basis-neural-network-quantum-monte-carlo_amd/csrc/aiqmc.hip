@@ -641,7 +641,7 @@ int aiqmc_destroy(aiqmc_ctx* c) {
   if (c->d_tm_scr) (void)hipFree(c->d_tm_scr);
   if (c->d_dscr) (void)hipFree(c->d_dscr);
   if (c->d_ecp_tab) (void)hipFree(c->d_ecp_tab);
-  void* pgp[] = {c->d_gmap, c->d_wnorm, c->d_pg, c->d_pgr};
+  void* pgp[] = {c->d_gmap, c->d_wnorm, c->d_pg, c->d_pgr, c->d_pk_op, c->d_pk_src, c->d_pk_cval};
   for (void* p : pgp)
     if (p) (void)hipFree(p);
   if (c->d_wcp) (void)hipFree(c->d_wcp);
@@ -696,6 +696,107 @@ int aiqmc_set_params(aiqmc_ctx* c, const double* flat, int64_t n, void* stream) 
   if (!c->d_wnorm) HIPCHK(hipMalloc((void**)&c->d_wnorm, NYW * sizeof(double)));
   HIPCHK(hipMemcpyAsync(c->d_wnorm, wn, sizeof(wn), hipMemcpyHostToDevice, s));
   HIPCHK(hipStreamSynchronize(s));
+  c->params_set = true;
+  return AIQMC_OK;
+}
+
+// Device repack of canonical parameters (fp64, device) into the kernel layout: the program is
+// read off pack_params itself by two probes (flat_j = j + 1 and 2 (j + 1)): an entry equal in both is
+// a constant of the system (atoms, charges, Jastrow cusps, V_nn), one that doubles is a copy of
+// canonical j, and the W_y block is the row-normalised y coefficients (nn.py:449-451).  Per entry
+// the arithmetic is pack_params' (double, same summation order for the row norms), so the kernel
+// layout is bitwise the host upload's.
+}  // extern "C"
+template <typename T>
+__global__ __launch_bounds__(256) void k_pack_params(const double* __restrict__ flat, const int* __restrict__ op,
+                                                     const int* __restrict__ src, const double* __restrict__ cval,
+                                                     int n, int wy_off, int wy_src0, int N, T* __restrict__ prm,
+                                                     double* __restrict__ wnorm) {
+  const int k = blockIdx.x * 256 + (int)threadIdx.x;
+  if (k >= n) return;
+  const int o = op[k];
+  double v;
+  if (o == 0) {
+    v = cval[k];
+  } else if (o == 1) {
+    v = flat[src[k]];
+  } else {
+    const int m = (k - wy_off) / N;
+    double a = 0.0;
+    for (int col = 0; col < N; ++col) {
+      // no fused multiply-add: the host's pack_params rounds the product and the sum apart
+#pragma clang fp contract(off)
+      const double w = flat[wy_src0 + m * N + col];
+      a += w * w;
+    }
+    const double nrm = sqrt(a);
+    v = flat[src[k]] / nrm;
+    if (k - wy_off == m * N) wnorm[m] = nrm;
+  }
+  prm[k] = (T)v;
+}
+
+extern "C" {
+static int build_pack_program(aiqmc_ctx* c, const ShapeOps& ops) {
+  const int64_t n = c->ncanon;
+  std::vector<double> fa(n), fb(n), la, lb;
+  for (int64_t j = 0; j < n; ++j) {
+    fa[j] = double(j + 1);
+    fb[j] = 2.0 * double(j + 1);
+  }
+  ops.pack(c, fa.data(), la);
+  ops.pack(c, fb.data(), lb);
+  const int64_t nk = (int64_t)la.size();
+  std::vector<int> op(nk, 0), src(nk, 0);
+  std::vector<double> cval(nk, 0.0);
+  const int wy_off = ops.wy_off, ny = NYW * c->N;
+  const int64_t wy_src0 = n - ny;
+  for (int64_t k = 0; k < nk; ++k) {
+    if (k >= wy_off && k < wy_off + ny) {
+      op[k] = 2;
+      src[k] = (int)(wy_src0 + (k - wy_off));
+    } else if (la[k] == lb[k]) {
+      op[k] = 0;
+      cval[k] = la[k];
+    } else if (lb[k] == 2.0 * la[k] && la[k] >= 1.0 && la[k] <= double(n) && la[k] == std::floor(la[k])) {
+      op[k] = 1;
+      src[k] = (int)la[k] - 1;
+    } else {
+      return fail(AIQMC_EINVAL, "internal: kernel-layout entry " + std::to_string(k) + " is neither a copy nor a constant");
+    }
+  }
+  HIPCHK(hipMalloc((void**)&c->d_pk_op, nk * sizeof(int)));
+  HIPCHK(hipMalloc((void**)&c->d_pk_src, nk * sizeof(int)));
+  HIPCHK(hipMalloc((void**)&c->d_pk_cval, nk * sizeof(double)));
+  HIPCHK(hipMemcpy(c->d_pk_op, op.data(), nk * sizeof(int), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c->d_pk_src, src.data(), nk * sizeof(int), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c->d_pk_cval, cval.data(), nk * sizeof(double), hipMemcpyHostToDevice));
+  return AIQMC_OK;
+}
+
+int aiqmc_set_params_device(aiqmc_ctx* c, const double* flat, int64_t n, void* stream) {
+  if (!c || !flat) return fail(AIQMC_EINVAL, "null argument");
+  if (n != c->ncanon)
+    return fail(AIQMC_EINVAL, "expected " + std::to_string(c->ncanon) + " parameters, got " + std::to_string(n));
+  HIPCHK(hipSetDevice(c->device));
+  ShapeOps ops;
+  shape_ops(c->N, c->A, &ops);
+  if (!c->d_pk_op) {
+    int rc = build_pack_program(c, ops);
+    if (rc) return rc;
+  }
+  if (!c->d_wnorm) HIPCHK(hipMalloc((void**)&c->d_wnorm, NYW * sizeof(double)));
+  const int nk = (int)ops.nprm;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g((nk + 255) / 256), b(256);
+  const int wy_src0 = (int)(n - NYW * c->N);
+  if (c->dtype == AIQMC_F32)
+    k_pack_params<float><<<g, b, 0, s>>>(flat, c->d_pk_op, c->d_pk_src, c->d_pk_cval, nk, ops.wy_off, wy_src0, c->N,
+                                         (float*)c->d_prm, c->d_wnorm);
+  else
+    k_pack_params<double><<<g, b, 0, s>>>(flat, c->d_pk_op, c->d_pk_src, c->d_pk_cval, nk, ops.wy_off, wy_src0,
+                                          c->N, (double*)c->d_prm, c->d_wnorm);
+  HIPCHK(hipGetLastError());
   c->params_set = true;
   return AIQMC_OK;
 }

@@ -75,6 +75,12 @@ struct aiqmc_ctx {
   // parameter gradients (aiqmc_logpsi_param_grad, walker_pgrad.h)
   int* d_gmap = nullptr;            // [ncanon]
   double* d_wnorm = nullptr;        // [6] |W_y row| of the current parameters
+  // device repack program of aiqmc_set_params_device (built once per context from pack_params):
+  // per kernel-layout entry an op (0 constant, 1 copy, 2 row-normalised y coefficient), its
+  // canonical source index and its constant value
+  int* d_pk_op = nullptr;
+  int* d_pk_src = nullptr;
+  double* d_pk_cval = nullptr;
   void* d_pg = nullptr;             // [pg_B][nkern] per-walker kernel-layout gradients
   void* d_pgr = nullptr;            // [nkern] weighted sum
   int pg_B = 0;

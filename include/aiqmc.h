@@ -79,6 +79,12 @@ int64_t aiqmc_param_count(const aiqmc_ctx* ctx);
 /* flat: HOST pointer, `n` doubles in tree_flatten order. Synchronous upload. */
 int aiqmc_set_params(aiqmc_ctx* ctx, const double* flat, int64_t n, void* stream);
 
+/* flat: DEVICE pointer (this context's device), `n` doubles in tree_flatten order, repacked into
+ * the kernel layout on `stream` (stream-ordered, no host synchronisation): the parameters of an
+ * optimiser step that stays on the device (the reference's params are device arrays updated by
+ * optax / kfac inside pmap, adam.py:49-59).  The kernel layout equals aiqmc_set_params' bitwise. */
+int aiqmc_set_params_device(aiqmc_ctx* ctx, const double* flat, int64_t n, void* stream);
+
 /* pos[B*3N] -> logabs[B], phase[B] (phase may be NULL). */
 int aiqmc_logpsi(aiqmc_ctx* ctx, const void* pos, int32_t B, void* logabs, void* phase,
                  void* stream);

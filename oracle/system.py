@@ -185,8 +185,8 @@ def tree_flatten(tree) -> List[np.ndarray]:
     elif isinstance(tree, (list, tuple)):
         for v in tree:
             out.extend(tree_flatten(v))
-    else:
-        out.append(np.asarray(tree, dtype=np.float64))
+    else:   # numpy / python leaves, or device tensors (a drop-in optimiser step keeps them on the GPU)
+        out.append(np.asarray(tree.detach().cpu() if hasattr(tree, "detach") else tree, dtype=np.float64))
     return out
 
 

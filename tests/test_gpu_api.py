@@ -204,3 +204,71 @@ def test_energy_stats_rejects_empty_and_host():
         _lib.energy_stats(torch.empty(0, device="cuda"))
     with pytest.raises(ValueError):
         _lib.energy_stats(torch.ones(4))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["N2", "Be", "C2_ecp", "H2"])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_set_params_device_equals_host_upload(name, dtype):
+    """aiqmc_set_params_device (canonical parameters repacked on the device, stream-ordered) gives
+    the same kernel layout as the host upload: log|psi|, its gradient, E_L and the parameter
+    gradient (which also reads the W_y row norms) bitwise equal on the same walkers."""
+    from aiqmc import systems
+    from aiqmc.initial_electrons_positions.init import init_electrons
+    from aiqmc.wavefunction_Ynlm.nn import flatten_params
+    s = systems.make_system(name)
+    flat = flatten_params(s.make_network().init(7))
+    pos = init_electrons(3, None, s.atoms, s.charges, s.spins, 64, 1.0)[0].to("cuda", dtype).contiguous()
+    outs = []
+    for mode in ("host", "device"):
+        ctx = s.context(dtype=dtype)
+        if mode == "host":
+            ctx.set_params(flat)
+        else:
+            ctx.set_params_device(torch.tensor(flat, dtype=torch.float64, device="cuda"))
+        la, g = ctx.logpsi_grad(pos)
+        e, _, _ = ctx.local_energy(pos)
+        pg = ctx.logpsi_param_grad(pos)
+        torch.cuda.synchronize()
+        outs.append([t.cpu() for t in (la, g, e, pg)])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_adam_steps_stay_on_the_device():
+    """The drop-in Adam step returns device-tensor leaves (views of one float64 vector) and the
+    next bind repacks them on the device: two steps through that path equal two steps with the
+    parameters round-tripped through the host (numpy leaves) -- the same optimiser arithmetic."""
+    from aiqmc.Energy import hamiltonian as H
+    from aiqmc.Loss import loss as L
+    from aiqmc.Optimizer import adam, optax_like as optax
+    from aiqmc.VMC import VMCmcstep
+    from aiqmc.wavefunction_Ynlm.nn import flatten_params
+    s, network, params, data = _setup(B=64)
+    local_energy = H.local_energy(f=network.apply, charges=s.charges, nspins=s.spins, use_scan=False)
+    runs = []
+    for host_roundtrip in (False, True):
+        ev = L.make_loss(network=network.apply, local_energy=local_energy, clip_local_energy=5.0,
+                         clip_from_median=False, center_at_clipped_energy=True, complex_output=True)
+        opt = optax.chain(optax.scale_by_adam(b1=0.9, b2=0.999, eps=1e-8, eps_root=0.0),
+                          optax.scale_by_schedule(lambda t: 0.05 / (1.0 + 0.01 * t)), optax.scale(-1.))
+        step = adam.make_training_step(adam.make_opt_update_step(ev, opt))
+        p, st, d = params, None, data
+        for t in range(2):
+            d, p, st, loss_v, aux = step(d, p, st, t)
+            if host_roundtrip:
+                p = L._unflatten_like(p, flatten_params(p))     # numpy leaves: the host upload path
+            else:
+                leaves = [l for l in _leaves(p)]
+                assert all(isinstance(l, torch.Tensor) and l.is_cuda for l in leaves)
+        runs.append(flatten_params(p))
+    np.testing.assert_array_equal(runs[0], runs[1])
+
+
+def _leaves(tree):
+    if isinstance(tree, dict):
+        return [x for k in sorted(tree) for x in _leaves(tree[k])]
+    if isinstance(tree, (list, tuple)):
+        return [x for v in tree for x in _leaves(v)]
+    return [tree]
