@@ -27,6 +27,11 @@ import torch
 from .. import constants
 
 
+# diagnostics: False routes every step through the torch statistics path (the A/B of the fused
+# single-rank path, tools/adam_only.py AIQMC_LOSS_TORCH=1)
+FUSED_ONE_RANK = True
+
+
 @dataclasses.dataclass
 class AuxiliaryLossData:
     """loss.py:28-41."""
@@ -117,8 +122,40 @@ def make_loss(network, local_energy, clip_local_energy: float = 0.0, clip_from_m
         return loss, AuxiliaryLossData(variance=variance, local_energy=e_l, clipped_energy=e_l,
                                        local_energy_mat=e_mat)
 
+    def value_and_grad_fused(params, data, e_l, e_mat):
+        """One rank, device energies: the statistics, the clipping and the two weight vectors in
+        one launch (aiqmc_loss_weights, the same formulas in double), then the parameter
+        gradients -- no host synchronisation and ~25 small torch launches fewer per step."""
+        from .. import _lib
+        cplx = torch.is_complex(e_l)
+        if cplx and not complex_output and bool(torch.any(e_l.imag != 0)):
+            raise NotImplementedError("complex local energies need complex_output=True (loss.py:256-265)")
+        phase = cplx and complex_output
+        B = e_l.numel()
+        wscale = (2.0 if complex_output else 1.0) / B
+        w, wp, clipped, st = _lib.loss_weights(e_l, clip_local_energy, center_at_clipped_energy, wscale, phase)
+        rdt = e_l.real.dtype if cplx else e_l.dtype
+        loss = torch.complex(st[0], st[1]).to(e_l.dtype) if cplx else st[0].to(rdt)
+        variance = st[2].to(rdt)
+        pos = data.positions if isinstance(data.positions, torch.Tensor) else torch.as_tensor(
+            np.asarray(data.positions))
+        dtype = pos.dtype if pos.dtype in (torch.float32, torch.float64) else torch.float32
+        ctx = net.bind(params, data.atoms, dtype)
+        g = ctx.logpsi_param_grad(pos.reshape(B, -1), weights=w.to(ctx.device, dtype))
+        if phase:
+            g = g + ctx.phase_param_grad(pos.reshape(B, -1), weights=wp.to(ctx.device, dtype))
+        aux = AuxiliaryLossData(variance=variance, local_energy=e_l, clipped_energy=clipped, local_energy_mat=e_mat)
+        return (loss, aux), g
+
     def value_and_grad(params, key, data):
-        e_l, e_mat, loss, variance = _energy(params, key, data)
+        e_l, e_mat = local_energy(params, key, data)
+        if (FUSED_ONE_RANK and not constants._active() and not clip_from_median and isinstance(e_l, torch.Tensor)
+                and e_l.is_cuda
+                and (e_l.real if torch.is_complex(e_l) else e_l).dtype in (torch.float32, torch.float64)):
+            return value_and_grad_fused(params, data, e_l, e_mat)
+        loss = constants.pmean(torch.mean(e_l))
+        d = e_l - loss
+        variance = constants.pmean(torch.mean(d * torch.conj(d))).real
         cplx = torch.is_complex(e_l) and bool(torch.any(e_l.imag != 0))
         if cplx and not complex_output:
             raise NotImplementedError("complex local energies need complex_output=True (loss.py:256-265)")

@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves", "aiqmc_phase_param_grad",
     "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals", "aiqmc_debug_set_ablate", "aiqmc_debug_set_fuse_accept", "aiqmc_debug_set_walker_pivots", "aiqmc_debug_set_packed_walkers", "aiqmc_debug_set_lap_waves",
     "aiqmc_debug_set_fuse_reduce", "aiqmc_energy_stats", "aiqmc_energy_stats_final",
-    "aiqmc_debug_limdrift_factor", "aiqmc_debug_launch_lds",
+    "aiqmc_debug_limdrift_factor", "aiqmc_debug_launch_lds", "aiqmc_loss_weights",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -130,6 +130,9 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_debug_set_ablate.restype = ctypes.c_int
     lib.aiqmc_debug_set_fuse_accept.argtypes = [vp, i32]
     lib.aiqmc_debug_set_fuse_accept.restype = ctypes.c_int
+    lib.aiqmc_loss_weights.argtypes = [vp, vp, i32, i64, ctypes.c_double, i32, ctypes.c_double, vp, vp, vp, vp, vp,
+                                       vp]
+    lib.aiqmc_loss_weights.restype = ctypes.c_int
     lib.aiqmc_debug_launch_lds.argtypes = [i32, i32, i32, i32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
     lib.aiqmc_debug_launch_lds.restype = ctypes.c_int
     lib.aiqmc_debug_set_walker_pivots.argtypes = [vp, i32]
@@ -227,6 +230,31 @@ def energy_stats(e_l: torch.Tensor, finalize: bool = True) -> torch.Tensor:
     check(load().aiqmc_energy_stats(_ptr(e), dt, e.numel(), _ptr(out), 1 if finalize else 0, _stream(e.device)),
           "aiqmc_energy_stats")
     return out
+
+
+def loss_weights(e_l: torch.Tensor, clip_scale: float, center_at_clipped: bool, wscale: float,
+                 want_imag: bool):
+    """aiqmc_loss_weights (one rank): for device local energies (real, or complex: re/im), the
+    energy-gradient weights w_re = wscale Re(diff), w_im = wscale Im(diff + aux) (None unless
+    want_imag), aux.clipped_energy (same dtype as e_l) and float64 device stats
+    [Re mean, Im mean, variance, Re centre, Im centre]."""
+    cplx = torch.is_complex(e_l)
+    er = (e_l.real if cplx else e_l).contiguous().reshape(-1)
+    if not er.is_cuda or er.dtype not in (torch.float32, torch.float64):
+        raise ValueError("loss_weights: float32/float64 (or complex64/128) device energies are required")
+    ei = e_l.imag.contiguous().reshape(-1) if cplx else None
+    n = er.numel()
+    wr = torch.empty_like(er)
+    wi = torch.empty_like(er) if want_imag else None
+    cr = torch.empty_like(er)
+    ci = torch.empty_like(er) if cplx else None
+    st = torch.empty(5, dtype=torch.float64, device=er.device)
+    dt = AIQMC_F32 if er.dtype == torch.float32 else AIQMC_F64
+    check(load().aiqmc_loss_weights(_ptr(er), _ptr(ei), dt, n, float(clip_scale), 1 if center_at_clipped else 0,
+                                    float(wscale), _ptr(wr), _ptr(wi), _ptr(cr), _ptr(ci), _ptr(st),
+                                    _stream(er.device)), "aiqmc_loss_weights")
+    clipped = torch.complex(cr, ci) if cplx else cr
+    return wr, wi, clipped.reshape(e_l.shape), st
 
 
 def energy_stats_final(out: torch.Tensor) -> torch.Tensor:

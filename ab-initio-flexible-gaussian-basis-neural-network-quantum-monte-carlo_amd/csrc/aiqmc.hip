@@ -261,6 +261,93 @@ __global__ void k_energy_stats_final(double* out) {
   if (threadIdx.x == 0) energy_stats_final(out);
 }
 
+// The energy-gradient weights of make_loss on one rank (Loss/loss.py:73-135 clipping, :206-208
+// statistics, :256-265 tangent), one workgroup, every sum in double and in a fixed order:
+//   m = mean(e) (the loss), variance = mean |e - m|^2;
+//   clip (scale > 0, centre m; clip_from_median = False): tv = mean |x - c| per component,
+//     clipped x = clamp(x, c - scale tv, c + scale tv); centre of the differences
+//     dc = mean(clipped) (center_at_clipped) or m; diff = clipped - dc; aux = dc;
+//   no clip: diff = e - m, aux = e (total_energy's clipped_energy, kept as written);
+//   w_re = wscale Re diff,  w_im = wscale Im(diff + aux)  (the d log|psi| and d phase weights);
+//   clipped_out = dc + diff (aux.clipped_energy; dc = m without clipping);
+//   stats = [m_re, m_im, variance, dc_re, dc_im].
+// e_im / w_im / clipped_im may be null (real local energies).  Replaces ~25 small torch launches
+// per training step (and the host sync of the complex check) on the single-rank path.
+template <typename T>
+__global__ __launch_bounds__(1024) void k_loss_weights(const T* __restrict__ er, const T* __restrict__ ei, int64_t n,
+                                                       double clip, int center_at_clipped, double wscale,
+                                                       T* __restrict__ wr, T* __restrict__ wi, T* __restrict__ cr,
+                                                       T* __restrict__ ci, double* __restrict__ stats) {
+  __shared__ double red[16];
+  const double nn = (double)n;
+  const bool cplx = ei != nullptr;
+  double a = 0.0, b = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    a += (double)er[i];
+    if (cplx) b += (double)ei[i];
+  }
+  const double mr = block_sum_1024(a, red) / nn;
+  const double mi = cplx ? block_sum_1024(b, red) / nn : 0.0;
+  double q = 0.0, tr = 0.0, ti = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const double dr = (double)er[i] - mr, di = cplx ? (double)ei[i] - mi : 0.0;
+    q += dr * dr + di * di;
+    tr += fabs(dr);
+    ti += fabs(di);
+  }
+  const double var = block_sum_1024(q, red) / nn;
+  const bool clipping = clip > 0.0;
+  double lor = 0.0, hir = 0.0, loi = 0.0, hii = 0.0, dcr = mr, dci = mi;
+  if (clipping) {
+    const double tvr = block_sum_1024(tr, red) / nn;
+    const double tvi = cplx ? block_sum_1024(ti, red) / nn : 0.0;
+    lor = mr - clip * tvr;
+    hir = mr + clip * tvr;
+    loi = mi - clip * tvi;
+    hii = mi + clip * tvi;
+    if (center_at_clipped) {
+      double sr = 0.0, si = 0.0;
+      for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const double x = (double)er[i];
+        sr += x < lor ? lor : (x > hir ? hir : x);
+        if (cplx) {
+          const double y = (double)ei[i];
+          si += y < loi ? loi : (y > hii ? hii : y);
+        }
+      }
+      dcr = block_sum_1024(sr, red) / nn;
+      dci = cplx ? block_sum_1024(si, red) / nn : 0.0;
+    }
+  }
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const double x = (double)er[i], y = cplx ? (double)ei[i] : 0.0;
+    double fr, fi, ar, ai;
+    if (clipping) {
+      const double xc = x < lor ? lor : (x > hir ? hir : x), yc = y < loi ? loi : (y > hii ? hii : y);
+      fr = xc - dcr;
+      fi = yc - dci;
+      ar = dcr;
+      ai = dci;
+    } else {
+      fr = x - mr;
+      fi = y - mi;
+      ar = x;
+      ai = y;
+    }
+    wr[i] = (T)(wscale * fr);
+    if (wi) wi[i] = (T)(wscale * (fi + ai));
+    if (cr) cr[i] = (T)(dcr + fr);   // centre + diff (= e without clipping: dc = m)
+    if (ci) ci[i] = (T)(dci + fi);
+  }
+  if (threadIdx.x == 0) {
+    stats[0] = mr;
+    stats[1] = mi;
+    stats[2] = var;
+    stats[3] = dcr;
+    stats[4] = dci;
+  }
+}
+
 // out[i] = grad[i] * taueff (limdrift, VMCmcstep.py:11-14 / drift_diffusion.py:9-12)
 template <typename T>
 __global__ __launch_bounds__(256) void k_scale_grad(const T* __restrict__ g, const double* __restrict__ taueff, int n,
@@ -1707,6 +1794,25 @@ int aiqmc_energy_stats(const void* e_l, int32_t dtype, int64_t n, double* out, i
     k_energy_stats<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)e_l, n, out, finalize != 0);
   else
     k_energy_stats<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)e_l, n, out, finalize != 0);
+  HIPCHK(hipGetLastError());
+  return AIQMC_OK;
+}
+
+int aiqmc_loss_weights(const void* e_re, const void* e_im, int32_t dtype, int64_t n, double clip_scale,
+                       int32_t center_at_clipped, double wscale, void* w_re, void* w_im, void* clipped_re,
+                       void* clipped_im, double* stats, void* stream) {
+  if (n <= 0) return fail(AIQMC_EINVAL, "empty batch");
+  if (!e_re || !w_re || !stats) return fail(AIQMC_EINVAL, "null argument");
+  if (dtype != AIQMC_F32 && dtype != AIQMC_F64) return fail(AIQMC_EINVAL, "dtype must be AIQMC_F32 or AIQMC_F64");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == AIQMC_F32)
+    k_loss_weights<float><<<dim3(1), dim3(1024), 0, s>>>((const float*)e_re, (const float*)e_im, n, clip_scale,
+                                                         center_at_clipped, wscale, (float*)w_re, (float*)w_im,
+                                                         (float*)clipped_re, (float*)clipped_im, stats);
+  else
+    k_loss_weights<double><<<dim3(1), dim3(1024), 0, s>>>((const double*)e_re, (const double*)e_im, n, clip_scale,
+                                                          center_at_clipped, wscale, (double*)w_re, (double*)w_im,
+                                                          (double*)clipped_re, (double*)clipped_im, stats);
   HIPCHK(hipGetLastError());
   return AIQMC_OK;
 }

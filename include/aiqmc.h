@@ -254,6 +254,20 @@ int aiqmc_dmc_tmoves(aiqmc_ctx* ctx, void* pos_inout, int32_t B, double tstep, i
 int aiqmc_energy_stats(const void* e_l, int32_t dtype, int64_t n, double* out, int32_t finalize, void* stream);
 int aiqmc_energy_stats_final(double* out, void* stream);
 
+/* The energy-gradient weights of make_loss on ONE rank (Loss/loss.py:73-135 clipping with the
+ * mean as centre, :206-208 statistics, :256-265 tangent weights), one launch: for local energies
+ * e = e_re + i e_im (e_im NULL: real) of n walkers,
+ *   stats[0..4] = [Re mean, Im mean, variance mean|e - mean|^2, Re centre, Im centre],
+ *   w_re[b] = wscale Re(diff_b),  w_im[b] = wscale Im(diff_b + aux_b)  (w_im may be NULL),
+ *   clipped_re/im[b] = aux.clipped_energy (may be NULL),
+ * with clip_scale > 0: total-variation window around the mean per component, diff = clipped -
+ * centre, centre = mean(clipped) (center_at_clipped) or the mean, aux = centre; clip_scale <= 0:
+ * diff = e - mean, aux = e.  Sums in double, fixed order.  (Several ranks: the statistics need
+ * all-reduces between the stages; the Python layer keeps its torch path there.) */
+int aiqmc_loss_weights(const void* e_re, const void* e_im, int32_t dtype, int64_t n, double clip_scale,
+                       int32_t center_at_clipped, double wscale, void* w_re, void* w_im, void* clipped_re,
+                       void* clipped_im, double* stats, void* stream);
+
 /* Optional HIP-event timing of the hot kernels, recorded on the caller's
  * stream around each launch while enabled.  Slots: 0 = proposal
  * value+gradient launches of aiqmc_mc_step, 1 = walker gradient launches of

@@ -272,3 +272,50 @@ def _leaves(tree):
     if isinstance(tree, (list, tuple)):
         return [x for v in tree for x in _leaves(v)]
     return [tree]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("complex_e", [False, True])
+@pytest.mark.parametrize("clip,center", [(5.0, True), (5.0, False), (0.0, True)])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_fused_loss_weights_match_torch_path(complex_e, clip, center, dtype):
+    """aiqmc_loss_weights (one launch: statistics, total-variation clipping, the two weight
+    vectors; Loss/loss.py:73-135, 206-208, 256-265) against the same formulas in torch float64
+    on heavy-tailed energies (outliers so the clipping window bites)."""
+    from aiqmc import _lib
+    g = torch.Generator().manual_seed(11)
+    B = 3001
+    re = torch.randn(B, generator=g, dtype=torch.float64) * 2 - 10
+    re[::97] *= 40.0
+    im = torch.randn(B, generator=g, dtype=torch.float64) * 0.3
+    im[::53] *= 30.0
+    e64 = torch.complex(re, im) if complex_e else re
+    cdt = {torch.float32: torch.complex64, torch.float64: torch.complex128}[dtype]
+    e = (e64.to(cdt) if complex_e else e64.to(dtype)).cuda()
+    wscale = 2.0 / B
+    w, wp, clipped, st = _lib.loss_weights(e, clip, center, wscale, complex_e)
+    # reference (torch path of make_loss, in float64 on the float-rounded energies)
+    x = e.cpu().to(torch.complex128 if complex_e else torch.float64)
+    m = x.mean()
+    var = ((x - m) * (x - m).conj()).mean().real
+    if clip > 0:
+        def cl(v, c):
+            tv = (v - c).abs().mean()
+            return torch.clamp(v, c - clip * tv, c + clip * tv)
+        if complex_e:
+            cx = torch.complex(cl(x.real, m.real), cl(x.imag, m.imag))
+        else:
+            cx = cl(x, m)
+        dc = cx.mean() if center else m
+        diff = cx - dc
+        aux = dc
+    else:
+        dc, diff, aux = m, x - m, x
+    tol = dict(rtol=1e-11, atol=1e-11) if dtype == torch.float64 else dict(rtol=2e-6, atol=2e-6)
+    np.testing.assert_allclose(w.cpu().double().numpy(), (wscale * diff.real).numpy(), **tol)
+    if complex_e:
+        np.testing.assert_allclose(wp.cpu().double().numpy(), (wscale * (diff + aux).imag).numpy(), **tol)
+        np.testing.assert_allclose(clipped.cpu().to(torch.complex128).numpy(), (dc + diff).numpy(), rtol=1e-6)
+    np.testing.assert_allclose(st[0].item(), float(m.real), rtol=1e-12)
+    np.testing.assert_allclose(st[2].item(), float(var), rtol=1e-12)
+    np.testing.assert_allclose(st[3].item(), float(dc.real), rtol=1e-12)

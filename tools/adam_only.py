@@ -2,7 +2,8 @@
 AIQMC_DIGEST_BIND=1: AINet.bind re-flattens and digests the parameters on every call (the
 behaviour before the identity/version key), for an A/B in one process tree.
 AIQMC_HOST_PARAMS=1: the optimiser's parameters round-trip through the host every step (round 4).
-AIQMC_PP=1: the C-atom ccECP Adam side measurement instead (complex E_L)."""
+AIQMC_PP=1: the C-atom ccECP Adam side measurement instead (complex E_L).
+AIQMC_LOSS_TORCH=1: the energy statistics / clipping / weights in torch ops (no fused launch)."""
 import hashlib, json, os, sys
 import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -22,6 +23,9 @@ if os.environ.get("AIQMC_DIGEST_BIND"):
             self._loaded[k] = digest
         return ctx
     nn.AINet.bind = bind
+if os.environ.get("AIQMC_LOSS_TORCH"):
+    from aiqmc.Loss import loss as _L0
+    _L0.FUSED_ONE_RANK = False
 if os.environ.get("AIQMC_HOST_PARAMS"):
     # the round-4 behaviour: the optimiser's new parameters copied to the host (numpy leaves) and
     # uploaded again by the next bind, for an A/B against the device-resident step
