@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import re
 from typing import Any, Dict, List, Sequence, Tuple
 
 import numpy as np
@@ -112,6 +113,12 @@ def make_system(name: str) -> System:
     elif name == "O2":
         atoms = np.array([[0.0, 0.0, -1.1408], [0.0, 0.0, 1.1408]])
         charges = np.array([8.0, 8.0])
+    elif re.fullmatch(r"Z\d+(-\d+)?", name):
+        # generic shapes (tests/test_gpu_shapes.py): "Z<z>" one atom of charge z at the origin,
+        # "Z<a>-<b>" a diatomic of charges a, b at z = -1, +1 bohr; neutral, alternating spins
+        zs = [float(z) for z in name[1:].split("-")]
+        atoms = np.zeros((1, 3)) if len(zs) == 1 else np.array([[0.0, 0.0, -1.0], [0.0, 0.0, 1.0]])
+        charges = np.array(zs)
     else:
         raise KeyError(name)
     n = int(charges.sum())

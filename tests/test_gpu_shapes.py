@@ -1,0 +1,119 @@
+"""Every built (nelectrons, natoms) shape against the float64 oracle (VERDICT r4 missing #2: the
+reference network is generic in nelectrons / natoms / nspins, nn.py:511-526).
+
+The library instantiates its kernels for 2 <= N <= 16 (the Gauss-Jordan's 64-lane layout: 16
+columns x 4 row groups) and A <= 2 (Lay<N,A>'s padded conv lane records, layout.h): 30 shapes,
+odd N with unequal spin channels included (alternating spins: N = 7 gives nspins (4, 3)).
+Systems: "Z<N>" one atom of charge N, "Z<a>-<b>" a diatomic (a + b = N) at z = -1, +1
+(oracle/system.py).  Per shape, four walkers (two for N > 10: the oracle's Laplacian),
+randomised auxiliary parameters:
+  fp64: log|psi| (1e-10), grad log|psi| (1e-8), E_L (1e-6 Ha, the north-star bar), one
+        host-draw Metropolis sweep (positions 1e-9), the parameter gradient (1e-8 of each
+        walker's largest component);
+  fp32: log|psi| and E_L against the same fp64 oracle (the reference's dtype, the parity
+        suite's fp32 tolerances).
+Outside the built set aiqmc_create refuses with AIQMC_EUNSUPPORTED and a message naming the
+limit (N = 17, A = 3)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(n, a) for a in (1, 2) for n in range(2, 17)]
+
+
+def _name(n, a):
+    return f"Z{n}" if a == 1 else f"Z{(n + 1) // 2}-{n // 2}"
+
+
+_REF = {}
+
+
+def _oracle(n, a):
+    """(system, params, pos, e_l, logabs, grad) of the fp64 oracle, cached per shape."""
+    if (n, a) not in _REF:
+        from oracle import hamiltonian, network, system
+        s = system.make_system(_name(n, a))
+        rng = np.random.default_rng(100 + 3 * n + a)
+        params = system.init_params(rng, s, randomize_aux=True)
+        pos = system.init_electrons(rng, s.atoms, s.charges, 4 if n <= 10 else 2, 1.0)
+        e, l, g = hamiltonian.batch_local_energy(network.Network(s), network.to_torch(params), torch.tensor(pos))
+        _REF[(n, a)] = (s, params, pos, e.numpy(), l.numpy(), g.numpy())
+    return _REF[(n, a)]
+
+
+def _ctx(s, params, dtype):
+    from oracle import system
+    from aiqmc import _lib
+    t = s.tables()
+    ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
+                       t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"], dtype=dtype,
+                       device=0)
+    ctx.set_params(system.flatten_params(params))
+    return ctx
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda sh: f"N{sh[0]}A{sh[1]}")
+def test_shape_fp64_matches_oracle(shape):
+    s, params, pos, e_ref, l_ref, g_ref = _oracle(*shape)
+    assert (s.nelectrons, s.natoms) == shape
+    ctx = _ctx(s, params, torch.float64)
+    x = torch.tensor(pos, device="cuda")
+    e, l, g = ctx.local_energy(x, want_logabs=True, want_grad=True)
+    l2, g2 = ctx.logpsi_grad(x)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(l.cpu().numpy(), l_ref, rtol=1e-10, atol=1e-10)
+    np.testing.assert_allclose(l2.cpu().numpy(), l_ref, rtol=1e-10, atol=1e-10)
+    np.testing.assert_allclose(g.cpu().numpy(), g_ref, rtol=1e-8, atol=1e-8)
+    np.testing.assert_allclose(g2.cpu().numpy(), g_ref, rtol=1e-8, atol=1e-8)
+    assert np.max(np.abs(e.cpu().numpy() - e_ref)) <= 1e-6, (e.cpu().numpy(), e_ref)
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda sh: f"N{sh[0]}A{sh[1]}")
+def test_shape_metropolis_and_param_grad_match_oracle(shape):
+    from oracle import loss, mcstep, network
+    s, params, pos, _, _, _ = _oracle(*shape)
+    N, B = s.nelectrons, pos.shape[0]
+    ctx = _ctx(s, params, torch.float64)
+    rng = np.random.default_rng(7 + N)
+    g1 = torch.tensor(rng.standard_normal((1, B, 3 * N)))
+    g2 = torch.tensor(rng.standard_normal((1, B, N, 3 * N)))
+    u = torch.tensor(rng.uniform(size=(1, B, N)))
+    ref = mcstep.mc_step(network.Network(s), network.to_torch(params), torch.tensor(pos), g1, g2, u, 0.05, 1)
+    idx = torch.arange(N)
+    x = torch.tensor(pos, device="cuda").contiguous()
+    ctx.mc_step(x, 1, 0.05, gauss1=g1, gauss2=g2.reshape(1, B, N, N, 3)[:, :, idx, idx, :].contiguous(), u=u)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(x.cpu().numpy(), ref.numpy(), rtol=1e-9, atol=1e-9)
+    O = ctx.logpsi_param_grad(torch.tensor(pos, device="cuda")).cpu().numpy()
+    O_ref = loss.logabs_param_grad(network.Network(s), params, torch.tensor(pos))
+    assert O.shape == O_ref.shape
+    err = np.abs(O - O_ref) / (np.abs(O_ref).max(axis=1, keepdims=True) + 1e-3)
+    assert err.max() < 1e-8, (err.max(), np.unravel_index(err.argmax(), err.shape))
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda sh: f"N{sh[0]}A{sh[1]}")
+def test_shape_fp32_matches_oracle(shape):
+    s, params, pos, e_ref, l_ref, _ = _oracle(*shape)
+    ctx = _ctx(s, params, torch.float32)
+    x = torch.tensor(pos, device="cuda").float().contiguous()
+    e, l, _ = ctx.local_energy(x, want_logabs=True, want_grad=True)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(l.double().cpu().numpy(), l_ref, rtol=1e-5, atol=2e-4)
+    np.testing.assert_allclose(e.double().cpu().numpy(), e_ref, rtol=2e-4, atol=2e-3)
+
+
+@pytest.mark.parametrize("n,a,what", [(17, 1, "nelectrons"), (18, 2, "nelectrons"), (10, 3, "no kernel instantiation")])
+def test_shape_outside_the_built_set_is_refused(n, a, what):
+    from aiqmc import _lib
+    atoms = np.zeros((a, 3))
+    atoms[:, 2] = np.arange(a)
+    charges = np.full(a, float(n) / a)
+    spins = np.array([1.0 if i % 2 == 0 else -1.0 for i in range(n)])
+    from oracle import system
+    par, anti, _, _ = system.jastrow_indices_ee(spins, n)
+    up, dn = system.spin_indices_h(spins)
+    with pytest.raises(Exception) as ei:
+        _lib.Context(n, a, (len(up), len(dn)), atoms, charges, up, dn, par, anti, dtype=torch.float64, device=0)
+    assert what in str(ei.value)
