@@ -12,7 +12,9 @@ so that drivers, benchmarks and tests build the same systems:
 * ``N2``     the benchmark molecule of BASELINE.json (R = 2.0744 bohr, SURVEY.md 8(d));
 * ``H2``, ``Be``, ``C``, ``Ne``: the remaining BASELINE.json systems (all-electron atoms /
   molecule, alternating spins as every reference example uses);
-* ``O2``     16 electrons (the largest shape built), alternating spins.
+* ``O2``     16 electrons (the largest shape built), alternating spins;
+* ``CO2_ecp`` example/CO2/co2_test.py:7-19 (AIQMCrelease1/2; C, O, O with ccECP, 16 valence
+  electrons, alternating spins): the three-atom shape (16, 3).
 """
 from __future__ import annotations
 
@@ -85,6 +87,7 @@ _GEOMETRY = {
     "C2_ecp": ([[0.0, 0.0, -1.0], [0.0, 0.0, 1.0]], [4.0, 4.0]),
     "N2": ([[0.0, 0.0, -1.0372], [0.0, 0.0, 1.0372]], [7.0, 7.0]),
     "O2": ([[0.0, 0.0, -1.1408], [0.0, 0.0, 1.1408]], [8.0, 8.0]),
+    "CO2_ecp": ([[1.33, 1.0, 1.0], [0.0, 1.0, 1.0], [2.66, 1.0, 1.0]], [4.0, 6.0, 6.0]),
 }
 SYSTEM_NAMES = tuple(_GEOMETRY)
 
@@ -132,11 +135,19 @@ def all_electron_tables(name: str, list_l: int = 2) -> EcpTables:
     return EcpTables(one(1.0), one(0.0), one(1.0), nl(2.0), nl(0.0), nl(1.0), list_l)
 
 
+# oxygen ccECP of the CO2 example (co2_test.py:11-19: Z_eff 6, one l = 0 projector), in release
+# 3's table shapes (the l = 0 term first, zero-padded as the carbon block)
+_O_LOCAL = ([1.0, 3.0, 2.0], [6.000000, 73.85984, -47.87600], [12.30997, 14.76962, 13.71419])
+_O_NONLOCAL = ([[2.0, 2.0], [2.0, 2.0], [2.0, 2.0]], [[85.86406, 0], [0, 0], [0, 0]],
+               [[13.65512, 0], [0, 0], [0, 0]])
+
+
 def ccecp_tables(name: str) -> EcpTables:
-    """The ccECP tables of a pseudopotential example system (one carbon block per atom)."""
-    if name not in ("C_ecp", "C2_ecp"):
+    """The ccECP tables of a pseudopotential example system (a carbon or oxygen block per atom)."""
+    blocks = {"C_ecp": "C", "C2_ecp": "CC", "CO2_ecp": "COO"}
+    if name not in blocks:
         raise KeyError(f"{name} has no pseudopotential tables")
-    A = make_system(name).natoms
-    rep = lambda rows: np.asarray([rows] * A, np.float64)
-    return EcpTables(rep(_C_LOCAL[0]), rep(_C_LOCAL[1]), rep(_C_LOCAL[2]), rep(_C_NONLOCAL[0]), rep(_C_NONLOCAL[1]),
-                     rep(_C_NONLOCAL[2]), 2)
+    loc = {"C": _C_LOCAL, "O": _O_LOCAL}
+    nl = {"C": _C_NONLOCAL, "O": _O_NONLOCAL}
+    rows = lambda tab, k: np.asarray([tab[e][k] for e in blocks[name]], np.float64)
+    return EcpTables(rows(loc, 0), rows(loc, 1), rows(loc, 2), rows(nl, 0), rows(nl, 1), rows(nl, 2), 2)

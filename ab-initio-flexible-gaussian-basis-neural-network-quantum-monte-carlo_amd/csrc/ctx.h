@@ -10,15 +10,6 @@
 #include "aiqmc.h"
 #include "walker_kernel.h"
 
-// (N, A) instantiations; the Makefile compiles shape.hip once per entry.  A development build
-// may restrict the list (make dev: -DAIQMC_DEV_SHAPES, N2 only).
-#ifdef AIQMC_DEV_SHAPES
-#define AIQMC_SHAPE_LIST(X) X(14, 2)
-#else
-#define AIQMC_SHAPE_LIST(X) X(2, 1) X(2, 2) X(3, 1) X(3, 2) X(4, 1) X(4, 2) X(5, 1) X(5, 2) X(6, 1) X(6, 2) X(7, 1) X(7, 2) X(8, 1) X(8, 2) X(9, 1) \
-  X(9, 2) X(10, 1) X(10, 2) X(11, 1) X(11, 2) X(12, 1) X(12, 2) X(13, 1) X(13, 2) X(14, 1) X(14, 2) X(15, 1) X(15, 2) X(16, 1) X(16, 2)
-#endif
-
 int aiqmc_fail(int code, const std::string& msg);
 using aq::KArgs;
 #include <utility>
@@ -116,6 +107,3 @@ struct ShapeOps {
 };
 
 
-#define AIQMC_DECL(n, a) bool aiqmc_shape_ops_##n##_##a(ShapeOps* ops);
-AIQMC_SHAPE_LIST(AIQMC_DECL)
-#undef AIQMC_DECL

@@ -76,7 +76,13 @@ struct Lay {
   // the conv weights, conv biases and single weights is contiguous here (strided by 4 above), so
   // one dwordx4 load fetches four values (round 4: the proposal launch issued 142 vector loads
   // per wave, most of them these weights, with the texture-address unit 62 % busy).
-  static constexpr int XQ = 8;   // conv outputs per layer, padded (Q0 = 3 A + 2 <= 8 for A <= 2)
+  // conv outputs per layer, padded to whole 16-byte records (8 for A <= 2: Q0 = 3 A + 2)
+  static constexpr int XQ = (Q0 > Q1 ? Q0 : Q1) <= 8 ? 8 : ((Q0 > Q1 ? Q0 : Q1) + 3) / 4 * 4;
+  // conv-bias record of a lane: its output of each full quad, then the Q mod 4 outputs every lane
+  // evaluates (4 for A <= 2)
+  static constexpr int CBN(int q) { return q / 4 + q % 4; }
+  static constexpr int XB = (CBN(Q0) > CBN(Q1) ? CBN(Q0) : CBN(Q1)) <= 4 ? 4
+                            : ((CBN(Q0) > CBN(Q1) ? CBN(Q0) : CBN(Q1)) + 3) / 4 * 4;
   static constexpr int x0 = (total + 3) / 4 * 4;
   // [3][N][4][XQ] conv weights of (electron i, unit f): w[i][4 q + f], q < Q
   static constexpr int xcw(int l) { return x0 + l * N * 4 * XQ; }
@@ -84,12 +90,12 @@ struct Lay {
   static constexpr int xsw(int l) { return xcw(3) + l * 4 * XQ; }
   // [3][XQ][4] single-layer weight rows w[q][0..3] (aligned copy)
   static constexpr int xsr(int l) { return xsw(3) + l * XQ * 4; }
-  // [3][N][4][4] conv biases of (electron i, unit f): b[i][4 s + f] for the Q / 4 full quads s,
+  // [3][N][4][XB] conv biases of (electron i, unit f): b[i][4 s + f] for the Q / 4 full quads s,
   // then b[i][q] for the Q mod 4 outputs every lane evaluates
-  static constexpr int xcb(int l) { return xsr(3) + l * N * 4 * 4; }
+  static constexpr int xcb(int l) { return xsr(3) + l * N * 4 * XB; }
   static constexpr int total_ext = xcb(3);   // device parameter buffer
   static_assert(Q0 <= XQ && Q1 <= XQ, "conv outputs exceed the padded lane records");
-  static_assert(Q0 / 4 + Q0 % 4 <= 4 && Q1 / 4 + Q1 % 4 <= 4, "conv bias record");
+  static_assert(CBN(Q0) <= XB && CBN(Q1) <= XB, "conv bias record");
 
   // canonical (tree_flatten) parameter count
   static constexpr long canon(int npar, int nanti) {

@@ -114,8 +114,8 @@ static void pack_params(const aiqmc_ctx* c, const double* flat, std::vector<doub
     for (int i = 0; i < N; ++i)
       for (int f = 0; f < 4; ++f) {
         for (int q = 0; q < Q[l]; ++q) out[Ly::xcw(l) + (i * 4 + f) * Ly::XQ + q] = out[cw[l] + i * D[l] + 4 * q + f];
-        for (int s4 = 0; s4 < QF; ++s4) out[Ly::xcb(l) + (i * 4 + f) * 4 + s4] = out[cb[l] + i * Q[l] + 4 * s4 + f];
-        for (int q = 4 * QF; q < Q[l]; ++q) out[Ly::xcb(l) + (i * 4 + f) * 4 + QF + q - 4 * QF] = out[cb[l] + i * Q[l] + q];
+        for (int s4 = 0; s4 < QF; ++s4) out[Ly::xcb(l) + (i * 4 + f) * Ly::XB + s4] = out[cb[l] + i * Q[l] + 4 * s4 + f];
+        for (int q = 4 * QF; q < Q[l]; ++q) out[Ly::xcb(l) + (i * 4 + f) * Ly::XB + QF + q - 4 * QF] = out[cb[l] + i * Q[l] + q];
       }
     for (int f = 0; f < 4; ++f)
       for (int q = 0; q < Q[l]; ++q) out[Ly::xsw(l) + f * Ly::XQ + q] = out[sw[l] + q * NH + f];

@@ -164,8 +164,8 @@ __global__ __launch_bounds__(64) void k_param_grad(KArgs ka) {
   for (int l = 0; l < 3; ++l) {
     const int d = l == 0 ? D0 : NH;
     const int DF = 3 * d + 2 * NH2, Q = DF / 4;
-    if (lane < nk * 2 * d) {
-      const int kw = lane / (2 * d), gl = lane - kw * 2 * d;
+    for (int it = lane; it < nk * 2 * d; it += 64) {   // 2 K D0 > 64 lanes for A >= 3
+      const int kw = it / (2 * d), gl = it - kw * 2 * d;
       T* sm = S(kw);
       const T* h = sm + SM::hl + SM::hoff(l);
       T* g1 = sm + SM::g1 + l * 2 * D0;

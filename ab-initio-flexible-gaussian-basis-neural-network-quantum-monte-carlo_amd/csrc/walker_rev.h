@@ -906,10 +906,10 @@ k_walker_rev(KArgs ka) {
     const cptr<T> sb = P + (l == 0 ? Ly::sng_b0 : (l == 1 ? Ly::sng_b1 : Ly::sng_b2));
     if constexpr (xlane) {
       // the lane's records of the lane-order blocks: 2 + 2 + 1 sixteen-byte loads
-      T cw8[Ly::XQ], sw8[Ly::XQ], cb4[4];
+      T cw8[Ly::XQ], sw8[Ly::XQ], cb4[Ly::XB];
       ld_vec<T, Ly::XQ>(P + Ly::xcw(l) + (ic * 4 + ff) * Ly::XQ, cw8);
       ld_vec<T, Ly::XQ>(P + Ly::xsw(l) + ff * Ly::XQ, sw8);
-      ld_vec<T, 4>(P + Ly::xcb(l) + (ic * 4 + ff) * 4, cb4);
+      ld_vec<T, Ly::XB>(P + Ly::xcb(l) + (ic * 4 + ff) * Ly::XB, cb4);
 #pragma unroll
       for (int q = 0; q < SM::QM; ++q)
         if (q < Q) {

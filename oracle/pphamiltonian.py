@@ -103,6 +103,19 @@ def c2_ccecp() -> ECP:
                two(c.non_local_exps), 2)
 
 
+def co2_ccecp() -> ECP:
+    """The CO2 example (AIQMCrelease2/example/CO2/co2_test.py:7-19; atoms C, O, O): the carbon
+    block and the oxygen ccECP (Z_eff 6: local 6.0 / 73.85984 / -47.87600 at exponents 12.30997 /
+    14.76962 / 13.71419, one l = 0 projector 85.86406 at 13.65512), in release 3's [A, 3, 2]
+    nonlocal layout (the l = 0 term first, as c_atom_ccecp)."""
+    c = c_atom_ccecp()
+    o_loc = ([1.0, 3.0, 2.0], [6.0, 73.85984, -47.87600], [12.30997, 14.76962, 13.71419])
+    o_nl = ([[2.0, 2.0], [2.0, 2.0], [2.0, 2.0]], [[85.86406, 0], [0, 0], [0, 0]], [[13.65512, 0], [0, 0], [0, 0]])
+    st = lambda a, o: np.concatenate([a, [o], [o]], axis=0)
+    return ECP(st(c.rn_local, o_loc[0]), st(c.local_coes, o_loc[1]), st(c.local_exps, o_loc[2]),
+               st(c.rn_non_local, o_nl[0]), st(c.non_local_coes, o_nl[1]), st(c.non_local_exps, o_nl[2]), 2)
+
+
 def local_pp_energy(ecp: ECP, pos: torch.Tensor, atoms: torch.Tensor, charges: torch.Tensor):
     """local_pp_energy (pseudopotential.py:86-117) summed over electrons and atoms."""
     N = pos.shape[0] // 3

@@ -110,14 +110,20 @@ def make_system(name: str) -> System:
     elif name == "N2":
         atoms = np.array([[0.0, 0.0, -1.0372], [0.0, 0.0, 1.0372]])
         charges = np.array([7.0, 7.0])
+    elif name == "CO2_ecp":
+        # AIQMCrelease2/example/CO2/co2_test.py:7-10: C, O, O with ccECP charges, alternating spins
+        atoms = np.array([[1.33, 1.0, 1.0], [0.0, 1.0, 1.0], [2.66, 1.0, 1.0]])
+        charges = np.array([4.0, 6.0, 6.0])
     elif name == "O2":
         atoms = np.array([[0.0, 0.0, -1.1408], [0.0, 0.0, 1.1408]])
         charges = np.array([8.0, 8.0])
-    elif re.fullmatch(r"Z\d+(-\d+)?", name):
+    elif re.fullmatch(r"Z\d+(-\d+){0,4}", name):
         # generic shapes (tests/test_gpu_shapes.py): "Z<z>" one atom of charge z at the origin,
-        # "Z<a>-<b>" a diatomic of charges a, b at z = -1, +1 bohr; neutral, alternating spins
+        # "Z<a>-<b>" a diatomic of charges a, b at z = -1, +1 bohr, up to five atoms "Z<a>-...-<e>"
+        # (the third to fifth off the axis, no symmetry); neutral, alternating spins
         zs = [float(z) for z in name[1:].split("-")]
-        atoms = np.zeros((1, 3)) if len(zs) == 1 else np.array([[0.0, 0.0, -1.0], [0.0, 0.0, 1.0]])
+        sites = np.array([[0.0, 0.0, -1.0], [0.0, 0.0, 1.0], [1.2, 0.7, 0.3], [-0.9, 1.1, -0.4], [0.3, -1.3, 0.8]])
+        atoms = np.zeros((1, 3)) if len(zs) == 1 else sites[:len(zs)]
         charges = np.array(zs)
     else:
         raise KeyError(name)

@@ -6,7 +6,8 @@ Configs: the reference's single-atom carbon ccECP example
 spins +-+-, list_l = 2, tables :13-23) -> C_ecp.npz, and its C2 example
 (example/C2/C2.py:8-27: atoms at z = -+1, both ccECP carbons, block spins ++++----)
 -> C2_ecp.npz, where the rotated electron NOT being offset by its atom (quirk E2)
-matters.  Arrays (float64):
+matters, and the CO2 example (AIQMCrelease2/example/CO2/co2_test.py: C, O, O ccECP, 16
+electrons, the three-atom shape) -> CO2_ecp.npz (2 walkers).  Arrays (float64):
   params_flat  canonical parameter vector; pos [B,12]; rot [B,3,3] the injected
   grid rotations (jax.random.orthogonal's role, pseudopotential.py:233-241);
   e_re, e_im [B]  complex E_L (pphamiltonian.py:177-188);
@@ -28,7 +29,9 @@ from oracle import network, pphamiltonian, system  # noqa: E402
 torch.set_default_dtype(torch.float64)
 
 
-CONFIGS = {"C_ecp": (31, pphamiltonian.c_atom_ccecp), "C2_ecp": (32, pphamiltonian.c2_ccecp)}
+CONFIGS = {"C_ecp": (31, pphamiltonian.c_atom_ccecp), "C2_ecp": (32, pphamiltonian.c2_ccecp),
+           "CO2_ecp": (33, pphamiltonian.co2_ccecp)}
+BATCH = {"CO2_ecp": 2}   # 16 electrons x 3 atoms x 50 points per walker through the oracle network
 
 
 def make(out_dir: str, name: str = "C_ecp", B: int = 4):
@@ -52,4 +55,4 @@ def make(out_dir: str, name: str = "C_ecp", B: int = 4):
 
 if __name__ == "__main__":
     for n in sys.argv[1:] or list(CONFIGS):
-        make(os.path.dirname(os.path.abspath(__file__)), n)
+        make(os.path.dirname(os.path.abspath(__file__)), n, BATCH.get(n, 4))

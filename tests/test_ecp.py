@@ -105,11 +105,11 @@ def test_cos_theta_quirk():
         np.testing.assert_allclose(cfg[0, 0].numpy(), np.linalg.norm(pos.numpy()) * g, rtol=1e-15)
 
 
-@pytest.mark.parametrize("name,n3", [("C_ecp", 12), ("C2_ecp", 24)])
-def test_golden_fixture_consistent(golden_dir, name, n3):
+@pytest.mark.parametrize("name,n3,B", [("C_ecp", 12, 4), ("C2_ecp", 24, 4), ("CO2_ecp", 48, 2)])
+def test_golden_fixture_consistent(golden_dir, name, n3, B):
     g = dict(np.load(os.path.join(golden_dir, f"{name}.npz")))
-    assert g["pos"].shape == (4, n3) and g["rot"].shape == (4, 3, 3)
-    np.testing.assert_allclose(np.einsum("bij,bkj->bik", g["rot"], g["rot"]), np.broadcast_to(np.eye(3), (4, 3, 3)),
+    assert g["pos"].shape == (B, n3) and g["rot"].shape == (B, 3, 3)
+    np.testing.assert_allclose(np.einsum("bij,bkj->bik", g["rot"], g["rot"]), np.broadcast_to(np.eye(3), (B, 3, 3)),
                                atol=1e-12)
     assert np.all(np.isfinite(g["e_re"])) and np.all(np.isfinite(g["logq_re"]))
 
@@ -123,17 +123,28 @@ def _ecp_ctx(dtype, name="C_ecp"):
     t = s.tables()
     ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
                        t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"], dtype=dtype, device=0)
-    e = pp.c_atom_ccecp() if name == "C_ecp" else pp.c2_ccecp()
+    e = {"C_ecp": pp.c_atom_ccecp, "C2_ecp": pp.c2_ccecp, "CO2_ecp": pp.co2_ccecp}[name]()
     ctx.set_ecp(e.rn_local, e.local_coes, e.local_exps, e.rn_non_local, e.non_local_coes, e.non_local_exps, e.list_l)
     return s, ctx
 
 
+def test_product_ccecp_tables_equal_the_oracle_tables():
+    """aiqmc.systems.ccecp_tables (what drivers and bench.py upload) == the oracle's tables."""
+    from aiqmc import systems
+    for name, o in [("C_ecp", pp.c_atom_ccecp()), ("C2_ecp", pp.c2_ccecp()), ("CO2_ecp", pp.co2_ccecp())]:
+        t = systems.ccecp_tables(name)
+        for k in ("rn_local", "local_coes", "local_exps", "rn_non_local", "non_local_coes", "non_local_exps"):
+            np.testing.assert_array_equal(getattr(t, k), getattr(o, k), err_msg=f"{name}.{k}")
+        assert t.list_l == o.list_l
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["C_ecp", "C2_ecp"])
+@pytest.mark.parametrize("name", ["C_ecp", "C2_ecp", "CO2_ecp"])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_ecp_local_energy_golden(golden_dir, dtype, name):
-    """C atom and the C2 example (two ccECP centres off the origin: quirk E2, the rotated
-    electron NOT offset by its atom, changes the answer there)."""
+    """C atom, the C2 example (two ccECP centres off the origin: quirk E2, the rotated
+    electron NOT offset by its atom, changes the answer there) and the CO2 example (three
+    atoms, carbon and oxygen ccECP blocks, 16 electrons)."""
     g = dict(np.load(os.path.join(golden_dir, f"{name}.npz")))
     s, ctx = _ecp_ctx(dtype, name)
     ctx.set_params(g["params_flat"])
@@ -155,7 +166,7 @@ def test_ecp_local_energy_golden(golden_dir, dtype, name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["C_ecp", "C2_ecp"])
+@pytest.mark.parametrize("name", ["C_ecp", "C2_ecp", "CO2_ecp"])
 def test_ecp_reuse_matches_scratch(golden_dir, name):
     """Quadrature configurations from the walker cache == evaluated from scratch (fp64)."""
     g = dict(np.load(os.path.join(golden_dir, f"{name}.npz")))
