@@ -54,7 +54,8 @@ typedef struct aiqmc_ctx aiqmc_ctx;
 /* System + network configuration (make_ai_net arguments, nn.py:511-526). */
 typedef struct aiqmc_cfg {
   int32_t nelectrons;            /* N  (2 <= N <= 16)                          */
-  int32_t natoms;                /* A                                          */
+  int32_t natoms;                /* A  ((N, A) in aiqmc_supported_shapes():   */
+                                 /*     every N with A <= 3, and (10,4),(10,5)) */
   int32_t nspins[2];             /* (n_up, n_down); both > 0                   */
   int32_t dtype;                 /* AIQMC_F32 | AIQMC_F64                      */
   int32_t device;                /* HIP device ordinal                         */
