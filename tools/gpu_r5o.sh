@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/ab
-VARS="base gjpl"
+VARS="${VARS:-base gjpl}"
 for t in $VARS; do
   AIQMC_LIB_VARIANT=$t timeout -k 10 120 python tools/pos_dump.py gpurun_out/ab/pos_$t.npy > /dev/null 2>&1 || { echo "$t pos_dump FAILED"; exit 1; }
 done
