@@ -39,6 +39,21 @@ def test_supported_shapes_include_benchmark_systems():
         assert s in shapes
 
 
+def test_shape_list_is_the_makefiles_and_the_shape_tests_cover_it():
+    """The dispatch table (aiqmc_supported_shapes) is generated from csrc/Makefile's SHAPES, and
+    tests/test_gpu_shapes.py runs every one of them against the oracle."""
+    import os
+    import re
+    from aiqmc import _lib
+    import test_gpu_shapes
+    mk = open(os.path.join(os.path.dirname(_lib.__file__), "..", "csrc", "Makefile")).read()
+    line = re.search(r"^SHAPES\s*:=\s*(.*)$", mk, re.M).group(1)
+    make_shapes = {tuple(int(v) for v in t.split("_")) for t in line.split()}
+    assert set(_lib.supported_shapes()) == make_shapes
+    assert set(test_gpu_shapes.SHAPES) == {sh for sh in make_shapes if sh[0] >= sh[1]}
+    assert {(n, a) for a in (1, 2) for n in range(2, 17)} <= make_shapes
+
+
 def test_last_error_is_a_string():
     from aiqmc import _lib
     assert isinstance(_lib.last_error(), str)
