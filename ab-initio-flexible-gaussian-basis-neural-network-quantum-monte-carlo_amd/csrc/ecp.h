@@ -177,6 +177,35 @@ __device__ __forceinline__ void ecp_group_norms(const T* R, int lane, double Fg[
   for (int g = 0; g < 4; ++g) Fg[g] = wave_sum(gl == g ? v : 0.0);
 }
 
+// The nonlocal radial factors v_l(r_ia) (pseudopotential.py:118-160) of every (electron, atom)
+// pair, once per pair instead of once per quadrature point (they do not depend on the point: fp64
+// pow and exp per term were ≈ 90 % of the launch's instructions); the same arithmetic, so the same
+// bits.  tm = 0: v_l; tm != 0: exp(-tstep v_l) - 1 (the T-move amplitude factor, T2).
+constexpr int ECP_MAXPAIR = 64;   // N A of every built shape (16 x 3, 10 x 5)
+template <typename T>
+__device__ __forceinline__ void ecp_pair_radials(const EcpArgs& ea, const T* x, int lane, double (*vl)[4], bool tm) {
+  const int N = ea.N, A = ea.A;
+  const int stride = 3 * (ea.KL + ea.L * ea.KN);
+  const double* atoms = ea.tab;
+  const double* tabs = ea.tab + 4 * A;
+  for (int j = lane; j < N * A; j += 64) {
+    const int i = j / A, a = j - (j / A) * A;
+    double r2 = 0.0;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const double t = (double)x[3 * i + d] - atoms[a * 3 + d];
+      r2 += t * t;
+    }
+    const double r = sqrt(r2);
+    const double* tnl = tabs + a * stride + 3 * ea.KL;
+    for (int l = 0; l < ea.L; ++l) {
+      const double v = ecp_radial(tnl + 3 * ea.KN * l, ea.KN, r, 0.0);
+      vl[j][l] = tm ? exp(-ea.tstep * v) - 1.0 : v;
+    }
+  }
+  __syncthreads();
+}
+
 template <typename T>
 __global__ __launch_bounds__(64) void k_ecp_energy(EcpArgs ea) {
   const int b = blockIdx.x;
@@ -195,6 +224,9 @@ __global__ __launch_bounds__(64) void k_ecp_energy(EcpArgs ea) {
   const double ph0 = ea.skip_nl ? 0.0 : (double)((const T*)ea.ph0)[b];
   const double dn = 1.0 / (la0 * la0 + ph0 * ph0);   // 1 / den, den = la0 + i ph0 (E4)
   double er = 0.0, ei = 0.0;
+  __shared__ double vl[ECP_MAXPAIR][4];
+  const bool pair_tab = N * A <= ECP_MAXPAIR && ea.L <= 4;
+  if (pair_tab && !ea.skip_nl) ecp_pair_radials<T>(ea, x, lane, vl, false);
   // zero nonlocal coefficients: every term is v_l(r) = 0 times a finite ratio, exactly 0
   for (int idx = ea.skip_nl ? M : lane; idx < M; idx += 64) {
     const int i = idx / (A * ECP_NQ);
@@ -222,7 +254,8 @@ __global__ __launch_bounds__(64) void k_ecp_energy(EcpArgs ea) {
     const double rr = (la * la0 + ph * ph0) * dn * w, ri = (ph * la0 - la * ph0) * dn * w;
     const double* tnl = tabs + a * stride + 3 * ea.KL;
     double s = 0.0;
-    for (int l = 0; l < ea.L; ++l) s += ecp_pl(l, cs) * ecp_radial(tnl + 3 * ea.KN * l, ea.KN, r, 0.0);   // E1
+    for (int l = 0; l < ea.L; ++l)
+      s += ecp_pl(l, cs) * (pair_tab ? vl[i * A + a][l] : ecp_radial(tnl + 3 * ea.KN * l, ea.KN, r, 0.0));   // E1
     er += s * rr;
     ei += s * ri;
   }
@@ -293,6 +326,9 @@ __global__ __launch_bounds__(64) void k_tmove(EcpArgs ea) {
   const double dn = 1.0 / (la0 * la0 + ph0 * ph0);
   double* scr = ea.scr + (size_t)b * M * 4;
   double nr = 0.0, ni = 0.0;
+  __shared__ double el[ECP_MAXPAIR][4];
+  const bool pair_tab = N * A <= ECP_MAXPAIR && ea.L <= 4;
+  if (pair_tab) ecp_pair_radials<T>(ea, x, lane, el, true);
   for (int idx = lane; idx < M; idx += 64) {
     const int i = idx / AQ;
     const int a = (idx / ECP_NQ) % A;
@@ -318,7 +354,8 @@ __global__ __launch_bounds__(64) void k_tmove(EcpArgs ea) {
     const double* tnl = tabs + a * stride + 3 * ea.KL;
     double wt = 0.0;
     for (int l = 0; l < ea.L; ++l)
-      wt += (exp(-ea.tstep * ecp_radial(tnl + 3 * ea.KN * l, ea.KN, r, 0.0)) - 1.0) * ecp_pl(l, cs);   // T2
+      wt += (pair_tab ? el[i * A + a][l] : exp(-ea.tstep * ecp_radial(tnl + 3 * ea.KN * l, ea.KN, r, 0.0)) - 1.0) *
+            ecp_pl(l, cs);   // T2
     const double tr = rr * wt, ti = ri * wt;
     const bool pos = tr > 0.0 || (tr == 0.0 && ti > 0.0);   // T3
     const double fr = pos ? tr : 0.0, fi = pos ? ti : 0.0;
