@@ -86,6 +86,7 @@ struct EcpArgs {
   void* xnew;           // k_ecp_points output [B*N*A*50][3]
   uint64_t seed, step;  // k_ecp_rot
   int skip_nl;          // k_ecp_energy: nonlocal coefficients all zero -- no quadrature was run
+  int cdf_lds;          // k_tmove: dynamic LDS holds every electron's cdf row [N][A*50+1][2]
   // T-moves (k_tmove)
   double tstep;
   const void* usel;     // [B] selection uniform (NULL: Philox)
@@ -384,10 +385,31 @@ __global__ __launch_bounds__(64) void k_tmove(EcpArgs ea) {
   int levels = 0;
   while ((1 << levels) < M1 + 1) ++levels;        // ceil(log2(M1 + 1))
   const int lo_[5] = {0, 1, 19, 55, 79}, hi_[5] = {1, 19, 55, 79, 151};
+  extern __shared__ double cdf_s[];   // cdf_lds: [N][M1][2]
   for (int e = lane; e < N; e += 64) {
     // T5: jnp.searchsorted(cdf_e, u + 1), cdf_e[k] = sum_{j<=k} row_e[j] / norm
     const double* fe = scr + (size_t)e * AQ * 4;
     int low = 0, high = M1;
+    if (ea.cdf_lds) {
+      // the row's cdf once, in the same order of operations as the per-probe sums below (so the
+      // same bits), then the search reads it: one pass over the row instead of one per probe
+      double* ce = cdf_s + (size_t)e * M1 * 2;
+      double cr = inr, ci = ini;
+      ce[0] = cr;
+      ce[1] = ci;
+      for (int j = 1; j < M1; ++j) {
+        const double fr = fe[4 * (j - 1)], fi = fe[4 * (j - 1) + 1];
+        cr += fr * inr - fi * ini;
+        ci += fr * ini + fi * inr;
+        ce[2 * j] = cr;
+        ce[2 * j + 1] = ci;
+      }
+      for (int lv = 0; lv < levels; ++lv) {
+        const int mid = (low + high) >> 1;
+        if (cplx_le(qr, 0.0, ce[2 * mid], ce[2 * mid + 1])) high = mid;
+        else low = mid;
+      }
+    } else
     for (int lv = 0; lv < levels; ++lv) {
       const int mid = (low + high) >> 1;
       double cr = inr, ci = ini;   // row_e[0] = 1

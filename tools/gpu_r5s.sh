@@ -1,5 +1,5 @@
-# round 5: ccECP radial factors once per (electron, atom) pair in k_ecp_energy / k_tmove (new) vs per
-# quadrature point (old library copy): outputs bitwise, ms per pp E_L batch and per T-move step
+# round 5: ECP A/B of the in-tree library (main) against a saved copy (old): per-pair radial factors,
+# then the T-move cdf once per row in LDS; outputs bitwise, ms per pp E_L batch and per T-move step
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/ab
