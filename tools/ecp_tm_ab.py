@@ -1,6 +1,6 @@
 """pp local energy and T-moves of the ccECP example systems on one library (AIQMC_LIB_VARIANT):
 outputs saved for a bitwise comparison between libraries, and ms per call (4096 walkers, fp32).
-usage: python tools/ecp_tm_ab.py out.npz"""
+usage: python tools/ecp_tm_ab.py out.npz   (ECP_SYSTEMS="C_ecp C2_ecp" restricts the systems)"""
 import json, os, sys, time
 import numpy as np
 import torch
@@ -11,7 +11,7 @@ from aiqmc.initial_electrons_positions.init import init_electrons  # noqa: E402
 from aiqmc.wavefunction_Ynlm.nn import flatten_params  # noqa: E402
 
 out, res = {}, {}
-for name in ("C_ecp", "C2_ecp", "CO2_ecp"):
+for name in os.environ.get("ECP_SYSTEMS", "C_ecp C2_ecp CO2_ecp").split():
     for dt in (torch.float32, torch.float64):
         s = systems.make_system(name)
         ctx = s.context(dtype=dt)
