@@ -166,6 +166,41 @@ def test_ecp_local_energy_golden(golden_dir, dtype, name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["Z4-2-2", "Z3-2-2"])
+def test_ecp_packed_three_atoms_match_oracle(name):
+    """pp E_L of N <= 8 systems with 3 atoms (the packed quadrature launch k_quad_value with
+    A >= 3 -- wider layer-0 lane records than any reference example) against the fp64 oracle,
+    live: the carbon ccECP block on every atom (the tables are independent of the charges),
+    2 walkers, injected rotations."""
+    from oracle import network, system
+    from aiqmc import _lib
+    s = system.make_system(name)
+    assert (s.nelectrons, s.natoms) in _lib.supported_shapes() or pytest.skip("shape not built")
+    c = pp.c_atom_ccecp()
+    A = s.natoms
+    rep = lambda a: np.concatenate([a] * A, axis=0)
+    ecp = pp.ECP(rep(c.rn_local), rep(c.local_coes), rep(c.local_exps), rep(c.rn_non_local), rep(c.non_local_coes),
+                 rep(c.non_local_exps), 2)
+    rng = np.random.default_rng(71)
+    params = system.init_params(rng, s, randomize_aux=True)
+    pos = system.init_electrons(rng, s.atoms, s.charges, 2, 1.0)
+    rots = pp.haar_rotations(rng, 2)
+    ref, _, _, _ = pp.batch_local_energy_pp(network.Network(s), network.to_torch(params), ecp, torch.tensor(pos), rots)
+    t = s.tables()
+    ctx = _lib.Context(s.nelectrons, s.natoms, s.nspins, s.atoms, s.charges, t["spin_up_indices"],
+                       t["spin_down_indices"], t["parallel_indices"], t["antiparallel_indices"], dtype=torch.float64,
+                       device=0)
+    ctx.set_ecp(ecp.rn_local, ecp.local_coes, ecp.local_exps, ecp.rn_non_local, ecp.non_local_coes,
+                ecp.non_local_exps, ecp.list_l)
+    ctx.set_params(system.flatten_params(params))
+    e = ctx.local_energy_ecp(torch.tensor(pos, device="cuda"), rot=torch.tensor(rots, device="cuda"))
+    torch.cuda.synchronize()
+    ref = ref.detach().numpy()
+    assert np.max(np.abs(e.real.cpu().numpy() - ref.real)) <= 1e-6, (e, ref)
+    assert np.max(np.abs(e.imag.cpu().numpy() - ref.imag)) <= 1e-6, (e, ref)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", ["C_ecp", "C2_ecp", "CO2_ecp"])
 def test_ecp_reuse_matches_scratch(golden_dir, name):
     """Quadrature configurations from the walker cache == evaluated from scratch (fp64)."""
