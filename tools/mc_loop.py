@@ -8,6 +8,7 @@ from aiqmc import systems, _lib
 from aiqmc.initial_electrons_positions.init import init_electrons
 from aiqmc.wavefunction_Ynlm.nn import flatten_params
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+NS = int(os.environ.get("AIQMC_NSTEPS", "10"))   # sweeps per mc_step call
 name = sys.argv[2] if len(sys.argv) > 2 else "N2"
 B = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
 s = systems.make_system(name)
@@ -33,14 +34,14 @@ if os.environ.get("AIQMC_HOST_DRAWS"):   # device-resident draws passed in (no P
     draws = dict(gauss1=torch.randn(10, B, 3 * N, device="cuda", generator=g),
                  gauss2=torch.randn(10, B, N, 3, device="cuda", generator=g),
                  u=torch.rand(10, B, N, device="cuda", generator=g))
-ctx.mc_step(pos, 10, 0.05, seed=1, offset=0, **draws)
+ctx.mc_step(pos, NS, 0.05, seed=1, offset=0, **draws)
 ctx.local_energy(pos)
 torch.cuda.synchronize()
 noprof = bool(os.environ.get("AIQMC_NOPROF"))   # no HIP events around the launches
 ctx.profile(not noprof)
 t0 = time.perf_counter()
 for k in range(iters):
-    ctx.mc_step(pos, 10, 0.05, seed=1, offset=10 * (k + 1), **draws)
+    ctx.mc_step(pos, NS, 0.05, seed=1, offset=NS * (k + 1), **draws)
     el, _, _ = ctx.local_energy(pos)
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / iters
