@@ -127,3 +127,37 @@ def test_shape_outside_the_built_set_is_refused(n, a, what):
     with pytest.raises(Exception) as ei:
         _lib.Context(n, a, (len(up), len(dn)), atoms, charges, up, dn, par, anti, dtype=torch.float64, device=0)
     assert what in str(ei.value)
+
+
+@pytest.mark.parametrize("shape", [(7, 1), (5, 3), (13, 3), (16, 3), (10, 5)], ids=lambda sh: f"N{sh[0]}A{sh[1]}")
+def test_shape_fp32_sweeps_follow_fp64(shape):
+    """Three fp32 Metropolis sweeps (the reference's dtype; packed N <= 8 kernels or the one-wave
+    proposal path) against fp64 sweeps from the same float-rounded walkers and host draws: at most
+    one acceptance decision in 100 flips, and the walkers that took the same decisions agree to
+    fp32 rounding."""
+    from oracle import system
+    n, a = shape
+    _skip_unbuilt(shape)
+    s = system.make_system(_name(n, a))
+    rng = np.random.default_rng(5 + n)
+    params = system.init_params(rng, s, randomize_aux=True)
+    B, NS = 64, 3
+    pos = system.init_electrons(rng, s.atoms, s.charges, B, 1.0).astype(np.float32).astype(np.float64)
+    g = torch.Generator().manual_seed(n + 10 * a)
+    kw = dict(gauss1=torch.randn(NS, B, 3 * n, generator=g, dtype=torch.float64),
+              gauss2=torch.randn(NS, B, n, 3, generator=g, dtype=torch.float64),
+              u=torch.rand(NS, B, n, generator=g, dtype=torch.float64))
+    c64, c32 = _ctx(s, params, torch.float64), _ctx(s, params, torch.float32)
+    x64 = torch.tensor(pos, device="cuda").contiguous()
+    x32 = x64.float().contiguous()
+    a64 = c64.mc_step(x64, NS, 0.05, count_accepts=True, **kw)
+    a32 = c32.mc_step(x32, NS, 0.05, count_accepts=True, **kw)
+    torch.cuda.synchronize()
+    assert torch.isfinite(x32).all()
+    n64, n32 = int(a64.sum()), int(a32.sum())
+    assert n64 > B * n * NS // 4, n64
+    assert abs(n32 - n64) <= max(1, B * n * NS // 100), (n32, n64)
+    dw = (x32.double() - x64).abs().reshape(B, -1).amax(1)
+    same = dw < 1e-3
+    assert int((~same).sum()) <= max(1, B // 20), dw.topk(4)
+    assert float(dw[same].max()) < 1e-4, float(dw[same].max())
