@@ -40,7 +40,7 @@ def _ctx(name, dtype=torch.float64):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["Be", "N2", "Ne"])
+@pytest.mark.parametrize("name", ["Be", "N2", "Ne", "Z7", "Z3-2-2"])   # + odd N, three atoms (round 5)
 def test_drift_diffusion_matches_oracle(name):
     from oracle import network, system
     s, ctx = _ctx(name)
