@@ -73,8 +73,8 @@ struct SmemQ {
   static constexpr int yv = xo + 4;               // [N][N]    Yt
   static constexpr int hl = yv + NI * NI;         // [N][D0]   ae features
   static constexpr int g2 = hl + NI * D0;         // [3][2][N][4] pair column means
-  static constexpr int S = g2 + 3 * 2 * NI * 4;   // [SW][12]  pair values of the patch
-  static constexpr int h3 = S + SW * 12;          // [N][4]    h-stream output
+  static constexpr int S = g2 + 3 * 2 * NI * 4;   // [NI][12]  new - old pair values (o, pi) of the patch
+  static constexpr int h3 = S + NI * 12;          // [N][4]    h-stream output
   static constexpr int size = h3 + NI * 4;
 };
 
@@ -175,7 +175,9 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
   wave_sync();
 
   // ---------------------------------------------------------------- F2 pairs of the moved electron
-  // lane NI part + o: part 0/1 pair (pi, o) at the new/old x_pi (column o), part 2/3 pair (o, pi)
+  // lane NI part + o: part 0/1 pair (pi, o) at the new/old x_pi (column o), part 2/3 pair (o, pi);
+  // new - old by one DPP row shift (lane + NI, inside the lane's 16-lane row), part 0 into the
+  // pair column means of row o, part 2 into S for the row-pi sums
   {
     const int part = sl / NI, o = sl % NI;
     const int os = o < N ? o : N - 1;
@@ -185,26 +187,32 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
     for (int c = 0; c < 3; ++c) d[c] = part < 2 ? xs[os * 3 + c] - xp[c] : xp[c] - xs[os * 3 + c];
     T v[3][4];
     pair_values<T, N, A>(d, P, v);
+    T dv[3][4];
 #pragma unroll
     for (int l = 0; l < 3; ++l)
 #pragma unroll
-      for (int f = 0; f < 4; ++f) S[sl * 12 + l * 4 + f] = v[l][f];
+      for (int f = 0; f < 4; ++f) dv[l][f] = v[l][f] - dpp<0x100 + NI>(v[l][f]);
     if (part < 2 && o < N && o != pi) {
       const T cusp = P[Ly::jee_c + pi * N + o], al = P[Ly::jee_a + pi * N + o];
       const T je = f_div(cusp * v[0][0], al * v[0][0] + T(1));
       jsum += part == 0 ? je : -je;
     }
+    if (part == 0 && o < N && o != pi) {
+      const int Gp = pi >= nup ? 1 : 0;
+      const T gw = Gp ? ginv1 : ginv0;
+#pragma unroll
+      for (int l = 0; l < 3; ++l)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) g2[((l * 2 + Gp) * N + o) * 4 + f] += dv[l][f] * gw;
+    }
+    if (part == 2) {
+#pragma unroll
+      for (int l = 0; l < 3; ++l)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) S[o * 12 + l * 4 + f] = dv[l][f];
+    }
   }
   wave_sync();
-  if (sl < N && sl != pi) {
-    const int Gp = pi >= nup ? 1 : 0;
-    const T gw = Gp ? ginv1 : ginv0;
-#pragma unroll
-    for (int l = 0; l < 3; ++l)
-#pragma unroll
-      for (int f = 0; f < 4; ++f)
-        g2[((l * 2 + Gp) * N + sl) * 4 + f] += (S[sl * 12 + l * 4 + f] - S[(NI + sl) * 12 + l * 4 + f]) * gw;
-  }
 #pragma unroll
   for (int t0 = 0; t0 < 24; t0 += SW) {
     const int t = t0 + sl;
@@ -213,7 +221,7 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
       const int k0 = G ? nup : 0, k1 = G ? N : nup;
       T acc = T(0);
       for (int k = k0; k < k1; ++k)
-        if (k != pi) acc += S[(2 * NI + k) * 12 + l * 4 + f] - S[(3 * NI + k) * 12 + l * 4 + f];
+        if (k != pi) acc += S[k * 12 + l * 4 + f];
       g2[((l * 2 + G) * N + pi) * 4 + f] += acc * (G ? ginv1 : ginv0);
     }
   }
@@ -481,8 +489,8 @@ struct SmemQG {
   static constexpr int hl = yv + NI * NI;        // h^0 [NI][D0], h^3 [NI][4]; then their adjoints
   static constexpr int h3 = hl + NI * D0;
   static constexpr int g2 = h3 + NI * 4;         // [3][2][N][4] pair column means, then their adjoints
-  static constexpr int S = g2 + 24 * NI;         // [SW][12] patch pair values (WALK: [N][N][12] all pairs); then dbar [N][N][3]
-  static constexpr int cq = S + cmax(cmax(SW * 12, 3 * NI * NI), WALK ? 12 * N * N : 0);   // conv outputs [NI][QM] + [2][NI][QL]
+  static constexpr int S = g2 + 24 * NI;         // [NI][12] new - old patch pair values (WALK: [N][N][12] all pairs); then dbar [N][N][3]
+  static constexpr int cq = S + cmax(cmax(NI * 12, 3 * NI * NI), WALK ? 12 * N * N : 0);   // conv outputs [NI][QM] + [2][NI][QL]
   static constexpr int sv = cq + NI * QM + 2 * NI * QL;      // [3][NI][4] single outputs
   static constexpr int ph = sv + 12 * NI;        // [N][N][2] Phi
   static constexpr int mx = ph + 2 * NI * NI;    // [N][N][2] B = A^{-1}
@@ -682,26 +690,32 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
     for (int c = 0; c < 3; ++c) d[c] = part < 2 ? xs[os * 3 + c] - xp[c] : xp[c] - xs[os * 3 + c];
     T v[3][4];
     pair_values<T, N, A>(d, P, v);
+    T dv[3][4];   // new - old (k_quad_value's F2)
 #pragma unroll
     for (int l = 0; l < 3; ++l)
 #pragma unroll
-      for (int f = 0; f < 4; ++f) S[sl * 12 + l * 4 + f] = v[l][f];
+      for (int f = 0; f < 4; ++f) dv[l][f] = v[l][f] - dpp<0x100 + NI>(v[l][f]);
     if (part < 2 && o < N && o != pi) {
       const T cusp = P[Ly::jee_c + pi * N + o], al = P[Ly::jee_a + pi * N + o];
       const T je = f_div(cusp * v[0][0], al * v[0][0] + T(1));
       jsum += part == 0 ? je : -je;
     }
+    if (part == 0 && o < N && o != pi) {
+      const int Gp = pi >= nup ? 1 : 0;
+      const T gw = Gp ? ginv1 : ginv0;
+#pragma unroll
+      for (int l = 0; l < 3; ++l)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) g2[((l * 2 + Gp) * N + o) * 4 + f] += dv[l][f] * gw;
+    }
+    if (part == 2) {
+#pragma unroll
+      for (int l = 0; l < 3; ++l)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) S[o * 12 + l * 4 + f] = dv[l][f];
+    }
   }
   wave_sync();
-  if (sl < N && sl != pi) {
-    const int Gp = pi >= nup ? 1 : 0;
-    const T gw = Gp ? ginv1 : ginv0;
-#pragma unroll
-    for (int l = 0; l < 3; ++l)
-#pragma unroll
-      for (int f = 0; f < 4; ++f)
-        g2[((l * 2 + Gp) * N + sl) * 4 + f] += (S[sl * 12 + l * 4 + f] - S[(NI + sl) * 12 + l * 4 + f]) * gw;
-  }
 #pragma unroll
   for (int t0 = 0; t0 < 24; t0 += SW) {
     const int t = t0 + sl;
@@ -710,7 +724,7 @@ __global__ __launch_bounds__(64) void k_quad_grad(KArgs ka) {
       const int k0 = G ? nup : 0, k1 = G ? N : nup;
       T acc = T(0);
       for (int k = k0; k < k1; ++k)
-        if (k != pi) acc += S[(2 * NI + k) * 12 + l * 4 + f] - S[(3 * NI + k) * 12 + l * 4 + f];
+        if (k != pi) acc += S[k * 12 + l * 4 + f];
       g2[((l * 2 + G) * N + pi) * 4 + f] += acc * (G ? ginv1 : ginv0);
     }
   }
