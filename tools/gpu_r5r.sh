@@ -1,8 +1,9 @@
-# round 5: counters of the C-atom ccECP quadrature launch (k_quad_value<float,4,1>, BASELINE config 3)
+# round 5: counters of the ccECP quadrature launch (k_quad_value<float,4,1>, BASELINE config 3;
+# ECP_SYSTEM=C2_ecp: k_quad_value<float,8,2>; PMC_TAG names the output directory)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_ecp
+OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_ecp${PMC_TAG:-}
 rm -rf $OUT; mkdir -p $OUT
 passes=(
  "mix=SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT"
@@ -19,7 +20,8 @@ done
 cd $GRAFT_REPO_ROOT
 python3 - <<'PY'
 import csv, glob, collections
-root = "gpurun_out/pmc_ecp"
+import os
+root = "gpurun_out/pmc_ecp" + os.environ.get("PMC_TAG", "")
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{root}/*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
