@@ -35,6 +35,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals", "aiqmc_debug_set_ablate", "aiqmc_debug_set_fuse_accept", "aiqmc_debug_set_walker_pivots", "aiqmc_debug_set_packed_walkers", "aiqmc_debug_set_lap_waves",
     "aiqmc_debug_set_fuse_reduce", "aiqmc_energy_stats", "aiqmc_energy_stats_final",
     "aiqmc_debug_limdrift_factor", "aiqmc_debug_launch_lds", "aiqmc_loss_weights",
+    "aiqmc_param_grad_weighted", "aiqmc_loss_level", "aiqmc_loss_pack", "aiqmc_loss_final",
 )
 
 PROF_MC_PROPOSAL = 0   # proposal value+gradient launches of aiqmc_mc_step
@@ -168,6 +169,10 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_profile_read.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64)]
     lib.aiqmc_energy_stats.argtypes = [vp, i32, i64, vp, i32, vp]
     lib.aiqmc_energy_stats_final.argtypes = [vp, vp]
+    lib.aiqmc_param_grad_weighted.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp, vp]
+    lib.aiqmc_loss_level.argtypes = [i32, vp, vp, i32, i64, vp, vp, dbl, dbl, i32, vp, vp, vp, vp, vp, vp]
+    lib.aiqmc_loss_pack.argtypes = [vp, vp, vp, i32, i32, vp, vp]
+    lib.aiqmc_loss_final.argtypes = [vp, vp, i32, i32, i32, i32, i32, vp, vp, vp]
     lib.aiqmc_last_error.restype = ctypes.c_char_p
     lib.aiqmc_supported_shapes.restype = ctypes.c_char_p
     for name in ("aiqmc_create", "aiqmc_destroy", "aiqmc_set_params", "aiqmc_set_params_device", "aiqmc_logpsi",
@@ -176,7 +181,8 @@ def load() -> ctypes.CDLL:
                  "aiqmc_logpsi_param_grad",
                  "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves",
                  "aiqmc_phase_param_grad", "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals",
-                 "aiqmc_energy_stats", "aiqmc_energy_stats_final"):
+                 "aiqmc_energy_stats", "aiqmc_energy_stats_final", "aiqmc_param_grad_weighted",
+                 "aiqmc_loss_level", "aiqmc_loss_pack", "aiqmc_loss_final"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib
@@ -255,6 +261,56 @@ def loss_weights(e_l: torch.Tensor, clip_scale: float, center_at_clipped: bool, 
                                     _stream(er.device)), "aiqmc_loss_weights")
     clipped = torch.complex(cr, ci) if cplx else cr
     return wr, wi, clipped.reshape(e_l.shape), st
+
+
+def _dt(t: torch.Tensor) -> int:
+    return AIQMC_F32 if t.dtype == torch.float32 else AIQMC_F64
+
+
+def loss_level(level: int, er: torch.Tensor, ei: Optional[torch.Tensor], L1=None, L2=None,
+               clip_scale: float = 0.0, wscale: float = 1.0, g0: bool = False, want_phase: bool = False):
+    """aiqmc_loss_level on this rank's device energies (er, ei: contiguous 1-D, float32/float64).
+    level 1 -> L1 [6] float64; level 2 -> L2 [2]; level 3 -> (w [1 or 2, n], wp [n] or None,
+    clipped_re, clipped_im or None, head [2] float64 = sums of the clipped energies)."""
+    n = er.numel()
+    dev = er.device
+    lib = load()
+    st = _stream(dev)
+    if level in (1, 2):
+        out = torch.empty(6 if level == 1 else 2, dtype=torch.float64, device=dev)
+        check(lib.aiqmc_loss_level(level, _ptr(er), _ptr(ei), _dt(er), n, _ptr(L1), None, 0.0, 0.0, 0, None, None,
+                                   None, None, _ptr(out), st), "aiqmc_loss_level")
+        return out
+    w = torch.empty(2 if g0 else 1, n, dtype=er.dtype, device=dev)
+    wp = torch.empty_like(er) if want_phase else None
+    cr = torch.empty_like(er)
+    ci = torch.empty_like(er) if ei is not None else None
+    head = torch.empty(2, dtype=torch.float64, device=dev)
+    check(lib.aiqmc_loss_level(3, _ptr(er), _ptr(ei), _dt(er), n, _ptr(L1), _ptr(L2), float(clip_scale),
+                               float(wscale), 1 if g0 else 0, _ptr(w), _ptr(wp), _ptr(cr), _ptr(ci), _ptr(head), st),
+          "aiqmc_loss_level")
+    return w, wp, cr, ci, head
+
+
+def loss_pack(g: torch.Tensor, gp: Optional[torch.Tensor], g0: Optional[torch.Tensor], head: torch.Tensor):
+    """L3 = [head (2), g + gp (P), g0 (P, if given)] as one float64 device vector."""
+    P = g.numel()
+    L3 = torch.empty(2 + P * (2 if g0 is not None else 1), dtype=torch.float64, device=g.device)
+    L3[:2].copy_(head)
+    check(load().aiqmc_loss_pack(_ptr(g), _ptr(gp), _ptr(g0), _dt(g), P, _ptr(L3), _stream(g.device)),
+          "aiqmc_loss_pack")
+    return L3
+
+
+def loss_final(L1: torch.Tensor, L3: torch.Tensor, P: int, g0: bool, center_at_clipped: bool, world: int,
+               dtype: torch.dtype):
+    """(grad [P] of dtype, stats [6] float64) from the summed level vectors."""
+    grad = torch.empty(P, dtype=dtype, device=L1.device)
+    stats = torch.empty(6, dtype=torch.float64, device=L1.device)
+    check(load().aiqmc_loss_final(_ptr(L1), _ptr(L3), P, 1 if g0 else 0, 1 if center_at_clipped else 0, int(world),
+                                  AIQMC_F32 if dtype == torch.float32 else AIQMC_F64, _ptr(grad), _ptr(stats),
+                                  _stream(L1.device)), "aiqmc_loss_final")
+    return grad, stats
 
 
 def energy_stats_final(out: torch.Tensor) -> torch.Tensor:
@@ -511,6 +567,18 @@ class Context:
         check(self._lib.aiqmc_logpsi_param_grad(self._h, _ptr(p), B, _ptr(w), _ptr(out), _ptr(la),
                                                 _stream(self.device)), "aiqmc_logpsi_param_grad")
         return (out, la) if want_logabs else out
+
+    def param_grad_weighted(self, pos: torch.Tensor, weights: torch.Tensor, phase: bool = False) -> torch.Tensor:
+        """[K, P] = weights [K, B] times d f / d theta (f = log|psi|, or the phase), one gradient pass."""
+        p = self._pos(pos)
+        B = p.shape[0]
+        w = weights.to(self.device, self.dtype).contiguous()
+        if w.dim() != 2 or w.shape[1] != B:
+            raise ValueError("weights must be [K, B]")
+        out = torch.empty(w.shape[0], self.nparams, dtype=self.dtype, device=self.device)
+        check(self._lib.aiqmc_param_grad_weighted(self._h, _ptr(p), B, 1 if phase else 0, _ptr(w), w.shape[0],
+                                                  _ptr(out), None, _stream(self.device)), "aiqmc_param_grad_weighted")
+        return out
 
     def phase_param_grad(self, pos: torch.Tensor, weights: Optional[torch.Tensor] = None,
                          want_phase: bool = False):

@@ -9,22 +9,48 @@ is initialised.  ``pmean_stats`` fuses the energy statistics of one iteration
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
 PMAP_AXIS_NAME = 'qmc_pmap_axis'
 
+# Run the collective path even at world size 1 (AIQMC_FORCE_COLLECTIVES=1 or force_collectives()):
+# the all-reduces then execute on a one-rank group, e.g. RCCL under torch.distributed.run
+# --nproc-per-node 1 (tests/test_gpu_rccl.py, bench.py --force-collectives).
+_FORCE = os.environ.get("AIQMC_FORCE_COLLECTIVES", "") == "1"
+# all-reduces issued through this module since import (the fused training step issues 3)
+ALLREDUCE_CALLS = 0
+
+
+def force_collectives(on: bool = True) -> None:
+    global _FORCE
+    _FORCE = bool(on)
+
 
 def _active() -> bool:
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    return (dist.is_available() and dist.is_initialized()
+            and (dist.get_world_size() > 1 or _FORCE))
+
+
+def world_size() -> int:
+    return dist.get_world_size() if _active() else 1
+
+
+def all_reduce_(x: torch.Tensor) -> torch.Tensor:
+    """In-place SUM all-reduce over the default group (counted); identity when inactive."""
+    global ALLREDUCE_CALLS
+    if _active():
+        ALLREDUCE_CALLS += 1
+        dist.all_reduce(x, op=dist.ReduceOp.SUM)
+    return x
 
 
 def psum(x: torch.Tensor) -> torch.Tensor:
     if not _active():
         return x
-    y = x.clone()
-    dist.all_reduce(y, op=dist.ReduceOp.SUM)
-    return y
+    return all_reduce_(x.clone())
 
 
 def pmean(x: torch.Tensor) -> torch.Tensor:
@@ -63,7 +89,7 @@ def pmean_stats(e_l: torch.Tensor):
             v = _lib.energy_stats(e_l, finalize=True)
         else:
             v = _lib.energy_stats(e_l, finalize=False)
-            dist.all_reduce(v, op=dist.ReduceOp.SUM)   # out[4..5] are rewritten below
+            all_reduce_(v)   # out[4..5] are rewritten below
             _lib.energy_stats_final(v)
         return v[4], v[5]
     e = e_l.to(torch.float64)

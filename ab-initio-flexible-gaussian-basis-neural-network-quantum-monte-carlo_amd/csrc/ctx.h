@@ -76,6 +76,7 @@ struct aiqmc_ctx {
   void* d_pg = nullptr;             // [pg_B][nkern] per-walker kernel-layout gradients
   void* d_pgr = nullptr;            // [nkern] weighted sum
   int pg_B = 0;
+  int pg_nw = 0;                     // weighted rows d_pgr holds before its chunk sums
   // optional per-kernel HIP-event timing (aiqmc_profile_*): slot -> recorded (start, stop) pairs
   bool prof = false;
   std::vector<hipEvent_t> ev_free;

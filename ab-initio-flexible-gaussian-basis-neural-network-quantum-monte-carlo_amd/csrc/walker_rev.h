@@ -952,6 +952,7 @@ k_walker_rev(KArgs ka) {
     const cptr<T> sngw = P + (l == 0 ? Ly::sng_w0 : (l == 1 ? Ly::sng_w1 : Ly::sng_w2));
     const cptr<T> sngb = P + (l == 0 ? Ly::sng_b0 : (l == 1 ? Ly::sng_b1 : Ly::sng_b2));
 #ifndef AQ_F4_NO_PRELOAD
+    (void)convw; (void)convb; (void)sngw; (void)sngb;  // the preloaded registers replace them
     if (l + 1 < 3) lw_load(l + 1);
 #ifndef AQ_F5_NO_PRELOAD
     if constexpr (PROP) {

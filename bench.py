@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-walkers", type=int, default=256, help="SURVEY 8(d): 256 walkers")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="keep a process group (and every all-reduce) at --gpus 1: the statistics and the "
+                         "fused training-step all-reduces run over --dist-backend on a one-rank group")
     ap.add_argument("--no-ecp", action="store_true", help="skip the C-atom ccECP local-energy side measurement")
     ap.add_argument("--no-adam", action="store_true", help="skip the Be-atom Adam training-step side measurement")
     ap.add_argument("--no-dmc", action="store_true", help="skip the C-atom DMC side measurement")
@@ -429,12 +432,19 @@ def main():
     # The device is bound before the process group so RCCL's communicator uses it.
     local_dev = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_dev)
-    if world > 1:
+    dist_on = world > 1 or args.force_collectives
+    backend = args.dist_backend if torch.cuda.is_available() else "gloo"
+    if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(args.dist_backend if torch.cuda.is_available() else "gloo")
+        if env_world is None:   # --force-collectives without a launcher: a one-rank group of its own
+            dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1)
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local_dev)
     dtype = torch.float32 if args.dtype == "f32" else torch.float64
     from aiqmc import constants, _lib
+    if args.force_collectives:
+        constants.force_collectives(True)
     from aiqmc.initial_electrons_positions.init import init_electrons
 
     atoms, charges, spins, network, params, ctx = build(args.system, dtype, local_dev)
@@ -473,7 +483,7 @@ def main():
         for _ in range(warmup):
             iteration()
         torch.cuda.synchronize()
-        if world > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
         # HIP events around the launches cost GPU time (round 4, N2: 3.07 -> 3.20 ms per iteration
@@ -489,7 +499,7 @@ def main():
                 ctx.profile(True)
             stats = iteration(evs if last else None)
         torch.cuda.synchronize()
-        if world > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
         t_local = time.perf_counter() - t0
@@ -500,7 +510,7 @@ def main():
         walk_ms, walk_n = ctx.profile_read(_lib.PROF_MC_WALKER)
         lap_ms, lap_n = ctx.profile_read(_lib.PROF_LOCAL_ENERGY)
         tt = torch.tensor([t_local, mc_ms, el_ms], dtype=torch.float64, device=dev)
-        if world > 1:
+        if dist_on:
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_job, mc_ms_max, el_ms_max = tt.tolist()
         mean_e, var_e = (float(stats[0]), float(stats[1]))
@@ -620,6 +630,9 @@ def main():
                                    "finite": weak["finite"]}
         if per_rank:
             out["strong_scaling_per_rank"] = per_rank
+        out["collectives"] = {"process_group": dist_on, "backend": backend if dist_on else None,
+                              "forced_at_world_1": bool(args.force_collectives and world == 1),
+                              "allreduce_calls_before_side_benches": constants.ALLREDUCE_CALLS}
         if world == 1 and not args.no_ecp:
             try:
                 out["ecp_c_atom"] = ecp_side_bench(dtype, dev, 4096, 5, not args.no_cpu_baseline)
@@ -631,7 +644,11 @@ def main():
                 out["ecp_c2"] = {"error": repr(e)}
         if world == 1 and not args.no_adam:
             try:
+                c0 = constants.ALLREDUCE_CALLS
                 out["adam_be_atom"] = adam_side_bench(dtype, dev, 4096, 5)
+                # forced collectives: the fused training step's 3 all-reduces per iteration (plus the
+                # MC loop's none) over the process group's backend
+                out["adam_be_atom"]["allreduce_calls"] = constants.ALLREDUCE_CALLS - c0
             except Exception as e:  # a side measurement, never a failure of the headline bench
                 out["adam_be_atom"] = {"error": repr(e)}
         if world == 1 and not args.no_adam:
@@ -655,7 +672,7 @@ def main():
             except Exception as e:  # the baseline is a report, never a failure of the bench
                 out["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -138,6 +138,13 @@ int aiqmc_logpsi_param_grad(aiqmc_ctx* ctx, const void* pos, int32_t B, const vo
 int aiqmc_phase_param_grad(aiqmc_ctx* ctx, const void* pos, int32_t B, const void* weights, void* out,
                            void* phase, void* stream);
 
+/* Several weighted sums from ONE per-walker gradient pass: out[k][P] = sum_b weights[k][b]
+ * d f(x_b) / d theta for k < nw (1..8), f = log|psi| (phase == 0) or the phase (phase != 0);
+ * vals[B] (optional) receives f at the walkers.  (The multi-rank energy gradient needs the
+ * clipping-weighted sum and the plain sum of d log|psi| together, aiqmc_loss_level.) */
+int aiqmc_param_grad_weighted(aiqmc_ctx* ctx, const void* pos, int32_t B, int32_t phase, const void* weights,
+                              int32_t nw, void* out, void* vals, void* stream);
+
 /* The orbital matrix of B walkers (Network.orbitals = make_orbitals.apply, nn.py:409-506,553):
  * orbitals[B][N][N][2] (re, im; ctx dtype) = Phi * Yt * exp(J_ee/N) exp(J_ae/N), rows = up
  * electrons then down electrons (spin_up_indices / spin_down_indices order), row r's envelope
@@ -268,6 +275,30 @@ int aiqmc_energy_stats_final(double* out, void* stream);
 int aiqmc_loss_weights(const void* e_re, const void* e_im, int32_t dtype, int64_t n, double clip_scale,
                        int32_t center_at_clipped, double wscale, void* w_re, void* w_im, void* clipped_re,
                        void* clipped_im, double* stats, void* stream);
+
+/* The same statistics, clipping and gradient weights over SEVERAL ranks, as three levels whose
+ * rank partials sum with one all-reduce each (Loss/loss.py:107,206,208 and the gradient pmean of
+ * Optimizer/adam.py:55).  aiqmc_loss_level(level, ...) for this rank's n energies:
+ *   level 1: out[0..5] = L1 = [sum |e - m|^2, n Re m, n Im m, n |m|^2, n, #(Im e != 0)]  (m: rank mean)
+ *   level 2: out[0..1] = L2 = [sum |Re e - Re E|, sum |Im e - Im E|]  from the SUMMED L1 (clipping only)
+ *   level 3: from the summed L1 (and L2 when clip_scale > 0): the clipped energies xc (the total-
+ *            variation window around the mean, clipped_re/im, may be NULL), the gradient weights
+ *            w[0][b] = wscale (Re xc_b - Re E), w[1][b] = wscale (g0 != 0; centre at the clipped mean),
+ *            wp[b] = the phase weight (wscale Im xc clipping, wscale (2 Im e - Im E) without; may be NULL),
+ *            and out[0..1] = [sum Re xc, sum Im xc].
+ * The caller then forms G = w[0]-weighted d log|psi| + wp-weighted d phase and G0 = w[1]-weighted
+ * d log|psi| (aiqmc_param_grad_weighted), packs L3 = [out[0..1], G, G0] (aiqmc_loss_pack: double
+ * L3[2 + 2P]), all-reduces it, and aiqmc_loss_final writes the pmean'd gradient
+ * grad = (G - (Re dc - Re E) G0) / world (ctx dtype) and stats[0..5] = [Re E, Im E, variance,
+ * Re dc, Im dc, #(Im e != 0) over all ranks] (dc: the clipped mean when center_at_clipped, else E).
+ * L1/L2/L3/out/stats are device doubles; weights and energies of `dtype`. */
+int aiqmc_loss_level(int32_t level, const void* e_re, const void* e_im, int32_t dtype, int64_t n,
+                     const double* L1, const double* L2, double clip_scale, double wscale, int32_t g0, void* w,
+                     void* wp, void* clipped_re, void* clipped_im, double* out, void* stream);
+int aiqmc_loss_pack(const void* g, const void* gp, const void* g0, int32_t dtype, int32_t P, double* L3,
+                    void* stream);
+int aiqmc_loss_final(const double* L1, const double* L3, int32_t P, int32_t g0, int32_t center_at_clipped,
+                     int32_t world, int32_t dtype, void* grad, double* stats, void* stream);
 
 /* Optional HIP-event timing of the hot kernels, recorded on the caller's
  * stream around each launch while enabled.  Slots: 0 = proposal

@@ -2,6 +2,7 @@
 import ctypes
 import re
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -27,9 +28,26 @@ def test_library_exports_every_header_symbol():
 
 
 def test_library_is_gfx950_code_object():
+    """Every translation unit's offload bundle (zstd-compressed since round 6) holds a gfx950 code
+    object and nothing for another GPU target."""
+    import subprocess
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import isa_resources
     from aiqmc import _lib
-    data = open(_lib.LIB_PATH, "rb").read()
-    assert b"gfx950" in data
+    with tempfile.TemporaryDirectory() as d:
+        fb = os.path.join(d, "fb")
+        subprocess.run([f"{isa_resources.LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", _lib.LIB_PATH,
+                        os.path.join(d, "x")], check=True, capture_output=True)
+        pieces = isa_resources.bundles(open(fb, "rb").read())
+        assert len(pieces) >= 2
+        for i, piece in enumerate(pieces):
+            b = os.path.join(d, f"b{i}")
+            open(b, "wb").write(piece)
+            lst = subprocess.run([f"{isa_resources.LLVM}/clang-offload-bundler", "--list", "--type=o", f"--input={b}"],
+                                 capture_output=True, text=True, check=True).stdout.split()
+            gpu = [t for t in lst if t.startswith("hip")]
+            assert gpu == ["hipv4-amdgcn-amd-amdhsa--gfx950"], lst
 
 
 def test_supported_shapes_include_benchmark_systems():

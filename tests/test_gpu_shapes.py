@@ -161,3 +161,67 @@ def test_shape_fp32_sweeps_follow_fp64(shape):
     same = dw < 1e-3
     assert int((~same).sum()) <= max(1, B // 20), dw.topk(4)
     assert float(dw[same].max()) < 1e-4, float(dw[same].max())
+
+
+@pytest.mark.parametrize("shape,B", [((4, 1), 5), ((2, 2), 5), ((3, 1), 7), ((6, 1), 3), ((8, 2), 3), ((7, 2), 5)],
+                         ids=lambda v: str(v))
+def test_param_grad_partial_last_wave(shape, B):
+    """k_param_grad packs K walkers per wave (K = 4 for N <= 4, 2 for N <= 8): B not a multiple of
+    K leaves the last wave partial (nk < K: the per-walker Gauss-Jordan skip, the zeroed reduction
+    slots, the output loops).  Per-walker rows and weighted sums of d log|psi| and d phase, fp64
+    vs the oracle and fp32 vs fp64, on such batches."""
+    from oracle import loss, network, system
+    n, a = shape
+    _skip_unbuilt(shape)
+    s = system.make_system(_name(n, a))
+    rng = np.random.default_rng(40 + n + a)
+    params = system.init_params(rng, s, randomize_aux=True)
+    pos = system.init_electrons(rng, s.atoms, s.charges, B, 1.0)
+    net = network.Network(s)
+    O_ref = loss.logabs_param_grad(net, params, torch.tensor(pos))
+    P_ref = loss.phase_param_grad(net, params, torch.tensor(pos))
+    w = rng.normal(size=B)
+    c64, c32 = _ctx(s, params, torch.float64), _ctx(s, params, torch.float32)
+    x = torch.tensor(pos, device="cuda")
+    for ref, fn in ((O_ref, "logpsi_param_grad"), (P_ref, "phase_param_grad")):
+        rows = getattr(c64, fn)(x).cpu().numpy()
+        ws = getattr(c64, fn)(x, weights=torch.tensor(w, device="cuda")).cpu().numpy()
+        scale = np.abs(ref).max(axis=1, keepdims=True) + 1e-3
+        assert (np.abs(rows - ref) / scale).max() < 1e-8, fn
+        np.testing.assert_allclose(ws, w @ ref, rtol=0, atol=1e-8 * np.abs(w @ ref).max())
+        r32 = getattr(c32, fn)(x.float().contiguous()).double().cpu().numpy()
+        assert (np.abs(r32 - ref) / scale).max() < 5e-3, fn
+        # the weighted multi-row entry (one gradient pass, two weight rows)
+        W = torch.tensor(np.stack([w, np.ones(B)]), device="cuda")
+        two = c64.param_grad_weighted(x, W, phase=fn.startswith("phase")).cpu().numpy()
+        np.testing.assert_allclose(two[0], ws, rtol=1e-13, atol=1e-13 * np.abs(ws).max())
+        np.testing.assert_allclose(two[1], ref.sum(0), rtol=0, atol=1e-8 * np.abs(ref.sum(0)).max())
+
+
+@pytest.mark.parametrize("shape", [(7, 1), (9, 2), (13, 3), (16, 3), (10, 4), (10, 5)], ids=lambda sh: f"N{sh[0]}A{sh[1]}")
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_set_params_device_equals_host_upload_shapes(shape, dtype):
+    """aiqmc_set_params_device on the round-5 shapes (odd N, A = 3..5 with their wider F4/B2 and
+    conv-bias records): log|psi|, its gradient, E_L and the parameter gradient bitwise equal to the
+    host upload."""
+    from oracle import system
+    n, a = shape
+    _skip_unbuilt(shape)
+    s = system.make_system(_name(n, a))
+    rng = np.random.default_rng(60 + n + a)
+    params = system.init_params(rng, s, randomize_aux=True)
+    flat = system.flatten_params(params)
+    pos = torch.tensor(system.init_electrons(rng, s.atoms, s.charges, 8, 1.0), device="cuda", dtype=dtype)
+    outs = []
+    for mode in ("host", "device"):
+        ctx = _ctx(s, params, dtype)
+        if mode == "device":   # over a different host upload, so a no-op device repack would fail
+            ctx.set_params(0.5 * flat)
+            ctx.set_params_device(torch.tensor(flat, dtype=torch.float64, device="cuda"))
+        la, g = ctx.logpsi_grad(pos)
+        e, _, _ = ctx.local_energy(pos)
+        pg = ctx.logpsi_param_grad(pos)
+        torch.cuda.synchronize()
+        outs.append([t.cpu() for t in (la, g, e, pg)])
+    for x_, y_ in zip(*outs):
+        assert torch.equal(x_, y_)

@@ -25,6 +25,27 @@ DEFAULT_LIB = os.path.join(ROOT, "ab-initio-flexible-gaussian-basis-neural-netwo
                            "aiqmc", "libaiqmc_hip.so")
 
 
+def bundles(data):
+    """The offload bundles a .hip_fatbin section concatenates (one per TU): plain
+    (__CLANG_OFFLOAD_BUNDLE__) or zstd-compressed (--offload-compress: "CCOB" + version, method,
+    total size, ...; each cut to its total size -- the section pads between them)."""
+    import struct
+    plain = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = sorted([m.start() for m in re.finditer(re.escape(plain), data)] +
+                    [m.start() for m in re.finditer(b"CCOB", data)])
+    out = []
+    for i, s in enumerate(starts):
+        e = starts[i + 1] if i + 1 < len(starts) else len(data)
+        if data[s:s + 4] == b"CCOB":
+            ver = struct.unpack_from("<H", data, s + 4)[0]
+            tot = struct.unpack_from("<I", data, s + 8)[0] if ver == 2 else struct.unpack_from("<Q", data, s + 8)[0]
+            if not 0 < tot <= e - s:
+                continue   # "CCOB" bytes inside another bundle's payload
+            e = s + tot
+        out.append(data[s:e])
+    return out
+
+
 def code_objects(lib):
     """The gfx950 code objects bundled in lib's .hip_fatbin section (one per translation unit)."""
     with tempfile.TemporaryDirectory() as d:
@@ -32,14 +53,10 @@ def code_objects(lib):
         subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", lib, os.path.join(d, "x")],
                        check=True, capture_output=True)
         data = open(fb, "rb").read()
-        # the section concatenates one offload bundle per TU; split at the bundle magic
-        magic = b"__CLANG_OFFLOAD_BUNDLE__"
-        starts = [m.start() for m in re.finditer(re.escape(magic), data)]
         out = []
-        for i, s in enumerate(starts):
-            e = starts[i + 1] if i + 1 < len(starts) else len(data)
+        for i, piece in enumerate(bundles(data)):
             bpath = os.path.join(d, f"b{i}")
-            open(bpath, "wb").write(data[s:e])
+            open(bpath, "wb").write(piece)
             lst = subprocess.run([f"{LLVM}/clang-offload-bundler", "--list", "--type=o", f"--input={bpath}"],
                                  capture_output=True, text=True)
             tgts = [t for t in lst.stdout.split() if "gfx950" in t]
