@@ -91,7 +91,8 @@ for tag, dt in (("f64", torch.float64), ("f32", torch.float32)):
     e_l, _ = le(params, None, data)
     ctx = network.apply._aiqmc_network.bind(params, data.atoms, dt)
     x = data.positions.reshape(256, -1)
-    gfn = lambda w, wp: (ctx.param_grad_weighted(x, w), ctx.param_grad_weighted(x, wp[None], phase=True)[0])
+    gfn = lambda w, wp: (ctx.param_grad_weighted(x, w),
+                         ctx.param_grad_weighted(x, wp[None], phase=True)[0] if wp is not None else None)
     constants.force_collectives(True)
     c0 = constants.ALLREDUCE_CALLS
     (loss1, aux1), g1 = ev.value_and_pmean_grad(params, None, data)
