@@ -64,6 +64,50 @@ __device__ __forceinline__ void stage_copy(T* dst, cptr<T> src, int n) {
   for (int i = cnt * 16 / (int)sizeof(T) + (int)threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
 }
 
+// The same copy split in two, so that the loads of a block can be issued a phase ahead of the
+// barrier that frees its LDS destination: stage_load issues this thread's 16-byte pieces into
+// registers (NU >= the pieces per thread of a one-wave workgroup), stage_store writes them.
+typedef unsigned int u4s __attribute__((ext_vector_type(4)));
+template <typename T, int CNT>
+struct StageRegs {
+  static constexpr int PIECES = CNT * (int)sizeof(T) / 16;
+  static constexpr int NU = (PIECES + 63) / 64 > 0 ? (PIECES + 63) / 64 : 1;
+  static constexpr int TL = CNT - PIECES * 16 / (int)sizeof(T);   // a tail shorter than 16 bytes (odd N)
+  u4s r[NU];
+  T tail;
+  __device__ __forceinline__ void load(cptr<T> src) {
+    const __attribute__((address_space(4))) u4s* s = (const __attribute__((address_space(4))) u4s*)src;
+#pragma unroll
+    for (int k = 0; k < NU; ++k) {
+      const int i = (int)threadIdx.x + k * (int)blockDim.x;
+      if (i < PIECES) r[k] = s[i];
+    }
+    if (TL > 0 && (int)threadIdx.x < TL) tail = src[CNT - TL + (int)threadIdx.x];
+  }
+  __device__ __forceinline__ void store(T* dst) const {
+    u4s* d = (u4s*)dst;
+#pragma unroll
+    for (int k = 0; k < NU; ++k) {
+      const int i = (int)threadIdx.x + k * (int)blockDim.x;
+      if (i < PIECES) d[i] = r[k];
+    }
+    if (TL > 0 && (int)threadIdx.x < TL) dst[CNT - TL + (int)threadIdx.x] = tail;
+  }
+};
+// local-energy stage prefetch (round 6, interleaved A/B on one box, N2 4096 walkers, µs per E_L
+// pair: 194.7 / 195.1 -> 192.2 / 191.3, E_L and positions bitwise equal;
+// profiles/r06_s2_ab_lap_prefetch.txt).  -DAQ_LAP_NO_PREFETCH: the synchronous stage_copy.
+#ifndef AQ_LAP_NO_PREFETCH
+constexpr bool kLapPrefetch = true;
+#else
+constexpr bool kLapPrefetch = false;
+#endif
+#ifdef AQ_LAP_PREFETCH2
+constexpr bool kLapPrefetch2 = kLapPrefetch;
+#else
+constexpr bool kLapPrefetch2 = false;
+#endif
+
 // One h-stream layer (nn.py:280-311) in first derivatives, column loop over electrons i.
 // ly: this layer's LapCache block (LDS); hb: dh/dx of every electron, updated in place
 // (column `lane` = min(lane, 48), see SmemLap).
@@ -346,8 +390,15 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
 #pragma unroll
   for (int m = 0; m < D0; ++m) h0b[m] = Lc[LC::h0b + le * D0 + m];
   static_assert(LC::layer_n * sizeof(T) % 16 == 0 && SM::ly * sizeof(T) % 16 == 0, "16-byte staging");
-  stage_copy<T>(ly, Lc, LC::layer_n);
-  __syncthreads();
+  // kLapPrefetch2: layer 0's block stays in registers over the per-electron stage (its latency
+  // behind that VALU work) and goes to LDS just before layer 0 reads it
+  StageRegs<T, LC::layer_n> l0;
+  if constexpr (kLapPrefetch2) {
+    l0.load(Lc);
+  } else {
+    stage_copy<T>(ly, Lc, LC::layer_n);
+    __syncthreads();
+  }
 
   // ------------------------------------------------------------------ per-electron stage (electron.h)
   ElecOut<T, A> eo;
@@ -373,17 +424,41 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
   T jd2 = (!PH && w0 && dir) ? eo.jae.d2 : T(0);
 
   // ------------------------------------------------------------------ h stream, first derivatives
+  // kLapPrefetch: each staged block's loads are issued one phase ahead (into spare VGPRs: the kernel
+  // runs at 2 waves/SIMD, 256 VGPRs each) and written to LDS after the barrier that frees it, so
+  // no wave waits a whole L2/HBM round trip at a stage boundary
+  if constexpr (kLapPrefetch2) {
+    l0.store(ly);
+    __syncthreads();
+  }
+  StageRegs<T, LC::layer_n> lnext;
+  if constexpr (kLapPrefetch) lnext.load(Lc + LC::layer_n);
   lap_layer<T, N, A, 0>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W);
   if constexpr (PH) {   // the e-e Jastrow terms and V_ee of layer 0's column loop: not part of theta
     jd1 = jd2 = vv = T(0);
   }
   __syncthreads();
-  stage_copy<T>(ly, Lc + LC::layer_n, LC::layer_n);
+  if constexpr (kLapPrefetch) lnext.store(ly);
+  else stage_copy<T>(ly, Lc + LC::layer_n, LC::layer_n);
   __syncthreads();
+  if constexpr (kLapPrefetch) lnext.load(Lc + 2 * LC::layer_n);
   lap_layer<T, N, A, 1>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W);
   __syncthreads();
-  stage_copy<T>(ly, Lc + 2 * LC::layer_n, LC::layer_n);
+  if constexpr (kLapPrefetch) lnext.store(ly);
+  else stage_copy<T>(ly, Lc + 2 * LC::layer_n, LC::layer_n);
   __syncthreads();
+  StageRegs<T, 8 * N * N> qnext;
+  StageRegs<T, (SM::stage_b ? 2 * N * N : 4)> bnext;
+  // kLapPrefetch2: E2's Phi row of electron le as well
+  T phrow[2 * N];
+  if constexpr (kLapPrefetch) {
+    qnext.load(Lc + LC::qs);
+    if constexpr (SM::stage_b) bnext.load(Lc + LC::bm);
+  }
+  if constexpr (kLapPrefetch2) {
+#pragma unroll
+    for (int j = 0; j < 2 * N; ++j) phrow[j] = Lc[LC::ph + le * 2 * N + j];
+  }
   lap_layer<T, N, A, 2>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W);
   if (W > 1) __syncthreads();   // the determinant terms read every wave's columns of dh/dx
 
@@ -408,10 +483,15 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
   {
     T* qd = sm + SM::qs;
     static_assert(LC::qs % 4 == 0 && LC::bm % 4 == 0 && SM::qs % 4 == 0 && SM::bs % 4 == 0, "16-byte staging");
-    stage_copy<T>(qd, Lc + LC::qs, 8 * N * N);
-    if constexpr (SM::stage_b) {
-      T* bd = sm + SM::bs;
-      stage_copy<T>(bd, Lc + LC::bm, 2 * N * N);
+    if constexpr (kLapPrefetch) {
+      qnext.store(qd);
+      if constexpr (SM::stage_b) bnext.store(sm + SM::bs);
+    } else {
+      stage_copy<T>(qd, Lc + LC::qs, 8 * N * N);
+      if constexpr (SM::stage_b) {
+        T* bd = sm + SM::bs;
+        stage_copy<T>(bd, Lc + LC::bm, 2 * N * N);
+      }
     }
   }
   __syncthreads();
@@ -427,7 +507,8 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
   T wbr = T(0), wbi = T(0), t2 = T(0);
 #pragma unroll
   for (int col = 0; col < N; ++col) {
-    const T pr = Ph[(le * N + col) * 2], pm = Ph[(le * N + col) * 2 + 1];
+    const T pr = kLapPrefetch2 ? phrow[2 * col] : Ph[(le * N + col) * 2];
+    const T pm = kLapPrefetch2 ? phrow[2 * col + 1] : Ph[(le * N + col) * 2 + 1];
     const T br = Bu[(col * N + le) * 2], bi = Bu[(col * N + le) * 2 + 1];
     wr[col] = pr * Yd1[col];
     wi[col] = pm * Yd1[col];

@@ -281,6 +281,22 @@ template <int N> struct PairTab {
 };
 template <int N> __constant__ PairTab<N> pair_tab{};
 
+// n consecutive elements global -> LDS by gfx950 LDS-DMA (global_load_lds_dword: lane l of each
+// wave-instruction writes the wave-uniform LDS base + 4 l; no VGPR destination).  The data is
+// counted on vmcnt: the caller waits (s_waitcnt vmcnt(0)) before anything reads or overwrites it.
+template <typename T>
+__device__ __forceinline__ void lds_dma(T* dst, const T* src, int n, int lane) {
+  const int nw = n * (int)sizeof(T) / 4;
+  const float* s = (const float*)src;
+  float* d = (float*)dst;
+#pragma unroll
+  for (int w = 0; w < nw; w += 64) {
+    if (w + lane < nw)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(s + w + lane),
+                                       (__attribute__((address_space(3))) void*)(d + w), 4, 0, 0);
+  }
+}
+
 // c ? x : +0 as a bit mask (no select of a loaded value: see the F1 cache loads)
 __device__ __forceinline__ float and_zero(bool c, float x) {
   return __builtin_bit_cast(float, __builtin_bit_cast(unsigned, x) & (c ? ~0u : 0u));
@@ -553,6 +569,14 @@ k_walker_rev(KArgs ka) {
   // the cached path is compiled there only (the general one serves walker launches, reuse-off
   // proposals and plain value+gradient calls)
   const bool reuse = !PREP && PROP;
+  // PROP: F1's walker-cache blocks by LDS-DMA (round 6, interleaved A/B on one box, N2 4096 walkers,
+  // µs per proposal launch: 220.7 / 221.4 -> 220.5 / 220.6, positions bitwise equal; 21 VALU and one
+  // VGPR fewer per wave; profiles/r06_s1_ab_f1_glds_slp.txt).  -DAQ_NO_F1_GLDS: VGPR-staged copies.
+#ifndef AQ_NO_F1_GLDS
+  constexpr bool f1_glds = PROP;
+#else
+  constexpr bool f1_glds = false;
+#endif
   // walker launch re-using its previous sweep's pivot order (F5; KArgs::pvok)
   const bool wfix = !PREP && !PROP && !isprop && ka.pvok != 0;
   T* Wc = (T*)ka.wcache + (size_t)(reuse ? pb : conf) * WC::size;
@@ -614,6 +638,16 @@ k_walker_rev(KArgs ka) {
     // all loads issued before the first LDS store
     constexpr int NY = (N * N + 63) / 64, NHh = (N * D0 + 63) / 64, NG = (3 * 2 * N * 4 + 63) / 64;
     T ry[NY], rh[NHh], rg[NG];
+    // f1_glds: the walker's Yt, ae-feature and g2 blocks go global -> LDS by LDS-DMA (no VGPR
+    // staging, no per-element selection); the moved electron's rows are patched in after they land
+    T eyv = T(0), eh0 = T(0);
+    if constexpr (f1_glds) {
+      lds_dma<T>(Yv, Wc + WC::yv, N * N, lane);
+      lds_dma<T>(sm + SM::hl, Wc + WC::h0, N * D0, lane);
+      lds_dma<T>(g2, Wc + WC::g2, 3 * 2 * N * 4, lane);
+      eyv = Eq[EC::yv + (lane < N ? lane : N - 1)];
+      eh0 = Eq[EC::h0 + (lane < D0 ? lane : D0 - 1)];
+    }
     // PROP: F0's positions too (walker pb's, the moved electron's proposed position from
     // k_moved_electron), so that every global load of F0/F1 is in flight before one barrier
     // Every load is issued unconditionally at a clamped, in-bounds index and the moved electron's
@@ -628,6 +662,7 @@ k_walker_rev(KArgs ka) {
       rsl = rowsrc[lane < N ? lane : N - 1];   // F5's slot table (after F4)
     }
     // unsigned offsets: the loads take the wave's base pointer in SGPRs plus a 32-bit lane offset
+    if constexpr (!f1_glds) {
 #pragma unroll
     for (int t = 0; t < NY; ++t) {
       const unsigned idx = lane + 64 * t;
@@ -648,6 +683,7 @@ k_walker_rev(KArgs ka) {
     for (int t = 0; t < NG; ++t) {
       const int idx = lane + 64 * t;
       rg[t] = Wc[WC::g2 + (idx < 3 * 2 * N * 4 ? idx : 3 * 2 * N * 4 - 1)];
+    }
     }
     {
       // one load per value from a selected address, masked to +0 by a bit and: a select between
@@ -677,6 +713,12 @@ k_walker_rev(KArgs ka) {
       AQ_SYNC();
       f2_pair_values(jc, ja);
     }
+    if constexpr (f1_glds) {
+      // the DMA'd blocks have landed (vmcnt counts LDS-DMA) before the moved electron's rows go over them
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane < N) Yv[pi * N + lane] = eyv;
+      if (lane < D0) sm[SM::hl + pi * D0 + lane] = eh0;
+    } else {
 #pragma unroll
     for (int t = 0; t < NY; ++t)
       if (lane + 64 * t < N * N) Yv[lane + 64 * t] = ry[t];
@@ -686,6 +728,7 @@ k_walker_rev(KArgs ka) {
 #pragma unroll
     for (int t = 0; t < NG; ++t)
       if (lane + 64 * t < 3 * 2 * N * 4) g2[lane + 64 * t] = rg[t];
+    }
   } else {
     if (wfix) pvr = Wc[WC::pv + (lane < 3 * N + 2 ? lane : 3 * N + 1)];   // to LDS after F4, before F5's write
     ElecOut<T, A> eo;

@@ -48,6 +48,57 @@ PEAK_FP64_TFLOPS = 78.6          # FP64 vector peak (spec)
 PEAK_HBM_GBS = 8000.0
 
 
+# General algorithmic FLOP model of one wavefunction forward for N electrons, A atoms (the side
+# configurations' rooflines; DESIGN.md 5, "FLOP models"), hand-counted from nn.py / Jastrow.py /
+# envelope.py with an FMA = 2 FLOP and a transcendental = 1:
+#   ae / ee features 9NA + 9N^2, Ylm terms and their means 86NA, Ylm stream N(48A + 240),
+#   Yt = y W^ 12N^2, h stream: per electron 65A + 292 (three conv + single layers with their group
+#   means), pair stream 108N^2, Phi 18N^2, envelope 20NA, Jastrows 2N^2 + 8NA, M = Phi Yt e^J 4N^2,
+#   complex LU (8/3)N^3  ->  F_fwd = 236NA + 532N + 153N^2 + (8/3)N^3.
+# For N2 it gives 5.14e4 against SURVEY 8(d)'s hand count 4.9e4; the headline keeps SURVEY's
+# constants (F_FWD_N2, F_EL_N2) so that its fraction stays comparable across rounds.
+def f_fwd(n, a):
+    return 236.0 * n * a + 532.0 * n + 153.0 * n * n + 8.0 / 3.0 * n ** 3
+
+
+def f_el(n, a):
+    """SURVEY 8(d)'s local-energy model on f_fwd: (F_fwd - F_LU)(3N + 2) + 16N^3 + 3N (8N^3 + 8N^2)."""
+    k = 3 * n
+    return (f_fwd(n, a) - 8.0 / 3.0 * n ** 3) * (k + 2) + 16.0 * n ** 3 + k * 8.0 * n ** 3 + k * 8.0 * n * n
+
+
+def load_pmc_side(lib_sha):
+    """Per-launch HBM bytes of the side configurations' dominant kernels (tools/gpu_side_prof.sh ->
+    profiles/pmc_side_rNN.json), used only when taken on THIS library build."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_side_r[0-9][0-9].json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("lib_sha16") == lib_sha:
+            d["pmc_file"] = os.path.relpath(f, ROOT)
+            return d
+    return None
+
+
+def side_roofline(kernel, flop_per_launch, avg_ms, launches, flop_model, pmc_side, side, peak=None, note=None):
+    """A roofline object for a side configuration's dominant kernel (fp32 VALU bound, as the headline)."""
+    peak = peak or PEAK_FP32_TFLOPS
+    achieved = flop_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms else None
+    rec = (pmc_side or {}).get("sides", {}).get(side) or {}
+    traffic = rec.get("hbm_bytes_per_launch")
+    out = {"kernel": kernel, "bound": "valu", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+           "frac": achieved / peak if achieved else None, "traffic": traffic,
+           "hbm_gbs": traffic / (avg_ms * 1e-3) / 1e9 if (traffic and avg_ms) else None,
+           "avg_launch_ms": avg_ms, "launches": launches, "flop_per_launch": flop_per_launch,
+           "flop_model": flop_model, "pmc_file": (pmc_side or {}).get("pmc_file"),
+           "pmc_null_reason": None if traffic else "no profiles/pmc_side_rNN.json taken on this library build"}
+    if note:
+        out["note"] = note
+    return out
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -158,7 +209,7 @@ def cpu_baseline(name, params, atoms, charges, nsteps_unused, tstep, sample_walk
     }
 
 
-def ecp_side_bench(dtype, device, walkers, steps, cpu_baseline_on, name="C_ecp"):
+def ecp_side_bench(dtype, device, walkers, steps, cpu_baseline_on, name="C_ecp", pmc_side=None):
     """BASELINE.json config 'C atom with ccECP pseudopotential, 4096 walkers, 1xMI355X': complex
     pp local energy (pphamiltonian.py:177-188) of the whole batch, Philox grid rotations.
     name="C2_ecp": the reference's example/C2 (8 pseudo-valence electrons, two atoms)."""
@@ -187,10 +238,17 @@ def ecp_side_bench(dtype, device, walkers, steps, cpu_baseline_on, name="C_ecp")
     nq = walkers * s.nelectrons * s.natoms * _lib.ECP_NQ
     cfg = ("C atom ccECP (Z_eff=4, 4 e-, list_l=2)" if name == "C_ecp" else
            f"{name}: {s.nelectrons} e-, {s.natoms} atoms, ccECP") + ", complex E_L incl. 50-point nonlocal quadrature"
+    N, A = s.nelectrons, s.natoms
+    qavg = q_ms / max(q_n, 1)
     res = {"config": cfg,
            "walkers": walkers, "local_energy_evals_per_s": walkers * steps / dt, "ms_per_eval_batch": 1e3 * dt / steps,
-           "quadrature_configs_per_launch": nq, "quadrature_launch_avg_ms": q_ms / max(q_n, 1),
-           "mean_energy_re": float(out.real.mean()), "finite": bool(torch.isfinite(out.real).all())}
+           "quadrature_configs_per_launch": nq, "quadrature_launch_avg_ms": qavg,
+           "mean_energy_re": float(out.real.mean()), "finite": bool(torch.isfinite(out.real).all()),
+           # the quadrature's value-only forwards of the displaced configurations (pseudopotential.py:
+           # 298-314 evaluates the network at every point; the kernel reuses the walker's cache)
+           "roofline": side_roofline(f"k_quad_value<float,{N},{A}> (value-only quadrature configurations)",
+                                     nq * f_fwd(N, A), qavg, q_n, f"configs x F_fwd({N},{A}) = {nq} x {f_fwd(N, A):.0f}",
+                                     pmc_side, "ecp_c" if name == "C_ecp" else "ecp_c2")}
     if cpu_baseline_on and name == "C_ecp":
         sys.path.insert(0, ROOT)
         from oracle import network as onet, pphamiltonian as opp, system as osys
@@ -254,7 +312,7 @@ def pp_adam_side_bench(dtype, device, walkers, steps):
             "energy": lv, "finite": bool(math.isfinite(lv))}
 
 
-def dmc_side_bench(dtype, device, walkers, steps, system="C_ecp"):
+def dmc_side_bench(dtype, device, walkers, steps, system="C_ecp", pmc_side=None):
     """DMC propagation through the drop-in API (DMC/dmc.py:72-93 + branch.py, as main_dmc.py:160-210
     drives it): T-moves, drift-diffusion, pp local energies before/after, weight update, stochastic
     comb.  system "C_ecp": the C-atom ccECP tables (the only ones the reference ships);
@@ -298,11 +356,27 @@ def dmc_side_bench(dtype, device, walkers, steps, system="C_ecp"):
     for k in range(2):
         one(k)
     torch.cuda.synchronize()
+    ctx.profile(True)
     t0 = time.perf_counter()
     for k in range(steps):
         eloc = one(100 + k)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    ctx.profile(False)
+    from aiqmc import _lib
+    l_ms, l_n = ctx.profile_read(_lib.PROF_LOCAL_ENERGY)
+    lavg = l_ms / max(l_n, 1)
+    fe, ff = f_el(N, A), f_fwd(N, A)
+    # one DMC step: a drift-diffusion sweep ((N + 1) value+gradient passes), two local energies,
+    # and with ccECP tables the T-move / nonlocal quadratures (N A 50 value-only configurations each)
+    nq = N * A * _lib.ECP_NQ if system.endswith("_ecp") else 0
+    it_flop = walkers * ((N + 1) * 3 * ff + 2 * fe + 3 * nq * ff)
+    rf = side_roofline(f"k_walker_rev<float,{N},{A},PREP> + k_walker_lap<float,{N},{A}> (local energy, 2 launches)",
+                       walkers * fe, lavg, l_n, f"B*F_EL({N},{A}) = {walkers}*{fe:.3g}", pmc_side,
+                       "dmc_ne" if system == "Ne" else "dmc_c")
+    rf["iteration_achieved"] = it_flop / (dt / steps) / 1e12
+    rf["iteration_frac"] = rf["iteration_achieved"] / PEAK_FP32_TFLOPS
+    rf["iteration_flop_model"] = "B*((N+1)*3*F_fwd + 2*F_EL + 3*N*A*50*F_fwd [ccECP only]) per DMC step"
     t0 = time.perf_counter()
     for k in range(steps):
         tm(data, params, PhiloxKey(5, k))
@@ -318,10 +392,10 @@ def dmc_side_bench(dtype, device, walkers, steps, system="C_ecp"):
             "energy_re_quantiles": {q: float(v) for q, v in zip(
                 ("p01", "p10", "p50", "p90", "p99"),
                 torch.quantile(eloc.real.double().cpu(), torch.tensor([0.01, 0.1, 0.5, 0.9, 0.99], dtype=torch.float64)))},
-            "finite": bool(torch.isfinite(eloc.real).all())}
+            "finite": bool(torch.isfinite(eloc.real).all()), "roofline": rf}
 
 
-def adam_side_bench(dtype, device, walkers, steps):
+def adam_side_bench(dtype, device, walkers, steps, pmc_side=None):
     """BASELINE.json config 'Be atom (4e-), 4096 walkers, Adam, 1xMI355X': one training iteration
     of main_all_electrons_adam_muti_GPU.py:177-190 = mc_step (nsteps=10) + make_loss energy gradient
     (local energy, clipping, GPU parameter gradient) + Adam update, through the drop-in API."""
@@ -352,15 +426,32 @@ def adam_side_bench(dtype, device, walkers, steps):
         data = mc_step(params, data, VMCmcstep.PhiloxKey(9, 10 * t))
         data, params, state, loss_v, aux = step(data, params, state, t)
     torch.cuda.synchronize()
+    from aiqmc import _lib
+    ctx = network.apply._aiqmc_network.context(atoms, dtype, None)   # the drop-in's context (nn.bind)
+    ctx.profile(True)
     t0 = time.perf_counter()
     for t in range(steps):
         data = mc_step(params, data, VMCmcstep.PhiloxKey(9, 100 + 10 * t))
         data, params, state, loss_v, aux = step(data, params, state, 2 + t)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
+    ctx.profile(False)
+    p_ms, p_n = ctx.profile_read(_lib.PROF_MC_PROPOSAL)
+    pavg = p_ms / max(p_n, 1)
+    ff = f_fwd(n, 1)
+    # whole iteration: 10 sweeps of (N + 1) value+gradient passes, the local energy, the parameter
+    # gradient (one value+gradient pass per walker), per walker
+    it_flop = walkers * (10 * (n + 1) * 3 * ff + f_el(n, 1) + 3 * ff)
+    rf = side_roofline(f"k_quad_grad<float,{n},1,false> (Metropolis proposals, 4 configurations per wave)",
+                       walkers * n * 3 * ff, pavg, p_n, f"B*N*3*F_fwd({n},1) = {walkers}*{n}*3*{ff:.0f}",
+                       pmc_side, "adam_be")
+    rf["iteration_achieved"] = it_flop / dt / 1e12
+    rf["iteration_frac"] = rf["iteration_achieved"] / PEAK_FP32_TFLOPS
+    rf["iteration_flop_model"] = "B*(10*(N+1)*3*F_fwd + F_EL + 3*F_fwd) per iteration / ms_per_iteration"
     return {"config": "Be atom (4 e-), Adam: mc_step (10 sweeps) + energy gradient + Adam update, drop-in API",
             "walkers": walkers, "ms_per_iteration": 1e3 * dt, "iterations_per_s": 1.0 / dt,
-            "walker_steps_per_s": walkers * 10 / dt, "energy": float(loss_v), "finite": bool(math.isfinite(float(loss_v)))}
+            "walker_steps_per_s": walkers * 10 / dt, "energy": float(loss_v), "finite": bool(math.isfinite(float(loss_v))),
+            "roofline": rf}
 
 
 def load_pmc(lib_sha):
@@ -527,6 +618,7 @@ def main():
     peak = PEAK_FP32_TFLOPS if dtype == torch.float32 else PEAK_FP64_TFLOPS
     lib_sha = _lib.library_sha16()
     pmc, pmc_reason = load_pmc(lib_sha)
+    pmc_side = load_pmc_side(lib_sha)
 
     def rooflines(m):
         B = m["B"]
@@ -635,17 +727,17 @@ def main():
                               "allreduce_calls_before_side_benches": constants.ALLREDUCE_CALLS}
         if world == 1 and not args.no_ecp:
             try:
-                out["ecp_c_atom"] = ecp_side_bench(dtype, dev, 4096, 5, not args.no_cpu_baseline)
+                out["ecp_c_atom"] = ecp_side_bench(dtype, dev, 4096, 5, not args.no_cpu_baseline, pmc_side=pmc_side)
             except Exception as e:  # a side measurement, never a failure of the headline bench
                 out["ecp_c_atom"] = {"error": repr(e)}
             try:
-                out["ecp_c2"] = ecp_side_bench(dtype, dev, 4096, 3, False, name="C2_ecp")
+                out["ecp_c2"] = ecp_side_bench(dtype, dev, 4096, 3, False, name="C2_ecp", pmc_side=pmc_side)
             except Exception as e:  # a side measurement, never a failure of the headline bench
                 out["ecp_c2"] = {"error": repr(e)}
         if world == 1 and not args.no_adam:
             try:
                 c0 = constants.ALLREDUCE_CALLS
-                out["adam_be_atom"] = adam_side_bench(dtype, dev, 4096, 5)
+                out["adam_be_atom"] = adam_side_bench(dtype, dev, 4096, 5, pmc_side=pmc_side)
                 # forced collectives: the fused training step's 3 all-reduces per iteration (plus the
                 # MC loop's none) over the process group's backend
                 out["adam_be_atom"]["allreduce_calls"] = constants.ALLREDUCE_CALLS - c0
@@ -658,11 +750,11 @@ def main():
                 out["pp_adam_c_atom"] = {"error": repr(e)}
         if world == 1 and not args.no_dmc:
             try:
-                out["dmc_c_atom"] = dmc_side_bench(dtype, dev, 4096, 5)
+                out["dmc_c_atom"] = dmc_side_bench(dtype, dev, 4096, 5, pmc_side=pmc_side)
             except Exception as e:  # a side measurement, never a failure of the headline bench
                 out["dmc_c_atom"] = {"error": repr(e)}
             try:
-                out["dmc_ne_atom"] = dmc_side_bench(dtype, dev, 4096, 5, system="Ne")
+                out["dmc_ne_atom"] = dmc_side_bench(dtype, dev, 4096, 5, system="Ne", pmc_side=pmc_side)
             except Exception as e:  # a side measurement, never a failure of the headline bench
                 out["dmc_ne_atom"] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:

@@ -64,6 +64,31 @@ def _be_training(B, dtype=torch.float64, lo=0, hi=None, seed=7):
     return s, network, params, data, ev, step, le
 
 
+def _pp_training(B, dtype=torch.float64):
+    """C atom ccECP with the pp drivers' loss (complex E_L, complex_output=True), B walkers."""
+    from aiqmc import systems
+    from aiqmc.Energy import pphamiltonian
+    from aiqmc.Loss import loss as L
+    from aiqmc.VMC.VMCmcstep import PhiloxKey
+    from aiqmc.wavefunction_Ynlm import nn
+    from aiqmc.initial_electrons_positions.init import init_electrons
+    s = systems.make_system("C_ecp")
+    network = s.make_network()
+    params = network.init(4)
+    e = systems.ccecp_tables("C_ecp")
+    log_network = nn.make_log_network(network.apply)
+    le = pphamiltonian.local_energy(f=network.apply, lognetwork=log_network, charges=s.charges, nspins=s.spins,
+                                    rn_local=e.rn_local, local_coes=e.local_coes, local_exps=e.local_exps,
+                                    rn_non_local=e.rn_non_local, non_local_coes=e.non_local_coes,
+                                    non_local_exps=e.non_local_exps, natoms=1, nelectrons=4, ndim=3, list_l=2)
+    ev = L.make_loss(network=log_network, local_energy=le, clip_local_energy=5.0, clip_from_median=False,
+                     center_at_clipped_energy=True, complex_output=True)
+    ev._aiqmc_local_energy = le
+    pos, sp = init_electrons(17, None, s.atoms, s.charges, s.spins, B, 1.0)
+    data = nn.AINetData(positions=pos.to("cuda", dtype).contiguous(), spins=sp, atoms=s.atoms, charges=s.charges)
+    return ev, params, data, PhiloxKey(23, 5), network.apply._aiqmc_network
+
+
 _RCCL_WORKER = r'''
 import os, sys
 sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2]); sys.path.insert(0, os.path.join(sys.argv[1], "tests"))
@@ -113,6 +138,22 @@ for tag, dt in (("f64", torch.float64), ("f32", torch.float32)):
     constants.force_collectives(False)
     _, p2, _, _, _ = step(data, params, None, 0)
     out[tag + "_params"] = np.stack([nn.flatten_params(p1), nn.flatten_params(p2)])
+# 3. complex local energies (C atom ccECP, complex_output=True): the phase-gradient weights too
+ev, params, data, key, net = T._pp_training(128)
+e_l, _ = ev._aiqmc_local_energy(params, key, data)
+ctx = net.bind(params, data.atoms, torch.float64)
+x = data.positions.reshape(128, -1)
+gfn = lambda w, wp: (ctx.param_grad_weighted(x, w), ctx.param_grad_weighted(x, wp[None], phase=True)[0])
+constants.force_collectives(True)
+c0 = constants.ALLREDUCE_CALLS
+(l1, a1), g1 = ev.value_and_pmean_grad(params, key, data)
+out["pp_calls"] = constants.ALLREDUCE_CALLS - c0
+constants.force_collectives(False)
+l2, v2, c2, g2, im2 = L.fused_levels(e_l, gfn, 5.0, True, True)
+(l3, a3), g3 = ev.value_and_pmean_grad(params, key, data)
+out["pp_g"] = np.stack([g1.cpu().numpy(), g2.cpu().numpy(), g3.cpu().numpy()])
+out["pp_loss"] = np.array([complex(l1), complex(l2), complex(l3)])
+out["pp_imag"] = float(im2)
 torch.cuda.synchronize()
 np.savez(sys.argv[3], **out)
 dist.destroy_process_group()
@@ -149,6 +190,13 @@ def test_rccl_one_rank_group_is_bitwise_identity(tmp_path):
         p = o[tag + "_params"]
         if tag == "f64":
             np.testing.assert_allclose(p[0], p[1], rtol=0, atol=1e-9)
+    # complex energies: phase weights in the same three all-reduces
+    assert int(o["pp_calls"]) == 3 and o["pp_imag"] > 0
+    g = o["pp_g"]
+    np.testing.assert_array_equal(g[0], g[1])
+    np.testing.assert_allclose(g[0], g[2], rtol=0, atol=1e-10 * np.abs(g[2]).max())
+    lo = o["pp_loss"]
+    assert lo[0] == lo[1] and abs(lo[0] - lo[2]) <= 1e-12 * abs(lo[2])
 
 
 def test_bench_force_collectives_over_rccl_under_torchrun(tmp_path):

@@ -3,4 +3,4 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-bash tools/ab_bitwise.sh ${VARS:-base glds slp} 2>&1 | tee gpurun_out/r6c_ab.txt
+bash tools/ab_bitwise.sh ${VARS:-base lpf} 2>&1 | tee gpurun_out/r6c_ab.txt
