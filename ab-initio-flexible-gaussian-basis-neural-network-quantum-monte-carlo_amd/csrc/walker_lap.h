@@ -96,16 +96,13 @@ struct StageRegs {
 };
 // local-energy stage prefetch (round 6, interleaved A/B on one box, N2 4096 walkers, µs per E_L
 // pair: 194.7 / 195.1 -> 192.2 / 191.3, E_L and positions bitwise equal;
-// profiles/r06_s2_ab_lap_prefetch.txt).  -DAQ_LAP_NO_PREFETCH: the synchronous stage_copy.
+// profiles/r06_s2_ab_lap_prefetch.txt).  -DAQ_LAP_NO_PREFETCH: the synchronous stage_copy.  Layer
+// 0's block kept in registers over the per-electron stage and E2's Phi row loaded with Q_f as well:
+// 190.1 / 189.4 vs 189.9 / 190.0, not bitwise (operand order); not kept (profiles/r06_s3_ab_lap_prefetch2.txt).
 #ifndef AQ_LAP_NO_PREFETCH
 constexpr bool kLapPrefetch = true;
 #else
 constexpr bool kLapPrefetch = false;
-#endif
-#ifdef AQ_LAP_PREFETCH2
-constexpr bool kLapPrefetch2 = kLapPrefetch;
-#else
-constexpr bool kLapPrefetch2 = false;
 #endif
 
 // One h-stream layer (nn.py:280-311) in first derivatives, column loop over electrons i.
@@ -390,15 +387,8 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
 #pragma unroll
   for (int m = 0; m < D0; ++m) h0b[m] = Lc[LC::h0b + le * D0 + m];
   static_assert(LC::layer_n * sizeof(T) % 16 == 0 && SM::ly * sizeof(T) % 16 == 0, "16-byte staging");
-  // kLapPrefetch2: layer 0's block stays in registers over the per-electron stage (its latency
-  // behind that VALU work) and goes to LDS just before layer 0 reads it
-  StageRegs<T, LC::layer_n> l0;
-  if constexpr (kLapPrefetch2) {
-    l0.load(Lc);
-  } else {
-    stage_copy<T>(ly, Lc, LC::layer_n);
-    __syncthreads();
-  }
+  stage_copy<T>(ly, Lc, LC::layer_n);
+  __syncthreads();
 
   // ------------------------------------------------------------------ per-electron stage (electron.h)
   ElecOut<T, A> eo;
@@ -427,10 +417,6 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
   // kLapPrefetch: each staged block's loads are issued one phase ahead (into spare VGPRs: the kernel
   // runs at 2 waves/SIMD, 256 VGPRs each) and written to LDS after the barrier that frees it, so
   // no wave waits a whole L2/HBM round trip at a stage boundary
-  if constexpr (kLapPrefetch2) {
-    l0.store(ly);
-    __syncthreads();
-  }
   StageRegs<T, LC::layer_n> lnext;
   if constexpr (kLapPrefetch) lnext.load(Lc + LC::layer_n);
   lap_layer<T, N, A, 0>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W);
@@ -449,15 +435,9 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
   __syncthreads();
   StageRegs<T, 8 * N * N> qnext;
   StageRegs<T, (SM::stage_b ? 2 * N * N : 4)> bnext;
-  // kLapPrefetch2: E2's Phi row of electron le as well
-  T phrow[2 * N];
   if constexpr (kLapPrefetch) {
     qnext.load(Lc + LC::qs);
     if constexpr (SM::stage_b) bnext.load(Lc + LC::bm);
-  }
-  if constexpr (kLapPrefetch2) {
-#pragma unroll
-    for (int j = 0; j < 2 * N; ++j) phrow[j] = Lc[LC::ph + le * 2 * N + j];
   }
   lap_layer<T, N, A, 2>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W);
   if (W > 1) __syncthreads();   // the determinant terms read every wave's columns of dh/dx
@@ -507,8 +487,7 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
   T wbr = T(0), wbi = T(0), t2 = T(0);
 #pragma unroll
   for (int col = 0; col < N; ++col) {
-    const T pr = kLapPrefetch2 ? phrow[2 * col] : Ph[(le * N + col) * 2];
-    const T pm = kLapPrefetch2 ? phrow[2 * col + 1] : Ph[(le * N + col) * 2 + 1];
+    const T pr = Ph[(le * N + col) * 2], pm = Ph[(le * N + col) * 2 + 1];
     const T br = Bu[(col * N + le) * 2], bi = Bu[(col * N + le) * 2 + 1];
     wr[col] = pr * Yd1[col];
     wi[col] = pm * Yd1[col];

@@ -270,3 +270,22 @@ def test_two_rank_adam_step_equals_concatenated_batch(tmp_path, world):
         assert abs(float(o["var"]) - float(aux_ref.variance)) <= 1e-10 * float(aux_ref.variance)
         np.testing.assert_allclose(o["clipped"], cl_ref[r * n:(r + 1) * n], rtol=1e-12, atol=1e-12)
         np.testing.assert_allclose(o["p"], p_ref, rtol=0, atol=1e-9)
+
+
+def test_complex_energies_need_complex_output_checked_after_the_step():
+    """Complex local energies with complex_output=False are the reference's error (loss.py:256-265).
+    The check is a device count carried in aux (no host read inside the loss) and raised by
+    make_training_step after its NaN test."""
+    from aiqmc.Loss import loss as L
+    from aiqmc.Optimizer import adam, optax_like as optax
+    ev, params, data, key, net = _pp_training(32)
+    le = ev._aiqmc_local_energy
+    bad = L.make_loss(network=le, local_energy=le,
+                      clip_local_energy=5.0, clip_from_median=False, center_at_clipped_energy=True,
+                      complex_output=False)
+    (loss, aux), g = bad.value_and_pmean_grad(params, key, data)
+    assert aux.imag_check is not None and int(aux.imag_check) > 0
+    opt = optax.chain(optax.scale_by_adam(b1=0.9, b2=0.999, eps=1e-8, eps_root=0.0), optax.scale(-1.))
+    step = adam.make_training_step(adam.make_opt_update_step(bad, opt))
+    with pytest.raises(NotImplementedError):
+        step(data, params, None, key)
