@@ -270,6 +270,15 @@ static inline unsigned prop_blocks(int nconf, int wpb) {
 // single-electron-moved configurations from the walker cache (quad_small.h): value only (pp
 // quadrature, N <= 8) or value + gradient (Metropolis proposals and walker launches, N <= 4),
 // several configurations per wave
+// AIQMC_WALK_SPLIT=0 keeps small-batch walker launches on one wave per walker (A/B timing)
+static bool walk_split_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("AIQMC_WALK_SPLIT");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v != 0;
+}
 // AIQMC_QUAD_GRAD=0 routes the packed proposals of 5 <= N <= 8 back to k_walker_rev (A/B timing)
 static bool quad_grad_off() {
   static const int off = [] {
@@ -348,6 +357,9 @@ static void walker_impl(int dtype, int mode, const KArgs& ka, int nconf, hipStre
                                               dim3(64 * RevWpb<float, true>::value),
                                               RevWpb<float, true>::value * SmemRev<float, N, A, kFwdReg>::bytes, s>>>(ka);
     }
+    else if (mode == MODE_GRAD && ka.walk_split && !ka.proposal && !ka.value_only && walk_split_on())
+      k_walker_rev<float, N, A, false, false, false, false, true><<<dim3(nconf), dim3(128), SmemRev<float, N, A>::bytes,
+                                                                  s>>>(ka);
     else if (mode == MODE_GRAD)
       k_walker_rev<float, N, A><<<dim3((nconf + RevWpb<float, false>::value - 1) / RevWpb<float, false>::value),
                                   dim3(64 * RevWpb<float, false>::value),

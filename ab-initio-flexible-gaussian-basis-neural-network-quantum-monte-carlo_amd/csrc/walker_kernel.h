@@ -296,6 +296,8 @@ struct KArgs {
   // walker launches of N <= 8 on k_walker_rev (one wave per walker) instead of the packed
   // k_quad_grad (aiqmc_debug_set_packed_walkers; A/B and parity)
   int one_wave;
+  // walker launch of a small batch as two waves per walker (k_walker_rev<..., SPL>: F1 and F2 at once)
+  int walk_split;
   // Metropolis caches (walker_rev.h WCache / ECache); nullptr outside aiqmc_mc_step
   void* wcache;
   void* ecache;

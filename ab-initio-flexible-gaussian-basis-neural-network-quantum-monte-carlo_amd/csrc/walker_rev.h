@@ -470,17 +470,131 @@ template <typename T, bool PROP, bool PREP = false> struct RevWpb {
   } while (0)
 #endif
 
+// One ordered pair (k, i) of B3 (walker_rev's pair adjoints): forward values (fresh) or the cached
+// t1, t2, then the adjoints back through the two double layers to d = x_i - x_k, into dbar
+// (a function so that both waves of a split walker launch can run it on their share of the pairs).
+// may_fresh (compile-time after unrolling): the pair may recompute its forward values; fresh
+// selects them per lane without a branch (a divergent branch here turned the uniform weights
+// into per-lane copies at the merge)
+template <typename T, int N, int A>
+__device__ __forceinline__ void b3_pair_adjoint(cptr<T> P, const T* xs, const T* g2b, T* dbar, int nup, int k, int i,
+                                                bool may_fresh, bool fresh, const T* tcache, T cusp, T al) {
+  using Ly = Lay<N, A>;
+  const T RSQ2 = T(0.70710678118654752);
+  // the uniform layer weights are re-read per pair from the scalar cache (s_load) instead of
+  // being kept in SGPRs across the kernel (which spills them through VALU lane writes)
+  cptr<T> Pq = P;
+  asm volatile("" : "+s"(Pq));
+  const int G = k >= nup ? 1 : 0;
+  T d[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) d[c] = xs[i * 3 + c] - xs[k * 3 + c];
+  const T r = f_sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+  T p0[4] = {r, d[0], d[1], d[2]};
+  T t1[4], t2[4];
+#pragma unroll
+  for (int o = 0; o < 4; ++o) {
+    t1[o] = tcache ? tcache[o] : T(0);
+    t2[o] = tcache ? tcache[4 + o] : T(0);
+  }
+  if (may_fresh) {
+    // recompute the two double layers (values)
+    T f1[4], p1[4], f2[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      T s = Pq[Ly::dbl_b0 + o];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) s += p0[m] * Pq[Ly::dbl_w0 + m * 4 + o];
+      f1[o] = f_tanh(s);
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) p1[o] = (p0[o] + f1[o]) * RSQ2;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      T s = Pq[Ly::dbl_b1 + o];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) s += p1[m] * Pq[Ly::dbl_w1 + m * 4 + o];
+      f2[o] = f_tanh(s);
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      t1[o] = fresh ? f1[o] : t1[o];
+      t2[o] = fresh ? f2[o] : t2[o];
+    }
+  }
+  // adjoints: output of layer l feeds g2[l][G][i] with weight 1/|G|
+  T pb2[4], pb1[4], pb0[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) pb2[f] = g2b[((2 * 2 + G) * N + i) * 4 + f];
+  T z2[4];
+#pragma unroll
+  for (int o = 0; o < 4; ++o) z2[o] = pb2[o] * RSQ2 * (T(1) - t2[o] * t2[o]);
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    T s = g2b[((1 * 2 + G) * N + i) * 4 + m] + pb2[m] * RSQ2;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) s += z2[o] * Pq[Ly::dbl_w1 + m * 4 + o];
+    pb1[m] = s;
+  }
+  T z1[4];
+#pragma unroll
+  for (int o = 0; o < 4; ++o) z1[o] = pb1[o] * RSQ2 * (T(1) - t1[o] * t1[o]);
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    T s = g2b[((0 * 2 + G) * N + i) * 4 + m] + pb1[m] * RSQ2;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) s += z1[o] * Pq[Ly::dbl_w0 + m * 4 + o];
+    pb0[m] = s;
+  }
+  // p0 = [r, d]; Pade e-e Jastrow once per unordered pair (k < i)
+  T rb = pb0[0];
+  {
+    // the pair's Jastrow parameters come loaded on every lane and are masked here (a branch
+    // around their loads waited for every load in flight, the cached tanh's included)
+    const T den = al * r + T(1);
+    rb += and_zero(k < i, cusp * f_rcp(den * den));
+  }
+  const T ir = f_rcp(r);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) dbar[(k * N + i) * 3 + c] = pb0[1 + c] + rb * d[c] * ir;
+}
+
+// The sweep's draws of walker conf (k_draws' arithmetic, fused into the walker launch)
+template <typename T, int N>
+__device__ __forceinline__ void walker_draws(const __attribute__((address_space(4))) KArgs* kl, int conf, int lane) {
+  if (kl->dg1 && lane < N) {
+    const uint32_t t = (uint32_t)(conf * N + lane);
+    const uint64_t seed = kl->seed, step = kl->step;
+    float a[3], b[3], c[4];
+    philox_normal3f(seed, step, t, 0u, a);
+    philox_normal3f(seed, step, t, 1u, b);
+    philox_u4(seed, step, t, 2u, c);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      ((T*)kl->dg1)[(size_t)t * 3 + k] = (T)a[k];
+      ((T*)kl->dg2)[(size_t)t * 3 + k] = (T)b[k];
+    }
+    ((T*)kl->du)[t] = (T)(c[0] - 5.9604644775390625e-08f);
+  }
+}
+
 // PW7 (proposals only, -DAQ_PW7 builds: measured slower, shape.hip): the small-batch instantiation, compiled for 7 waves/SIMD with the COMPACT
 // LDS layout, so that the B N proposals of a strong-scaling rank (512 N2 walkers: 7,168 waves) run
 // in one round instead of 1.4 (shape.hip chooses it by batch size)
 // PH (PREP only): the adjoint pass of the PHASE -- seeded by Im d log det / dH instead of Re, so
 // that the LapCache's node weights, feature adjoints and pair-local curvature are those of
 // theta = arg psi (the complex_output=True kinetic energy, hamiltonian.py:110-130)
-template <typename T, int N, int A, bool PREP = false, bool PROP = false, bool PW7 = false, bool PH = false>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * RevWpb<T, PROP, PREP>::value))) __attribute__((amdgpu_waves_per_eu(RevWaves<T, N, A, PREP, PROP, PW7>::value))) void
+// SPL (walker launches of small batches, shape.hip): two waves per walker -- wave 0 the
+// per-electron stage F1 and everything after F2, wave 1 the pair stream F2 (its walker-cache rows,
+// the column sums g2, J_ee) at the same time; wave 1 hands g2 and J_ee over through LDS at one
+// workgroup barrier and exits.  F1 and F2 depend on the positions only (nn.py:106-153).
+template <typename T, int N, int A, bool PREP = false, bool PROP = false, bool PW7 = false, bool PH = false,
+          bool SPL = false>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * (SPL ? 2 : RevWpb<T, PROP, PREP>::value)))) __attribute__((amdgpu_waves_per_eu(RevWaves<T, N, A, PREP, PROP, PW7>::value))) void
 k_walker_rev(KArgs ka) {
   static_assert(!PW7 || (PROP && !PREP), "PW7 is a proposal instantiation");
   static_assert(!PH || PREP, "PH is an adjoint-pass instantiation");
+  static_assert(!SPL || (!PROP && !PREP), "SPL is a walker-launch instantiation");
   using Ly = Lay<N, A>;
   constexpr bool fwd_reg = PROP && kFwdReg;
   constexpr bool compact = PROP && PW7 && fwd_reg;
@@ -491,18 +605,19 @@ k_walker_rev(KArgs ka) {
   using SM = SmemRev<T, N, A, fwd_reg, compact>;
   using LCc = LapCache<N, A>;
   constexpr int D0 = SM::D0;
-  constexpr int WPB = RevWpb<T, PROP, PREP>::value;
+  constexpr int WPB = SPL ? 2 : RevWpb<T, PROP, PREP>::value;
   const cptr<T> P = param_ptr<T>(ka.prm);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   // wave index within the workgroup, wave-uniform (scalar)
   const int wv = WPB > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
-  T* sm = (T*)(smem_raw + wv * SM::bytes);
+  // SPL: both waves work on one walker's LDS block
+  T* sm = (T*)(smem_raw + (SPL ? 0 : wv) * SM::bytes);
   T* xs = sm + SM::xs;
 
   // The PROP instantiation is launched only for proposals that read the walker cache (shape.hip
   // routes reuse-off proposals to the general one), so there both path flags are compile-time.
   const bool isprop = PROP ? true : (ka.proposal != 0);
-  const int conf = xcd_major(blockIdx.x, gridDim.x) * WPB + wv;
+  const int conf = SPL ? xcd_major(blockIdx.x, gridDim.x) : xcd_major(blockIdx.x, gridDim.x) * WPB + wv;
   if (WPB > 1 && conf >= ka.nconf) return;
   const int lane = WPB > 1 ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   const int lc = lane >> 4;
@@ -529,7 +644,9 @@ k_walker_rev(KArgs ka) {
   }
   // reuse-off proposals: the walker limdrift factor, read by the wave before the divergent F0
   const T te_walk = (!PROP && isprop && !ka.xnew) ? taueff_wave<T>(ka.taueff, ka.tacc, 0, ka.tstep, ka.tpart) : T(0);
-  if (!PREP && !isprop && ka.acc.lpn) {
+  if (SPL && wv != 0) {
+    // SPL wave 1: the positions come from wave 0 (after its acceptance) through LDS
+  } else if (!PREP && !isprop && ka.acc.lpn) {
     // the previous sweep's acceptance of this walker's N proposals (k_accept's arithmetic)
     const T te1 = taueff_wave<T>(ka.acc.taueff, ka.acc.tacc, 0, ka.acc.tstep, ka.acc.tpart);
     const T te2 = taueff_wave<T>(ka.acc.taueff, ka.acc.tacc, 1, ka.acc.tstep, ka.acc.tpart);
@@ -558,7 +675,8 @@ k_walker_rev(KArgs ka) {
     }
     xs[lane] = x;
   }
-  if constexpr (!PROP) AQ_SYNC();
+  if constexpr (SPL) __syncthreads();   // wave 1 reads the positions
+  else if constexpr (!PROP) AQ_SYNC();
 
   AQ_PH(0);
   // ------------------------------------------------------------------ F1 per-electron stage (electron.h)
@@ -729,7 +847,7 @@ k_walker_rev(KArgs ka) {
     for (int t = 0; t < NG; ++t)
       if (lane + 64 * t < 3 * 2 * N * 4) g2[lane + 64 * t] = rg[t];
     }
-  } else {
+  } else if (!SPL || wv == 0) {
     if (wfix) pvr = Wc[WC::pv + (lane < 3 * N + 2 ? lane : 3 * N + 1)];   // to LDS after F4, before F5's write
     ElecOut<T, A> eo;
     electron_stage<T, N, A>(P, xs + le * 3, le, lc, eo);
@@ -757,7 +875,7 @@ k_walker_rev(KArgs ka) {
     }
   }
   AQ_SYNC();
-  if (!PREP && !isprop) {
+  if (!PREP && !isprop && (!SPL || wv == 0)) {
     for (int idx = lane; idx < N * N; idx += 64) Wc[WC::yv + idx] = Yv[idx];
     for (int idx = lane; idx < N * D0; idx += 64) Wc[WC::h0 + idx] = sm[SM::hl + idx];
   }
@@ -807,7 +925,7 @@ k_walker_rev(KArgs ka) {
       }
       g2[((l * 2 + G) * N + pi) * 4 + f] += acc * (G ? ginv1 : ginv0);
     }
-  } else if (!reuse) {
+  } else if (!reuse && (!SPL || wv == 1)) {
     {
       const int i = lane >> 2, kq = lane & 3;
       const bool icol = i < N;
@@ -880,10 +998,35 @@ k_walker_rev(KArgs ka) {
     }
   }
   AQ_SYNC();
-  if (!PREP && !isprop) {
+  if (!PREP && !isprop && (!SPL || wv == 1)) {
     for (int idx = lane; idx < 3 * 2 * N * 4; idx += 64) Wc[WC::g2 + idx] = g2[idx];
     const T je = wave_sum(jve);
     if (lane == 0) Wc[WC::jee] = je;
+    if (SPL) sm[SM::R + lane] = jve;   // per lane, so that wave 0's sums keep their order (region R is free until F5)
+  }
+  if constexpr (SPL) {
+    __syncthreads();   // wave 0 has the stage (F1), wave 1 the pair sums g2 and J_ee (F2)
+    if (wv != 0) {
+      // wave 1: the sweep's draws of this walker, then its half of B3 once wave 0 has the
+      // adjoints g2b (B2) -- the pairs it = 64 + lane, 192 + lane, ... (wave 0 takes the others)
+      walker_draws<T, N>(late_args(), conf, lane);
+      if (ka.wcache) {
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        constexpr int NPR = N * (N - 1);
+        for (int it = 64 + lane; it < NPR; it += 128) {
+          const int k = it / (N - 1);
+          const int jj = it - k * (N - 1);
+          const int i = jj + (jj >= k ? 1 : 0);
+          b3_pair_adjoint<T, N, A>(P, xs, sm + SM::g2, sm + SM::dbar, nup, k, i, false, false,
+                                   Wc + WC::pt + (k * N + i) * 8, P[Ly::jee_c + k * N + i], P[Ly::jee_a + k * N + i]);
+        }
+        __syncthreads();
+      }
+      return;
+    }
+    jve = sm[SM::R + lane];
   }
 
   AQ_PH(2);
@@ -1851,86 +1994,8 @@ k_walker_rev(KArgs ka) {
   // from walker pb's cache, so iterations >= 1 skip the forward recompute.
   // one ordered pair (k, i): forward values (fresh) or the cached t1, t2 of walker pb, then the
   // adjoints back through the two double layers to d = x_i - x_k
-  // may_fresh (compile-time after unrolling): the pair may recompute its forward values; fresh
-  // selects them per lane without a branch (a divergent branch here turned the uniform weights
-  // into per-lane copies at the merge)
   auto pair_adjoint = [&](int k, int i, bool may_fresh, bool fresh, const T* tcache, T cusp, T al) {
-    // the uniform layer weights are re-read per pair from the scalar cache (s_load) instead of
-    // being kept in SGPRs across the kernel (which spills them through VALU lane writes)
-    cptr<T> Pq = P;
-    asm volatile("" : "+s"(Pq));
-    const int G = k >= nup ? 1 : 0;
-    T d[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) d[c] = xs[i * 3 + c] - xs[k * 3 + c];
-    const T r = f_sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
-    T p0[4] = {r, d[0], d[1], d[2]};
-    T t1[4], t2[4];
-#pragma unroll
-    for (int o = 0; o < 4; ++o) {
-      t1[o] = tcache ? tcache[o] : T(0);
-      t2[o] = tcache ? tcache[4 + o] : T(0);
-    }
-    if (may_fresh) {
-      // recompute the two double layers (values)
-      T f1[4], p1[4], f2[4];
-#pragma unroll
-      for (int o = 0; o < 4; ++o) {
-        T s = Pq[Ly::dbl_b0 + o];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) s += p0[m] * Pq[Ly::dbl_w0 + m * 4 + o];
-        f1[o] = f_tanh(s);
-      }
-#pragma unroll
-      for (int o = 0; o < 4; ++o) p1[o] = (p0[o] + f1[o]) * RSQ2;
-#pragma unroll
-      for (int o = 0; o < 4; ++o) {
-        T s = Pq[Ly::dbl_b1 + o];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) s += p1[m] * Pq[Ly::dbl_w1 + m * 4 + o];
-        f2[o] = f_tanh(s);
-      }
-#pragma unroll
-      for (int o = 0; o < 4; ++o) {
-        t1[o] = fresh ? f1[o] : t1[o];
-        t2[o] = fresh ? f2[o] : t2[o];
-      }
-    }
-    // adjoints: output of layer l feeds g2[l][G][i] with weight 1/|G|
-    T pb2[4], pb1[4], pb0[4];
-#pragma unroll
-    for (int f = 0; f < 4; ++f) pb2[f] = g2b[((2 * 2 + G) * N + i) * 4 + f];
-    T z2[4];
-#pragma unroll
-    for (int o = 0; o < 4; ++o) z2[o] = pb2[o] * RSQ2 * (T(1) - t2[o] * t2[o]);
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      T s = g2b[((1 * 2 + G) * N + i) * 4 + m] + pb2[m] * RSQ2;
-#pragma unroll
-      for (int o = 0; o < 4; ++o) s += z2[o] * Pq[Ly::dbl_w1 + m * 4 + o];
-      pb1[m] = s;
-    }
-    T z1[4];
-#pragma unroll
-    for (int o = 0; o < 4; ++o) z1[o] = pb1[o] * RSQ2 * (T(1) - t1[o] * t1[o]);
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      T s = g2b[((0 * 2 + G) * N + i) * 4 + m] + pb1[m] * RSQ2;
-#pragma unroll
-      for (int o = 0; o < 4; ++o) s += z1[o] * Pq[Ly::dbl_w0 + m * 4 + o];
-      pb0[m] = s;
-    }
-    // p0 = [r, d]; Pade e-e Jastrow once per unordered pair (k < i)
-    T rb = pb0[0];
-    {
-      // the pair's Jastrow parameters come loaded on every lane and are masked here (a branch
-      // around their loads waited for every load in flight, the cached tanh's included)
-      const T den = al * r + T(1);
-      rb += and_zero(k < i, cusp * f_rcp(den * den));
-    }
-    const T ir = f_rcp(r);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) dbar[(k * N + i) * 3 + c] = pb0[1 + c] + rb * d[c] * ir;
+    b3_pair_adjoint<T, N, A>(P, xs, g2b, dbar, nup, k, i, may_fresh, fresh, tcache, cusp, al);
   };
   constexpr int NPR = N * (N - 1);
   if (reuse && !AQ_ABL(32)) {
@@ -1970,15 +2035,18 @@ k_walker_rev(KArgs ka) {
   } else if (!reuse) {
     if (!PREP && !isprop && ka.wcache) {
       // walker launch of a sweep: F2 has just written every pair's tanh outputs to the walker
-      // cache; read them back instead of recomputing the two double layers
+      // cache; read them back instead of recomputing the two double layers.  SPL: wave 1 (waiting
+      // at this barrier since F2) takes the odd 64-pair blocks
+      if constexpr (SPL) __syncthreads();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      for (int it = lane; it < NPR; it += 64) {
+      for (int it = lane; it < NPR; it += SPL ? 128 : 64) {
         const int k = it / (N - 1);
         const int jj = it - k * (N - 1);
         const int i = jj + (jj >= k ? 1 : 0);
         pair_adjoint(k, i, false, false, Wc + WC::pt + (k * N + i) * 8, P[Ly::jee_c + k * N + i], P[Ly::jee_a + k * N + i]);
       }
+      if constexpr (SPL) __syncthreads();   // wave 1's share of dbar is in LDS
     } else {
       for (int it = lane; it < NPR; it += 64) {
         const int k = it / (N - 1);
@@ -2029,21 +2097,8 @@ k_walker_rev(KArgs ka) {
     if (kl->sumsq) ((T*)kl->sumsq)[conf] = sumsq;
     if (kl->tacc) tacc_add(kl->tacc, isprop ? 1 : 0, conf, (double)sumsq);
   }
-  if constexpr (!PREP) {
-    if (kl->dg1 && !isprop && lane < N) {   // the sweep's draws of walker conf (k_draws)
-      const uint32_t t = (uint32_t)(conf * N + lane);
-      const uint64_t seed = kl->seed, step = kl->step;
-      float a[3], b[3], c[4];
-      philox_normal3f(seed, step, t, 0u, a);
-      philox_normal3f(seed, step, t, 1u, b);
-      philox_u4(seed, step, t, 2u, c);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        ((T*)kl->dg1)[(size_t)t * 3 + k] = (T)a[k];
-        ((T*)kl->dg2)[(size_t)t * 3 + k] = (T)b[k];
-      }
-      ((T*)kl->du)[t] = (T)(c[0] - 5.9604644775390625e-08f);
-    }
+  if constexpr (!PREP && !SPL) {   // SPL: wave 1 made them
+    if (!isprop) walker_draws<T, N>(kl, conf, lane);
   }
   AQ_PH(9);
 }
