@@ -18,7 +18,7 @@ SIDES = {
     "ecp_c": ["k_quad_value<float, 4, 1>"],
     "ecp_c2": ["k_quad_value<float, 8, 2>"],
     "adam_be": ["k_quad_grad<float, 4, 1, false>"],
-    "dmc_ne": ["k_walker_rev<float, 10, 1, true, false, false, false>", "k_walker_lap<float, 10, 1, 1, false>"],
+    "dmc_ne": ["k_walker_rev<float, 10, 1, true, false", "k_walker_lap<float, 10, 1, 1, false>"],
 }
 PASSES = ("fetch", "write", "mix")
 

@@ -40,7 +40,8 @@ def rows(path):
             yield (r[0], int(r[1]) // max(1, int(r[2])), r[3] / 1e3, int(r[2]),
                    {"vgpr": r[4], "agpr": r[5], "sgpr": r[6], "lds_bytes": r[7], "scratch": r[8]})
         return
-    for t in csv.DictReader(open(os.path.join(path, "run_kernel_trace.csv"))):
+    traces = sorted(glob.glob(os.path.join(path, "*kernel_trace.csv")))
+    for t in csv.DictReader(open(traces[0])):
         yield (t["Kernel_Name"], int(t["Grid_Size_X"]) // max(1, int(t["Workgroup_Size_X"])),
                (int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) / 1e3, int(t["Workgroup_Size_X"]),
                {"vgpr": int(t["VGPR_Count"]), "agpr": int(t["Accum_VGPR_Count"]), "sgpr": int(t["SGPR_Count"]),
