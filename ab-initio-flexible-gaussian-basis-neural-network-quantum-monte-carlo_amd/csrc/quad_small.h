@@ -75,8 +75,21 @@ struct SmemQ {
   static constexpr int g2 = hl + NI * D0;         // [3][2][N][4] pair column means
   static constexpr int S = g2 + 3 * 2 * NI * 4;   // [NI][12]  new - old pair values (o, pi) of the patch
   static constexpr int h3 = S + NI * 12;          // [N][4]    h-stream output
-  static constexpr int size = h3 + NI * 4;
+  static constexpr int pv = h3 + NI * 4;          // [2N+1]    the walker's pivot record (fixed-order LU)
+  static constexpr int size = pv + 2 * NI + 4;
 };
+
+// k_quad_value's determinant by LU in the walker's pivot order (the record its walker launch wrote,
+// gj.h layout: row of step k, 1 / |pivot_k|, the order's parity) instead of partial pivoting: no
+// pivot search per step.  A slot whose pivot k falls below 0.1 of its walker's (or out of the float
+// range) reruns the pivoted LU.  A quadrature configuration moves one electron far (onto the sphere
+// around an atom), and still 2.9 % of C2 ccECP configurations need the rerun (CPU experiment on the
+// fp64 oracle's matrices).  -DAQ_QUAD_PIVOTED: the pivoted LU always.
+#ifndef AQ_QUAD_PIVOTED
+constexpr bool kQuadFixedLU = true;
+#else
+constexpr bool kQuadFixedLU = false;
+#endif
 
 // F1 of the packed kernels: walker pb's cached stage (positions X, walker cache Wc) with electron
 // pi's entries from its moved-electron record Eq, into the slot's LDS block.  Every load is
@@ -172,6 +185,10 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
   // ---------------------------------------------------------------- F1 cached stage of walker pb
   T jsum = quad_stage_load<T, N, A, SW>((const T*)ka.pos + (size_t)pb * 3 * N, Wc, Eq, pi, sl, xs, sm + SQ::xo,
                                         Yv, hl, g2);
+  if constexpr (kQuadFixedLU) {   // the walker's pivot record (order, 1 / |pivot|, parity) for F5
+    const T v = Wc[WC::pv + (sl < 2 * N + 1 ? sl : 2 * N)];
+    if (sl < 2 * N + 1) sm[SQ::pv + sl] = v;
+  }
   wave_sync();
 
   // ---------------------------------------------------------------- F2 pairs of the moved electron
@@ -307,6 +324,17 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
   // lane c < NI of the slot's first 16-lane row holds column c; column k comes by DPP row_newbcast
   T lsum = T(0), ur = T(1), ui = T(0);
   int inv = 0;
+  // one LU step's pivot bookkeeping: log|pivot|^2, the running phase, 1 / pivot
+  auto pivot_step = [&](T pr, T pim, T& ipr, T& ipi, T& rabs) {
+    const T den = pr * pr + pim * pim;
+    T lden;
+    pivot_recip(pr, pim, den, ipr, ipi, rabs, lden);
+    lsum += lden;
+    const T xr = pr * rabs, xi = pim * rabs;
+    const T nr = ur * xr - ui * xi, ni = ur * xi + ui * xr;
+    ur = nr;
+    ui = ni;
+  };
   if constexpr (SW == 16) {
     // N <= 4: one element per lane, lane 4r + c of the row holds A[r][c].  The pivot row of
     // column k is the max of packed keys over the column's four lanes (bits of |re| + |im| with
@@ -315,7 +343,7 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
     // the pivot row's entry of this lane's column by one lane permute.
     const int r = sl >> 2, c = sl & 3;
     const bool rl = r < N;
-    T a = T(0), b = T(0);
+    T a0 = T(0), b0 = T(0);
     if (rl && c < N) {
       const int src = ka.rowsrc[r];
       const int sp = r < nup ? 0 : 1;
@@ -327,48 +355,75 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
         im += hv * P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 1];
       }
       const T y = Yv[r * N + c];
-      a = re * y;
-      b = im * y;
+      a0 = re * y;
+      b0 = im * y;
     }
     const int rowbase = lane & ~15;
-    unsigned used = 0;
+    auto pivoted = [&]() {
+      T a = a0, b = b0;
+      lsum = T(0);
+      ur = T(1);
+      ui = T(0);
+      inv = 0;
+      unsigned used = 0;
 #pragma unroll
-    for (int k = 0; k < N; ++k) {
-      const T akr = k == 0 ? quad_bcast<0>(a) : (k == 1 ? quad_bcast<1>(a) : (k == 2 ? quad_bcast<2>(a) : quad_bcast<3>(a)));
-      const T aki = k == 0 ? quad_bcast<0>(b) : (k == 1 ? quad_bcast<1>(b) : (k == 2 ? quad_bcast<2>(b) : quad_bcast<3>(b)));
-      const bool open = rl && !((used >> r) & 1u);
-      unsigned key = open ? ((key_bits(f_abs(akr) + f_abs(aki)) & ~3u) | (unsigned)(3 - r)) : 0u;
-      {
-        const unsigned k4 = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x124, 0xF, 0xF, true);
-        key = key > k4 ? key : k4;
-        const unsigned k8 = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x128, 0xF, 0xF, true);
-        key = key > k8 ? key : k8;
+      for (int k = 0; k < N; ++k) {
+        const T akr = k == 0 ? quad_bcast<0>(a) : (k == 1 ? quad_bcast<1>(a) : (k == 2 ? quad_bcast<2>(a) : quad_bcast<3>(a)));
+        const T aki = k == 0 ? quad_bcast<0>(b) : (k == 1 ? quad_bcast<1>(b) : (k == 2 ? quad_bcast<2>(b) : quad_bcast<3>(b)));
+        const bool open = rl && !((used >> r) & 1u);
+        unsigned key = open ? ((key_bits(f_abs(akr) + f_abs(aki)) & ~3u) | (unsigned)(3 - r)) : 0u;
+        {
+          const unsigned k4 = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x124, 0xF, 0xF, true);
+          key = key > k4 ? key : k4;
+          const unsigned k8 = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x128, 0xF, 0xF, true);
+          key = key > k8 ? key : k8;
+        }
+        const int p = 3 - (int)(key & 3u);
+        const T p0r = row_bcast(a, k), p1r = row_bcast(a, 4 + k), p2r = row_bcast(a, 8 + k), p3r = row_bcast(a, 12 + k);
+        const T p0i = row_bcast(b, k), p1i = row_bcast(b, 4 + k), p2i = row_bcast(b, 8 + k), p3i = row_bcast(b, 12 + k);
+        const T pr = p == 0 ? p0r : (p == 1 ? p1r : (p == 2 ? p2r : p3r));
+        const T pim = p == 0 ? p0i : (p == 1 ? p1i : (p == 2 ? p2i : p3i));
+        const T er = __shfl(a, rowbase + 4 * p + c), ei = __shfl(b, rowbase + 4 * p + c);   // A[p][c]
+        inv += __builtin_popcount(used >> p);
+        used |= 1u << p;
+        T ipr, ipi, rabs;
+        pivot_step(pr, pim, ipr, ipi, rabs);   // 1 / pivot
+        if (rl && !((used >> r) & 1u)) {   // rows still open: A[r][:] -= (A[r][k] / pivot) A[p][:]
+          const T mr = akr * ipr - aki * ipi, mi = akr * ipi + aki * ipr;
+          a -= mr * er - mi * ei;
+          b -= mr * ei + mi * er;
+        }
       }
-      const int p = 3 - (int)(key & 3u);
-      const T p0r = row_bcast(a, k), p1r = row_bcast(a, 4 + k), p2r = row_bcast(a, 8 + k), p3r = row_bcast(a, 12 + k);
-      const T p0i = row_bcast(b, k), p1i = row_bcast(b, 4 + k), p2i = row_bcast(b, 8 + k), p3i = row_bcast(b, 12 + k);
-      const T pr = p == 0 ? p0r : (p == 1 ? p1r : (p == 2 ? p2r : p3r));
-      const T pim = p == 0 ? p0i : (p == 1 ? p1i : (p == 2 ? p2i : p3i));
-      const T er = __shfl(a, rowbase + 4 * p + c), ei = __shfl(b, rowbase + 4 * p + c);   // A[p][c]
-      inv += __builtin_popcount(used >> p);
-      used |= 1u << p;
-      const T den = pr * pr + pim * pim;
-      T ipr_, ipi_, rabs_, lden_;
-      pivot_recip(pr, pim, den, ipr_, ipi_, rabs_, lden_);
-      lsum += lden_;
-      {
-        const T rm = rabs_;
-        const T xr = pr * rm, xi = pim * rm;
-        const T nr = ur * xr - ui * xi, ni = ur * xi + ui * xr;
-        ur = nr;
-        ui = ni;
+    };
+    if constexpr (kQuadFixedLU) {
+      // the walker's order: pivot row p of step k and 1 / |walker pivot k| from the slot's LDS copy
+      T a = a0, b = b0;
+      bool bad = false, done = false;
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        const T akr = k == 0 ? quad_bcast<0>(a) : (k == 1 ? quad_bcast<1>(a) : (k == 2 ? quad_bcast<2>(a) : quad_bcast<3>(a)));
+        const T aki = k == 0 ? quad_bcast<0>(b) : (k == 1 ? quad_bcast<1>(b) : (k == 2 ? quad_bcast<2>(b) : quad_bcast<3>(b)));
+        const int p = (int)sm[SQ::pv + k];
+        const T rk = sm[SQ::pv + N + k];
+        const T er = __shfl(a, rowbase + 4 * p + c), ei = __shfl(b, rowbase + 4 * p + c);   // A[p][c]
+        // A[p][k]: lane c = k of this quad holds it in er
+        const T pr = k == 0 ? quad_bcast<0>(er) : (k == 1 ? quad_bcast<1>(er) : (k == 2 ? quad_bcast<2>(er) : quad_bcast<3>(er)));
+        const T pim = k == 0 ? quad_bcast<0>(ei) : (k == 1 ? quad_bcast<1>(ei) : (k == 2 ? quad_bcast<2>(ei) : quad_bcast<3>(ei)));
+        done = done || (p == r);
+        T ipr, ipi, rabs;
+        pivot_step(pr, pim, ipr, ipi, rabs);
+        bad = bad || !(rk >= T(0.1) * rabs);   // |pivot| below 0.1 of the walker's (or not finite)
+        if (rl && !done) {
+          const T mr = akr * ipr - aki * ipi, mi = akr * ipi + aki * ipr;
+          a -= mr * er - mi * ei;
+          b -= mr * ei + mi * er;
+        }
       }
-      const T ipr = ipr_, ipi = ipi_;   // 1 / pivot
-      if (rl && !((used >> r) & 1u)) {   // rows still open: A[r][:] -= (A[r][k] / pivot) A[p][:]
-        const T mr = akr * ipr - aki * ipi, mi = akr * ipi + aki * ipr;
-        a -= mr * er - mi * ei;
-        b -= mr * ei + mi * er;
-      }
+      inv = (int)sm[SQ::pv + 2 * N];
+      const unsigned long long bm = __ballot(bad);
+      if ((bm >> (lane & ~(SW - 1))) & ((1ull << SW) - 1ull)) pivoted();   // this slot: partial pivoting
+    } else {
+      pivoted();
     }
   } else {
     // 5 <= N <= 8: lane 4r + g of the slot holds A[r][g] and A[r][g + 4] (row r, two columns).
@@ -378,12 +433,12 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
     // two entries of this lane's columns come by lane permutes.
     const int r = sl >> 2, g = sl & 3;
     const bool rl = r < N;
-    T a[2], b[2];
+    T a0[2], b0[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int c = g + 4 * h;
-      a[h] = T(0);
-      b[h] = T(0);
+      a0[h] = T(0);
+      b0[h] = T(0);
       if (rl && c < N) {
         const int src = ka.rowsrc[r];
         const int sp = r < nup ? 0 : 1;
@@ -395,31 +450,15 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
           im += hv * P[Ly::orb_w + ((sp * 4 + f) * N + c) * 2 + 1];
         }
         const T y = Yv[r * N + c];
-        a[h] = re * y;
-        b[h] = im * y;
+        a0[h] = re * y;
+        b0[h] = im * y;
       }
     }
     const int sbase = lane & ~31;
-    unsigned used = 0;
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
+    // one step of either order: eliminate column k with pivot row p (rows still open: A[r][:] -=
+    // (A[r][k] / pivot) A[p][:])
+    auto lu_step = [&](int k, int p, T* a, T* b, bool open_after, T akr, T aki, T& rabs) {
       const int kh = k >> 2;
-      T akr, aki;   // A[r][k]
-      if ((k & 3) == 0) { akr = quad_bcast<0>(a[kh]); aki = quad_bcast<0>(b[kh]); }
-      else if ((k & 3) == 1) { akr = quad_bcast<1>(a[kh]); aki = quad_bcast<1>(b[kh]); }
-      else if ((k & 3) == 2) { akr = quad_bcast<2>(a[kh]); aki = quad_bcast<2>(b[kh]); }
-      else { akr = quad_bcast<3>(a[kh]); aki = quad_bcast<3>(b[kh]); }
-      const bool open = rl && !((used >> r) & 1u);
-      unsigned key = open ? ((key_bits(f_abs(akr) + f_abs(aki)) & ~7u) | (unsigned)(7 - r)) : 0u;
-      {
-        const unsigned k4 = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x124, 0xF, 0xF, true);
-        key = key > k4 ? key : k4;
-        const unsigned k8 = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x128, 0xF, 0xF, true);
-        key = key > k8 ? key : k8;
-        const unsigned k16 = (unsigned)__shfl_xor((int)key, 16);
-        key = key > k16 ? key : k16;
-      }
-      const int p = 7 - (int)(key & 7u);
       const int srcl = sbase + 4 * p + g;
       const T er0 = __shfl(a[0], srcl), ei0 = __shfl(b[0], srcl);   // A[p][g]
       const T er1 = __shfl(a[1], srcl), ei1 = __shfl(b[1], srcl);   // A[p][g + 4]
@@ -431,27 +470,70 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
         else if ((k & 3) == 2) { pr = quad_bcast<2>(sr); pim = quad_bcast<2>(si); }
         else { pr = quad_bcast<3>(sr); pim = quad_bcast<3>(si); }
       }
-      inv += __builtin_popcount(used >> p);   // earlier pivots below p in the row order
-      used |= 1u << p;
-      const T den = pr * pr + pim * pim;
-      T ipr_, ipi_, rabs_, lden_;
-      pivot_recip(pr, pim, den, ipr_, ipi_, rabs_, lden_);
-      lsum += lden_;
-      {
-        const T rm = rabs_;
-        const T xr = pr * rm, xi = pim * rm;
-        const T nr = ur * xr - ui * xi, ni = ur * xi + ui * xr;
-        ur = nr;
-        ui = ni;
-      }
-      const T ipr = ipr_, ipi = ipi_;   // 1 / pivot
-      if (rl && !((used >> r) & 1u)) {   // rows still open: A[r][:] -= (A[r][k] / pivot) A[p][:]
+      T ipr, ipi;
+      pivot_step(pr, pim, ipr, ipi, rabs);   // 1 / pivot
+      if (open_after) {
         const T mr = akr * ipr - aki * ipi, mi = akr * ipi + aki * ipr;
         a[0] -= mr * er0 - mi * ei0;
         b[0] -= mr * ei0 + mi * er0;
         a[1] -= mr * er1 - mi * ei1;
         b[1] -= mr * ei1 + mi * er1;
       }
+    };
+    auto col_k = [&](int k, const T* a, const T* b, T& akr, T& aki) {   // A[r][k]
+      const int kh = k >> 2;
+      if ((k & 3) == 0) { akr = quad_bcast<0>(a[kh]); aki = quad_bcast<0>(b[kh]); }
+      else if ((k & 3) == 1) { akr = quad_bcast<1>(a[kh]); aki = quad_bcast<1>(b[kh]); }
+      else if ((k & 3) == 2) { akr = quad_bcast<2>(a[kh]); aki = quad_bcast<2>(b[kh]); }
+      else { akr = quad_bcast<3>(a[kh]); aki = quad_bcast<3>(b[kh]); }
+    };
+    auto pivoted = [&]() {
+      T a[2] = {a0[0], a0[1]}, b[2] = {b0[0], b0[1]};
+      lsum = T(0);
+      ur = T(1);
+      ui = T(0);
+      inv = 0;
+      unsigned used = 0;
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        T akr, aki;
+        col_k(k, a, b, akr, aki);
+        const bool open = rl && !((used >> r) & 1u);
+        unsigned key = open ? ((key_bits(f_abs(akr) + f_abs(aki)) & ~7u) | (unsigned)(7 - r)) : 0u;
+        {
+          const unsigned k4 = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x124, 0xF, 0xF, true);
+          key = key > k4 ? key : k4;
+          const unsigned k8 = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x128, 0xF, 0xF, true);
+          key = key > k8 ? key : k8;
+          const unsigned k16 = (unsigned)__shfl_xor((int)key, 16);
+          key = key > k16 ? key : k16;
+        }
+        const int p = 7 - (int)(key & 7u);
+        inv += __builtin_popcount(used >> p);   // earlier pivots below p in the row order
+        used |= 1u << p;
+        T rabs;
+        lu_step(k, p, a, b, rl && !((used >> r) & 1u), akr, aki, rabs);
+      }
+    };
+    if constexpr (kQuadFixedLU) {
+      T a[2] = {a0[0], a0[1]}, b[2] = {b0[0], b0[1]};
+      bool bad = false, done = false;
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        T akr, aki;
+        col_k(k, a, b, akr, aki);
+        const int p = (int)sm[SQ::pv + k];
+        const T rk = sm[SQ::pv + N + k];
+        done = done || (p == r);
+        T rabs;
+        lu_step(k, p, a, b, rl && !done, akr, aki, rabs);
+        bad = bad || !(rk >= T(0.1) * rabs);   // |pivot| below 0.1 of the walker's (or not finite)
+      }
+      inv = (int)sm[SQ::pv + 2 * N];
+      const unsigned long long bm = __ballot(bad);
+      if ((bm >> (lane & ~(SW - 1))) & ((1ull << SW) - 1ull)) pivoted();   // this slot: partial pivoting
+    } else {
+      pivoted();
     }
   }
   const T jt = slot_sum<SW>(jsum);
