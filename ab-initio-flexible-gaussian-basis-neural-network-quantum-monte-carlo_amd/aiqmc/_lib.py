@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "aiqmc_debug_set_proposal_reuse", "aiqmc_debug_phase_cycles", "aiqmc_debug_local_energy_forward",
     "aiqmc_set_ecp", "aiqmc_local_energy_ecp", "aiqmc_local_energy_ecp_complex", "aiqmc_logpsi_param_grad",
     "aiqmc_dmc_drift_diffusion", "aiqmc_dmc_weights", "aiqmc_dmc_branch", "aiqmc_dmc_tmoves", "aiqmc_phase_param_grad",
-    "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals", "aiqmc_debug_set_ablate", "aiqmc_debug_set_fuse_accept", "aiqmc_debug_set_walker_pivots", "aiqmc_debug_set_packed_walkers", "aiqmc_debug_set_lap_waves",
+    "aiqmc_dmc_weights_ex", "aiqmc_dmc_cut_minima", "aiqmc_orbitals", "aiqmc_debug_set_ablate", "aiqmc_debug_set_fuse_accept", "aiqmc_debug_set_walker_pivots", "aiqmc_debug_set_packed_walkers", "aiqmc_debug_set_quad_pivoted", "aiqmc_debug_set_lap_waves",
     "aiqmc_debug_set_fuse_reduce", "aiqmc_energy_stats", "aiqmc_energy_stats_final",
     "aiqmc_debug_limdrift_factor", "aiqmc_debug_launch_lds", "aiqmc_loss_weights",
     "aiqmc_param_grad_weighted", "aiqmc_loss_level", "aiqmc_loss_pack", "aiqmc_loss_final",
@@ -140,6 +140,8 @@ def load() -> ctypes.CDLL:
     lib.aiqmc_debug_set_walker_pivots.restype = ctypes.c_int
     lib.aiqmc_debug_set_packed_walkers.argtypes = [vp, i32]
     lib.aiqmc_debug_set_packed_walkers.restype = ctypes.c_int
+    lib.aiqmc_debug_set_quad_pivoted.argtypes = [vp, i32]
+    lib.aiqmc_debug_set_quad_pivoted.restype = ctypes.c_int
     lib.aiqmc_debug_set_fuse_reduce.argtypes = [vp, i32]
     lib.aiqmc_debug_set_fuse_reduce.restype = ctypes.c_int
     lib.aiqmc_debug_limdrift_factor.argtypes = [vp, vp, i32, ctypes.c_double, i32,
@@ -478,6 +480,11 @@ class Context:
     def set_packed_walkers(self, on: bool):
         """Diagnostics: walker launches of N <= 8 several per wave (default) or one wave each."""
         check(self._lib.aiqmc_debug_set_packed_walkers(self._h, int(bool(on))), "aiqmc_debug_set_packed_walkers")
+
+    def set_quad_pivoted(self, on: bool):
+        """Diagnostics: the N <= 8 ECP quadrature launch factors every configuration with partial
+        pivoting (on) instead of the walker's recorded order with a per-configuration fallback."""
+        check(self._lib.aiqmc_debug_set_quad_pivoted(self._h, int(bool(on))), "aiqmc_debug_set_quad_pivoted")
 
     def set_fuse_reduce(self, mode):
         """Diagnostics: fp32 mc_step limdrift sums fused into the walker / proposal launches as

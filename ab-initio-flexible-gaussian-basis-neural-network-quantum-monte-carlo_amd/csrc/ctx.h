@@ -39,6 +39,7 @@ struct aiqmc_ctx {
   int ablate = 0;                                           // AQ_ABLATE development builds (walker_rev.h)
   int fuse_accept = 1;                                      // acceptance fused into the next walker launch
   int walker_fixed_gj = 1;                                  // walker launches re-use the previous sweep's pivot order
+  int quad_pivoted = 0;                                     // k_quad_value: partial pivoting for every slot (test)
   int packed_walkers = 1;                                   // N <= 8 walker launches several per wave
   int fuse_reduce = 1;                                      // fp32 mc_step: limdrift sums by integer atomics
   int wide_reduce = 1;                                      // unfused fp32 sweeps: k_taueff_part (0: k_taueff)

@@ -398,7 +398,7 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
     if constexpr (kQuadFixedLU) {
       // the walker's order: pivot row p of step k and 1 / |walker pivot k| from the slot's LDS copy
       T a = a0, b = b0;
-      bool bad = false, done = false;
+      bool bad = ka.quad_pivoted != 0, done = false;
 #pragma unroll
       for (int k = 0; k < N; ++k) {
         const T akr = k == 0 ? quad_bcast<0>(a) : (k == 1 ? quad_bcast<1>(a) : (k == 2 ? quad_bcast<2>(a) : quad_bcast<3>(a)));
@@ -517,7 +517,7 @@ __global__ __launch_bounds__(64) void k_quad_value(KArgs ka) {
     };
     if constexpr (kQuadFixedLU) {
       T a[2] = {a0[0], a0[1]}, b[2] = {b0[0], b0[1]};
-      bool bad = false, done = false;
+      bool bad = ka.quad_pivoted != 0, done = false;
 #pragma unroll
       for (int k = 0; k < N; ++k) {
         T akr, aki;

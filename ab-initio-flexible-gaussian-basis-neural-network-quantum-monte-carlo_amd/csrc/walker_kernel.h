@@ -298,6 +298,8 @@ struct KArgs {
   int one_wave;
   // walker launch of a small batch as two waves per walker (k_walker_rev<..., SPL>: F1 and F2 at once)
   int walk_split;
+  // k_quad_value: every slot takes the partial-pivoting LU, not the walker's order (aiqmc_debug_set_quad_pivoted)
+  int quad_pivoted;
   // Metropolis caches (walker_rev.h WCache / ECache); nullptr outside aiqmc_mc_step
   void* wcache;
   void* ecache;

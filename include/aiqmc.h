@@ -363,6 +363,12 @@ int aiqmc_debug_launch_lds(int32_t nelectrons, int32_t natoms, int32_t dtype, in
  * Results agree to rounding. */
 int aiqmc_debug_set_packed_walkers(aiqmc_ctx* ctx, int32_t on);
 
+/* Diagnostics: the ECP quadrature's value launch for N <= 8 (k_quad_value) factors each displaced
+ * configuration's matrix in its walker's recorded pivot order and re-runs partial pivoting only for
+ * a configuration whose pivot falls below 0.1 of the walker's; on = 1 takes partial pivoting for
+ * every configuration (the fallback path everywhere).  Results agree to rounding. */
+int aiqmc_debug_set_quad_pivoted(aiqmc_ctx* ctx, int32_t on);
+
 /* Diagnostics: in fp32, aiqmc_mc_step can sum the two limdrift reductions of each sweep
  * (|grad|^2 over the walkers, over the proposals; VMCmcstep.py:11-14) inside the walker and
  * proposal launches, as exact 64-bit integer sums of |grad|^2 in units of 2^-16: no reduction

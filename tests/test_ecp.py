@@ -272,3 +272,35 @@ def test_c2_quadrature_not_offset_by_atom():
     for i in range(8):
         for a in range(2):
             np.testing.assert_allclose(np.linalg.norm(moved[i, a, :, i], axis=-1), r[i, a], rtol=1e-7)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["C_ecp", "C2_ecp"])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_quad_walker_order_lu_matches_partial_pivoting(name, dtype):
+    """k_quad_value (N <= 8) factors each displaced configuration in its walker's recorded pivot
+    order and re-runs partial pivoting for a configuration whose pivot falls below 0.1 of the
+    walker's; aiqmc_debug_set_quad_pivoted(1) sends every configuration down that fallback.  Both
+    must give the same quadrature log|psi| / phase and E_L to rounding (fp64 1e-11, fp32 2e-5
+    relative on log|psi|), over 512 walkers with Philox rotations (the fallback is taken for a
+    few % of C2's configurations in the default mode, so both branches run)."""
+    from oracle import system
+    s, ctx = _ecp_ctx(dtype, name)
+    rng = np.random.default_rng(11)
+    ctx.set_params(system.flatten_params(system.init_params(rng, s, randomize_aux=True)))
+    pos = torch.tensor(system.init_electrons(rng, s.atoms, s.charges, 512, 1.0), device="cuda", dtype=dtype)
+    e1, l1, p1 = ctx.local_energy_ecp(pos, seed=9, offset=0, want_quadrature=True)
+    ctx.set_quad_pivoted(True)
+    e2, l2, p2 = ctx.local_energy_ecp(pos, seed=9, offset=0, want_quadrature=True)
+    ctx.set_quad_pivoted(False)
+    e3 = ctx.local_energy_ecp(pos, seed=9, offset=0)
+    torch.cuda.synchronize()
+    l1, l2, p1, p2 = (t.double().cpu().numpy() for t in (l1, l2, p1, p2))
+    assert np.isfinite(l1).all() and np.isfinite(l2).all()
+    tol = 1e-11 if dtype == torch.float64 else 2e-5
+    np.testing.assert_allclose(l1, l2, rtol=tol, atol=tol)
+    dp = np.angle(np.exp(1j * (p1 - p2)))
+    assert np.max(np.abs(dp)) <= (1e-10 if dtype == torch.float64 else 1e-4)
+    d = torch.abs(e1 - e2) / torch.clamp(torch.abs(e2), min=1.0)
+    assert d.max().item() <= (1e-10 if dtype == torch.float64 else 1e-5)
+    assert torch.equal(e1, e3)   # the debug switch restores the default path
