@@ -276,31 +276,51 @@ def test_c2_quadrature_not_offset_by_atom():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["C_ecp", "C2_ecp"])
-@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-def test_quad_walker_order_lu_matches_partial_pivoting(name, dtype):
+def test_quad_walker_order_lu_matches_partial_pivoting(name):
     """k_quad_value (N <= 8) factors each displaced configuration in its walker's recorded pivot
     order and re-runs partial pivoting for a configuration whose pivot falls below 0.1 of the
-    walker's; aiqmc_debug_set_quad_pivoted(1) sends every configuration down that fallback.  Both
-    must give the same quadrature log|psi| / phase and E_L to rounding (fp64 1e-11, fp32 2e-5
-    relative on log|psi|), over 512 walkers with Philox rotations (the fallback is taken for a
-    few % of C2's configurations in the default mode, so both branches run)."""
+    walker's; aiqmc_debug_set_quad_pivoted(1) sends every configuration down that fallback.
+    512 walkers, host Haar rotations (C2: the fallback is taken for a few % of the configurations
+    in the default mode, so both branches run).  fp64: both orders agree to 1e-11 (log|psi|,
+    phase, E_L).  fp32: measured against the fp64 values, the walker order is no less accurate
+    than partial pivoting (max and 99.99th-percentile |error| of log|psi|, within 1.5x; measured
+    on MI355X: equal maxima, 3.2e-4 C and 1.2e-3 C2, tools/quad_lu_accuracy.py) and E_L agrees
+    to 1e-5 relative."""
     from oracle import system
-    s, ctx = _ecp_ctx(dtype, name)
     rng = np.random.default_rng(11)
-    ctx.set_params(system.flatten_params(system.init_params(rng, s, randomize_aux=True)))
-    pos = torch.tensor(system.init_electrons(rng, s.atoms, s.charges, 512, 1.0), device="cuda", dtype=dtype)
-    e1, l1, p1 = ctx.local_energy_ecp(pos, seed=9, offset=0, want_quadrature=True)
-    ctx.set_quad_pivoted(True)
-    e2, l2, p2 = ctx.local_energy_ecp(pos, seed=9, offset=0, want_quadrature=True)
-    ctx.set_quad_pivoted(False)
-    e3 = ctx.local_energy_ecp(pos, seed=9, offset=0)
-    torch.cuda.synchronize()
-    l1, l2, p1, p2 = (t.double().cpu().numpy() for t in (l1, l2, p1, p2))
-    assert np.isfinite(l1).all() and np.isfinite(l2).all()
-    tol = 1e-11 if dtype == torch.float64 else 2e-5
-    np.testing.assert_allclose(l1, l2, rtol=tol, atol=tol)
-    dp = np.angle(np.exp(1j * (p1 - p2)))
-    assert np.max(np.abs(dp)) <= (1e-10 if dtype == torch.float64 else 1e-4)
-    d = torch.abs(e1 - e2) / torch.clamp(torch.abs(e2), min=1.0)
-    assert d.max().item() <= (1e-10 if dtype == torch.float64 else 1e-5)
-    assert torch.equal(e1, e3)   # the debug switch restores the default path
+    s0, _ = _ecp_ctx(torch.float64, name)
+    params = system.flatten_params(system.init_params(rng, s0, randomize_aux=True))
+    pos = system.init_electrons(rng, s0.atoms, s0.charges, 512, 1.0)
+    rot = pp.haar_rotations(rng, 512)
+    res = {}
+    for dtype in (torch.float64, torch.float32):
+        s, ctx = _ecp_ctx(dtype, name)
+        ctx.set_params(params)
+        p = torch.tensor(pos, device="cuda", dtype=dtype)
+        r = torch.tensor(rot, device="cuda", dtype=dtype)
+        for piv in (False, True):
+            ctx.set_quad_pivoted(piv)
+            e, l, ph = ctx.local_energy_ecp(p, rot=r, want_quadrature=True)
+            torch.cuda.synchronize()
+            res[(dtype, piv)] = (e.cpu().numpy().astype(np.complex128), l.double().cpu().numpy().ravel(),
+                                 ph.double().cpu().numpy().ravel())
+        ctx.set_quad_pivoted(False)
+        e3 = ctx.local_energy_ecp(p, rot=r)
+        torch.cuda.synchronize()
+        assert np.array_equal(e3.cpu().numpy().astype(np.complex128), res[(dtype, False)][0])   # switch restored
+    (ef, lf, pf), (ep, lp, pq) = res[(torch.float64, False)], res[(torch.float64, True)]
+    assert np.isfinite(lf).all()
+    np.testing.assert_allclose(lf, lp, rtol=1e-11, atol=1e-11)
+    assert np.max(np.abs(np.angle(np.exp(1j * (pf - pq))))) <= 1e-10
+    assert np.max(np.abs(ef - ep)) <= 1e-10
+    ref = lp
+    errs = {}
+    for piv in (False, True):
+        e32, l32, _ = res[(torch.float32, piv)]
+        assert np.isfinite(l32).all()
+        d = np.abs(l32 - ref)
+        errs[piv] = (d.max(), np.quantile(d, 0.9999))
+    assert errs[False][0] <= 1.5 * errs[True][0] + 1e-5, errs
+    assert errs[False][1] <= 1.5 * errs[True][1] + 1e-6, errs
+    e_a, e_b = res[(torch.float32, False)][0], res[(torch.float32, True)][0]
+    assert np.max(np.abs(e_a - e_b) / np.maximum(np.abs(e_b), 1.0)) <= 1e-5
