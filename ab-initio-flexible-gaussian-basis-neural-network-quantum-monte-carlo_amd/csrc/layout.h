@@ -118,7 +118,7 @@ struct LapCache {
   static constexpr int D0 = 4 * A;
   static constexpr int QM = (3 * D0 + 2 * NH2) / 4;   // conv outputs of layer 0 (the widest layer)
   // one block per h-stream layer l at l * layer_n (staged in LDS a layer at a time)
-  static constexpr int cn = 0;                        // [N][QM][2]  conv nodes: 1 - c^2, abar phi''(z)
+  static constexpr int cn = 0;                        // [N][QM][2]  conv nodes: (1 - c^2) / 4, abar phi''(z) / 16
   static constexpr int sn = cn + N * QM * 2;          // [N][4][2]   single nodes: 1 - s^2, abar phi''(z)
   static constexpr int sd = sn + N * NH * 2;          // [2][N][3][4] sum_{k in G, k != i} dh2[k,i][f] / d(x_i - x_k)_c
   static constexpr int layer_n = (sd + 2 * N * 3 * NH2 + 3) / 4 * 4;
@@ -127,7 +127,10 @@ struct LapCache {
   static constexpr int ph = bm + 2 * N * N;           // [N][N][2]   Phi
   static constexpr int qs = ph + 2 * N * N;           // [N][N][4][2] Q_f[r,s] = sum_c W_{s(r)}[f,c] Yt[r,c] B[c,s]
   static constexpr int scal = qs + 8 * N * N;         // [0]         pair-local part of the Laplacian
-  static constexpr int size = (scal + 4 + 31) / 32 * 32;
+  // [N][N][2][4] tanh outputs t1, t2 of the double layers of ordered pair (k, i) (diagonal included), so
+  // that the first-derivative pass carries only the derivative chain through the pair stream
+  static constexpr int pt = (scal + 4 + 7) / 8 * 8;
+  static constexpr int size = (pt + 8 * N * N + 31) / 32 * 32;
 };
 
 }  // namespace aq

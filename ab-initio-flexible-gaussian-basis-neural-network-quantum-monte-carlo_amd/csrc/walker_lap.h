@@ -38,7 +38,7 @@ struct SmemLap {
   // lane-private arrays [..][49]: direction lanes 0..47 own a column; the 16 value-row
   // lanes share column 48 (they carry no derivatives; their stores there are don't-cares)
   static constexpr int yd = ly + LapCache<N, A>::layer_n;    // [2][N][49] dYt/dx, d2Yt/dx2 of row le
-  static constexpr int hb = yd + 2 * N * 49;                 // [N][4][49] dh/dx
+  static constexpr int hb = (yd + 2 * N * 49 + 3) / 4 * 4;   // [N][49][4] dh/dx (a lane's 4 units: one 16-byte access)
   static constexpr int end = hb + N * NH * 49;
   // Q_f [N][N][4][2] (and B [N][N][2] where it fits) staged over ly + yd once both are dead
   static constexpr int qs = ly;
@@ -106,12 +106,37 @@ constexpr bool kLapPrefetch = false;
 #endif
 
 // One h-stream layer (nn.py:280-311) in first derivatives, column loop over electrons i.
-// ly: this layer's LapCache block (LDS); hb: dh/dx of every electron, updated in place
+// ly: this layer's LapCache block (LDS); hb: dh/dx of every electron [N][49][NH], updated in place
 // (column `lane` = min(lane, 48), see SmemLap).
+// The pair tanh's of one column: t_{j+1}[o] of pair (le, i) for j < L from the LapCache (16-byte loads)
+template <typename T, int L>
+struct PairT {
+  T t[L > 0 ? L : 1][4];
+  __device__ __forceinline__ void load(cptr<T> src) {
+    if constexpr (L > 0 && sizeof(T) == 4) {
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      const __attribute__((address_space(4))) f4* s = (const __attribute__((address_space(4))) f4*)src;
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const f4 v = s[j];
+        t[j][0] = v.x;
+        t[j][1] = v.y;
+        t[j][2] = v.z;
+        t[j][3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < L; ++j)
+#pragma unroll
+        for (int o = 0; o < 4; ++o) t[j][o] = src[j * 4 + o];
+    }
+  }
+};
+
 template <typename T, int N, int A, int L>
 __device__ __forceinline__ void lap_layer(cptr<T> P, const T* xs, T* hb, const T* ly, const PJ<T>* hf, int lane,
                                           int lc, int er, int le, bool val, bool dir, bool live, int nup, T& jd1,
-                                          T& jd2, T& vv, T& acc, int wv, int W) {
+                                          T& jd2, T& vv, T& acc, int wv, int W, cptr<T> Lpt) {
   using Ly = Lay<N, A>;
   using LC = LapCache<N, A>;
   constexpr int DIN = (L == 0) ? 4 * A : NH;
@@ -136,10 +161,10 @@ __device__ __forceinline__ void lap_layer(cptr<T> P, const T* xs, T* hb, const T
     for (int m = 0; m < DIN; ++m) g1[0][m] = g1[1][m] = T(0);
     for (int k = 0; k < nup; ++k)
 #pragma unroll
-      for (int m = 0; m < DIN; ++m) g1[0][m] += hb[(k * NH + m) * 49 + lane];
+      for (int m = 0; m < DIN; ++m) g1[0][m] += hb[(k * 49 + lane) * NH + m];
     for (int k = nup; k < N; ++k)
 #pragma unroll
-      for (int m = 0; m < DIN; ++m) g1[1][m] += hb[(k * NH + m) * 49 + lane];
+      for (int m = 0; m < DIN; ++m) g1[1][m] += hb[(k * 49 + lane) * NH + m];
 #pragma unroll
     for (int m = 0; m < DIN; ++m) {
       g1[0][m] *= ginv[0];
@@ -155,9 +180,22 @@ __device__ __forceinline__ void lap_layer(cptr<T> P, const T* xs, T* hb, const T
 #ifndef AQ_LAP_COL_UNROLL
 #define AQ_LAP_COL_UNROLL 2
 #endif
+  // the pair tanh's of the lane's pairs (le, i) (LapCache pt, written by the adjoint pass), loaded two
+  // columns ahead: lap_layer carries only the derivative chain through the double layers
+  PairT<T, L> tn1, tn2;
+  if constexpr (L > 0) {
+    tn1.load(Lpt + wv * 8);
+    tn2.load(Lpt + (wv + W < N ? wv + W : wv) * 8);
+  }
 #pragma unroll AQ_LAP_COL_UNROLL
   for (int i = wv; i < N; i += W) {
     const bool diag = (le == i);
+    PairT<T, L> tcur;
+    if constexpr (L > 0) {
+      tcur = tn1;
+      tn1 = tn2;
+      tn2.load(Lpt + (i + 2 * W < N ? i + 2 * W : i) * 8);
+    }
     T d[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) d[c] = xs[i * 3 + c] - xs[le * 3 + c];
@@ -178,37 +216,26 @@ __device__ __forceinline__ void lap_layer(cptr<T> P, const T* xs, T* hb, const T
       }
       if (val && live && er < i) vv += ir;      // V_ee, each pair once (hamiltonian.py:177-187)
     }
-    // pair stream h2[le,i] = [r, x_i - x_le] through L double layers (nn.py:305-309): value and
-    // derivative along x_{le,lc}
-    T pv[4], pd[4];
-    pv[0] = r;
+    // pair stream h2[le,i] = [r, x_i - x_le] through L double layers (nn.py:305-309): the derivative
+    // along x_{le,lc}, with the layers' tanh outputs of the adjoint pass
+    T pd[4];
     pd[0] = r1;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      pv[1 + c] = d[c];
-      pd[1 + c] = (lc == c) ? T(-1) : T(0);
-    }
+    for (int c = 0; c < 3; ++c) pd[1 + c] = (lc == c) ? T(-1) : T(0);
 #pragma unroll
     for (int j = 0; j < L; ++j) {
       const cptr<T> dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
-      const cptr<T> db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
-      T tv[4], td[4];
+      T td[4];
 #pragma unroll
       for (int o = 0; o < 4; ++o) {
-        T zv = db[o], zd = T(0);
+        T zd = T(0);
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          zv += pv[m] * dw[m * 4 + o];
-          zd += pd[m] * dw[m * 4 + o];
-        }
-        tv[o] = f_tanh(zv);
-        td[o] = (T(1) - tv[o] * tv[o]) * zd;
+        for (int m = 0; m < 4; ++m) zd += pd[m] * dw[m * 4 + o];
+        const T tv = tcur.t[j][o];
+        td[o] = (T(1) - tv * tv) * zd;
       }
 #pragma unroll
-      for (int o = 0; o < 4; ++o) {
-        pv[o] = (pv[o] + tv[o]) * RSQ2;
-        pd[o] = (pd[o] + td[o]) * RSQ2;
-      }
+      for (int o = 0; o < 4; ++o) pd[o] = (pd[o] + td[o]) * RSQ2;
     }
     // column means of h2 over the spin groups (nn.py:151): lane (c, e != i) sees pair (e, i)
     // only; lane (c, i) sees every pair (k, i) -- their derivative sums from the LapCache
@@ -226,7 +253,7 @@ __device__ __forceinline__ void lap_layer(cptr<T> P, const T* xs, T* hb, const T
 #pragma unroll
     for (int m = 0; m < DIN; ++m) {
       if constexpr (L == 0) hi[m] = (diag && dir) ? hf[m].d1 : T(0);
-      else hi[m] = hb[(i * NH + m) * 49 + lane];
+      else hi[m] = hb[(i * 49 + lane) * NH + m];
     }
     // convolutional layer c = tanh(mean_4(f w) + b) (network_blocks.py:106-116)
     const T* cn = ly + LC::cn + i * LC::QM * 2;
@@ -245,7 +272,7 @@ __device__ __forceinline__ void lap_layer(cptr<T> P, const T* xs, T* hb, const T
         else F = g2[1][idx - 3 * DIN - 4];
         z += convw[i * DF + idx] * F;
       }
-      z *= T(0.25);
+      // the conv's mean_4 factor 1/4 is folded into the LapCache's node weights (adjoint pass)
       cq[q] = cn[2 * q] * z;
       acc += cn[2 * q + 1] * z * z;
     }
@@ -258,7 +285,7 @@ __device__ __forceinline__ void lap_layer(cptr<T> P, const T* xs, T* hb, const T
       for (int q = 0; q < Q; ++q) z += sngw[q * NH + f] * cq[q];
       const T s1 = sn[2 * f] * z;
       acc += sn[2 * f + 1] * z * z;
-      hb[(i * NH + f) * 49 + lane] = (DIN == NH) ? (hi[f] + s1) * RSQ2 : s1;
+      hb[(i * 49 + lane) * NH + f] = (DIN == NH) ? (hi[f] + s1) * RSQ2 : s1;
     }
   }
 }
@@ -313,7 +340,7 @@ __device__ __forceinline__ T ss_mfma(const T* Qs, const T* hb, const int* rowsrc
     for (int m = 0; m < NM; ++m) acc[m] = V4{T(0), T(0), T(0), T(0)};
 #pragma unroll 2
     for (int s = wv; s < N; s += W) {
-      const T bop = hb[(rowsrc[s] * NH + q) * 49 + 16 * c + e];
+      const T bop = hb[(rowsrc[s] * 49 + 16 * c + e) * NH + q];
 #pragma unroll
       for (int m = 0; m < NM; ++m) {
         const int i = 16 * m + e;            // A row (r, f); A column k = unit q of electron s
@@ -333,7 +360,7 @@ __device__ __forceinline__ T ss_mfma(const T* Qs, const T* hb, const int* rowsrc
       for (int v = 0; v < 4; ++v) {
         const int i = 16 * m + MT::row(q, v);
         const int r = i >> 2, f = i & 3;
-        if (16 * (m + 1) <= 4 * N || r < N) p += hb[(rowsrc[r < N ? r : N - 1] * NH + f) * 49 + 16 * c + e] * acc[m][v];
+        if (16 * (m + 1) <= 4 * N || r < N) p += hb[(rowsrc[r < N ? r : N - 1] * 49 + 16 * c + e) * NH + f] * acc[m][v];
       }
     p += __shfl_xor(p, 16);
     p += __shfl_xor(p, 32);
@@ -354,8 +381,11 @@ __device__ __forceinline__ T ss_mfma(const T* Qs, const T* hb, const int* rowsrc
 // complex quantity whose real part the log|psi| pass takes (d^2 log det = tr(B d^2A) - tr(B dA B dA)
 // is complex; theta = Im log det); the Jastrow factors are real and drop out.  Outputs: el[conf] =
 // sum_dir d^2 theta / dx^2 (no potential, no |grad|^2), grad = grad theta.
+#ifndef AQ_LAP_WPE
+#define AQ_LAP_WPE 2
+#endif
 template <typename T, int N, int A, int WMAX, bool PH = false>
-__global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) void k_walker_lap(KArgs ka) {
+__global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LAP_WPE))) void k_walker_lap(KArgs ka) {
   using Ly = Lay<N, A>;
   using LC = LapCache<N, A>;
   using SM = SmemLap<T, N, A>;
@@ -381,6 +411,7 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
   const int l49 = lane < 48 ? lane : 48;
   T* yd = sm + SM::yd;
   const cptr<T> Lc = param_ptr<T>((const T*)ka.lapcache + (size_t)conf * LC::size);
+  const cptr<T> Lpt = Lc + LC::pt + le * N * 8;   // pair tanh's of the lane's row le
 
   if (w0 && lane < 3 * N) xs[lane] = ((const T*)ka.pos)[(size_t)conf * 3 * N + lane];
   T h0b[D0];
@@ -419,7 +450,7 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
   // no wave waits a whole L2/HBM round trip at a stage boundary
   StageRegs<T, LC::layer_n> lnext;
   if constexpr (kLapPrefetch) lnext.load(Lc + LC::layer_n);
-  lap_layer<T, N, A, 0>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W);
+  lap_layer<T, N, A, 0>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W, Lpt);
   if constexpr (PH) {   // the e-e Jastrow terms and V_ee of layer 0's column loop: not part of theta
     jd1 = jd2 = vv = T(0);
   }
@@ -428,7 +459,7 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
   else stage_copy<T>(ly, Lc + LC::layer_n, LC::layer_n);
   __syncthreads();
   if constexpr (kLapPrefetch) lnext.load(Lc + 2 * LC::layer_n);
-  lap_layer<T, N, A, 1>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W);
+  lap_layer<T, N, A, 1>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W, Lpt);
   __syncthreads();
   if constexpr (kLapPrefetch) lnext.store(ly);
   else stage_copy<T>(ly, Lc + 2 * LC::layer_n, LC::layer_n);
@@ -439,7 +470,7 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
     qnext.load(Lc + LC::qs);
     if constexpr (SM::stage_b) bnext.load(Lc + LC::bm);
   }
-  lap_layer<T, N, A, 2>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W);
+  lap_layer<T, N, A, 2>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W, Lpt);
   if (W > 1) __syncthreads();   // the determinant terms read every wave's columns of dh/dx
 
   // ------------------------------------------------------------------ determinant terms
@@ -448,7 +479,7 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(2))) 
   const T* Qs = nullptr;                     // LDS copy, set after E1
   const T* Bu = (const T*)(Lc + LC::bm);     // LDS copy after E1 where it fits
   const cptr<T> Ph = Lc + LC::ph;
-#define UH(r, f) hb[(rowsrc[r] * NH + (f)) * 49 + l49]
+#define UH(r, f) hb[(rowsrc[r] * 49 + l49) * NH + (f)]
   // E1: Yt row jets of electron le (stored after the per-electron stage)
   T Yd1[N], Yd2[N];
 #pragma unroll

@@ -975,6 +975,11 @@ k_walker_rev(KArgs ka) {
 #pragma unroll
               for (int o = 0; o < 4; ++o) tp[o] = q[o];
             }
+            if (PREP && icol) {   // LapCache: the same for k_walker_lap, the diagonal's finite values included
+              T* tp = Lw + LCc::pt + (k * N + ii) * 8 + j * 4;
+#pragma unroll
+              for (int o = 0; o < 4; ++o) tp[o] = q[o];
+            }
   #pragma unroll
             for (int o = 0; o < 4; ++o) {
               p[o] = (p[o] + q[o]) * RSQ2;
@@ -1768,11 +1773,13 @@ k_walker_rev(KArgs ka) {
           const T g = cb * (T(1) - c * c) * T(0.25);
           if constexpr (PREP) {
             // conv node (stored once, by the lane of its quad position): tanh', abar * tanh''
+            // (pre-scaled by the conv's 1/4 and its square: k_walker_lap multiplies the unscaled sum,
+            // the same products bit for bit since the scalings are powers of two)
             if (ilive && (qq & 3) == ff) {
               const T c1 = T(1) - c * c;
               T* cn = Lw + l * LCc::layer_n + LCc::cn + (ic * LCc::QM + qq) * 2;
-              cn[0] = c1;
-              cn[1] = T(-2) * c * c1 * cb;
+              cn[0] = c1 * T(0.25);
+              cn[1] = (T(-2) * c * c1 * cb) * T(0.0625);
             }
           }
           if (full) {
@@ -1857,16 +1864,27 @@ k_walker_rev(KArgs ka) {
 #pragma unroll
             for (int f = 0; f < 4; ++f) s1[j][c][f] = T(0);
         }
+        // the pair's double-layer tanh's: written by this lane in F2 (LapCache pt, same (k, i) per lane),
+        // read back one pair ahead instead of re-running the value chain in each pass
+        const int kfirst = k0 + ((kq - k0) & 3);
+        const T* tpb = Lw + LCc::pt + ii * 8;
+        T tq[8];
+#pragma unroll
+        for (int o = 0; o < 8; ++o) tq[o] = tpb[(kfirst < k1 ? kfirst : k0) * N * 8 + o];
 #pragma unroll 1
-        for (int k = k0 + ((kq - k0) & 3); k < k1; k += 4) {
+        for (int k = kfirst; k < k1; k += 4) {
           const bool dg = (k == ii);
           const T m = (ilv && !dg) ? T(1) : T(0);
+          T tcur[8];
+#pragma unroll
+          for (int o = 0; o < 8; ++o) tcur[o] = tq[o];
+#pragma unroll
+          for (int o = 0; o < 8; ++o) tq[o] = tpb[(k + 4 < k1 ? k + 4 : k) * N * 8 + o];
           T d[3];
 #pragma unroll
           for (int c = 0; c < 3; ++c) d[c] = xs[ii * 3 + c] - xs[k * 3 + c];
           const T r = f_sqrt(dg ? T(1) : d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
           const T ir = f_rcp(r);
-          T pv[4] = {r, d[0], d[1], d[2]};
           T p1[NC][4], p2[NC][4];
 #pragma unroll
           for (int c = 0; c < NC; ++c) {
@@ -1883,16 +1901,10 @@ k_walker_rev(KArgs ka) {
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             const cptr<T> dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
-            const cptr<T> db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
             const T* gl = gb + (j + 1) * 2 * N * 4;
             T tv[4];
 #pragma unroll
-            for (int o = 0; o < 4; ++o) {
-              T zv = db[o];
-#pragma unroll
-              for (int mm = 0; mm < 4; ++mm) zv += pv[mm] * dw[mm * 4 + o];
-              tv[o] = f_tanh(zv);
-            }
+            for (int o = 0; o < 4; ++o) tv[o] = tcur[j * 4 + o];
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
               T z1[4], z2[4];
@@ -1918,8 +1930,6 @@ k_walker_rev(KArgs ka) {
                 pcurv += m * gl[o] * p2[c][o];
               }
             }
-#pragma unroll
-            for (int o = 0; o < 4; ++o) pv[o] = (pv[o] + tv[o]) * RSQ2;
           }
         }
         // column i's totals over its four lanes; lane kq stores direction C0 + kq (kq < NC)
