@@ -127,10 +127,11 @@ struct LapCache {
   static constexpr int ph = bm + 2 * N * N;           // [N][N][2]   Phi
   static constexpr int qs = ph + 2 * N * N;           // [N][N][4][2] Q_f[r,s] = sum_c W_{s(r)}[f,c] Yt[r,c] B[c,s]
   static constexpr int scal = qs + 8 * N * N;         // [0]         pair-local part of the Laplacian
-  // [N][N][2][4] tanh outputs t1, t2 of the double layers of ordered pair (k, i) (diagonal included), so
-  // that the first-derivative pass carries only the derivative chain through the pair stream
-  static constexpr int pt = (scal + 4 + 7) / 8 * 8;
-  static constexpr int size = (pt + 8 * N * N + 31) / 32 * 32;
+  // [N][N][pt_n] per ordered pair (k, i), diagonal included: tanh outputs t1[4], t2[4] of the two double
+  // layers, so that the first-derivative pass carries only the derivative chain through the pair stream
+  static constexpr int pt_n = 8;
+  static constexpr int pt = (scal + 4 + 3) / 4 * 4;
+  static constexpr int size = (pt + pt_n * N * N + 31) / 32 * 32;
 };
 
 }  // namespace aq

@@ -31,6 +31,22 @@
 
 namespace aq {
 
+// Diagnostics build (-DAQ_PHASE_PROF): per-phase shader-clock cycles of k_walker_lap, summed over waves
+// into aq_phase_cycles[16 + k] (the proposal slots: no proposal runs inside a local-energy call; the
+// adjoint pass records into [0..9])
+#ifdef AQ_PHASE_PROF
+#define LPH(k)                                                                            \
+  do {                                                                                    \
+    const unsigned long long t_ = __builtin_readcyclecounter();                           \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&aq_phase_cycles[16 + (k)], t_ - t_ph);        \
+    t_ph = t_;                                                                            \
+  } while (0)
+#else
+#define LPH(k) \
+  do {         \
+  } while (0)
+#endif
+
 template <typename T, int N, int A>
 struct SmemLap {
   static constexpr int xs = 0;                               // [48] positions
@@ -108,16 +124,22 @@ constexpr bool kLapPrefetch = false;
 // One h-stream layer (nn.py:280-311) in first derivatives, column loop over electrons i.
 // ly: this layer's LapCache block (LDS); hb: dh/dx of every electron [N][49][NH], updated in place
 // (column `lane` = min(lane, 48), see SmemLap).
-// The pair tanh's of one column: t_{j+1}[o] of pair (le, i) for j < L from the LapCache (16-byte loads)
-template <typename T, int L>
+// One column's record of the lane's pair (le, i): layers 1, 2 take the double layers' tanh outputs t1, t2
+// (LapCache pt, 16-byte chunks 0 .. NCH - 1); layer 0 (NCH = 0) the e-e Jastrow parameters cusp, alpha of
+// the pair from the parameter block
+template <typename T, int N, int A, int NCH>
 struct PairT {
-  T t[L > 0 ? L : 1][4];
-  __device__ __forceinline__ void load(cptr<T> src) {
-    if constexpr (L > 0 && sizeof(T) == 4) {
+  T t[NCH > 0 ? NCH : 1][4];
+  __device__ __forceinline__ void load(cptr<T> src, cptr<T> P, int le, int i) {
+    if constexpr (NCH == 0) {
+      using Ly = Lay<N, A>;
+      t[0][0] = P[Ly::jee_c + le * N + i];
+      t[0][1] = P[Ly::jee_a + le * N + i];
+    } else if constexpr (sizeof(T) == 4) {
       typedef float f4 __attribute__((ext_vector_type(4)));
       const __attribute__((address_space(4))) f4* s = (const __attribute__((address_space(4))) f4*)src;
 #pragma unroll
-      for (int j = 0; j < L; ++j) {
+      for (int j = 0; j < NCH; ++j) {
         const f4 v = s[j];
         t[j][0] = v.x;
         t[j][1] = v.y;
@@ -126,7 +148,7 @@ struct PairT {
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < L; ++j)
+      for (int j = 0; j < NCH; ++j)
 #pragma unroll
         for (int o = 0; o < 4; ++o) t[j][o] = src[j * 4 + o];
     }
@@ -174,28 +196,22 @@ __device__ __forceinline__ void lap_layer(cptr<T> P, const T* xs, T* hb, const T
   }
 
   // multi-wave mode: wave wv of the walker's workgroup takes columns i = wv, wv + W, ...
-  // Unrolled by two (round 4, N2 4096 walkers, local-energy pair 195.9-196.6 -> 193.5-193.9 us at
-  // the same 191 VGPRs; by four, or E4's (r, s) loop by two / four as well: no further gain,
+  // Two columns per iteration (round 4, N2 4096 walkers, local-energy pair 195.9-196.6 -> 193.5-193.9 us
+  // at the same 191 VGPRs; by four, or E4's (r, s) loop by two / four as well: no further gain,
   // profiles/r04_s9_ab_lap_unroll.txt)
-#ifndef AQ_LAP_COL_UNROLL
-#define AQ_LAP_COL_UNROLL 2
-#endif
-  // the pair tanh's of the lane's pairs (le, i) (LapCache pt, written by the adjoint pass), loaded two
-  // columns ahead: lap_layer carries only the derivative chain through the double layers
-  PairT<T, L> tn1, tn2;
-  if constexpr (L > 0) {
-    tn1.load(Lpt + wv * 8);
-    tn2.load(Lpt + (wv + W < N ? wv + W : wv) * 8);
-  }
-#pragma unroll AQ_LAP_COL_UNROLL
-  for (int i = wv; i < N; i += W) {
+  // the lane's pair records (le, i): layers 1, 2 the double layers' tanh outputs (LapCache pt, written by
+  // the adjoint pass: the column loop carries only the derivative chain), layer 0 the e-e Jastrow
+  // parameters.  Two columns per iteration, the next iteration's records loaded at its top (a whole
+  // iteration of arithmetic in flight before they are used)
+  using Rec = PairT<T, N, A, L>;
+  constexpr int PS = LC::pt_n;
+  auto column = [&](int i, const Rec& tcur) {
     const bool diag = (le == i);
-    PairT<T, L> tcur;
-    if constexpr (L > 0) {
-      tcur = tn1;
-      tn1 = tn2;
-      tn2.load(Lpt + (i + 2 * W < N ? i + 2 * W : i) * 8);
-    }
+    // single-node weights of column i first: read before this column's dh/dx stores (LDS, in order)
+    const T* sn = ly + LC::sn + i * NH * 2;
+    T snv[2 * NH];
+#pragma unroll
+    for (int f = 0; f < 2 * NH; ++f) snv[f] = sn[f];
     T d[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) d[c] = xs[i * 3 + c] - xs[le * 3 + c];
@@ -205,8 +221,7 @@ __device__ __forceinline__ void lap_layer(cptr<T> P, const T* xs, T* hb, const T
     const T r1 = -dl * ir;   // dr/dx_{le,lc}, with d = x_i - x_le
     if constexpr (L == 0) {
       // Pade e-e Jastrow term cusp r / (1 + alpha r) of pair (le, i) (Jastrow.py:51-52)
-      const T cusp = P[Ly::jee_c + le * N + i];
-      const T al = P[Ly::jee_a + le * N + i];
+      const T cusp = tcur.t[0][0], al = tcur.t[0][1];
       const T iden = f_rcp(al * r + T(1));
       const T j1 = cusp * iden * iden;          // J'(r)
       const T j2 = T(-2) * al * j1 * iden;      // J''(r)
@@ -277,16 +292,34 @@ __device__ __forceinline__ void lap_layer(cptr<T> P, const T* xs, T* hb, const T
       acc += cn[2 * q + 1] * z * z;
     }
     // single linear + tanh + residual (nn.py:296-300)
-    const T* sn = ly + LC::sn + i * NH * 2;
 #pragma unroll
     for (int f = 0; f < NH; ++f) {
       T z = T(0);
 #pragma unroll
       for (int q = 0; q < Q; ++q) z += sngw[q * NH + f] * cq[q];
-      const T s1 = sn[2 * f] * z;
-      acc += sn[2 * f + 1] * z * z;
+      const T s1 = snv[2 * f] * z;
+      acc += snv[2 * f + 1] * z * z;
       hb[(i * 49 + lane) * NH + f] = (DIN == NH) ? (hi[f] + s1) * RSQ2 : s1;
     }
+  };
+  const cptr<T> Lrow = Lpt;   // record (le, i) at Lrow + i * PS
+  Rec c0, c1;
+  const int i1 = wv + W < N ? wv + W : wv;
+  c0.load(Lrow + wv * PS, P, le, wv);
+  c1.load(Lrow + i1 * PS, P, le, i1);
+#pragma unroll 1
+  for (int i = wv; i < N; i += 2 * W) {
+    Rec n0, n1;
+    const int i2 = i + 2 * W < N ? i + 2 * W : i, i3 = i + 3 * W < N ? i + 3 * W : i;
+    n0.load(Lrow + i2 * PS, P, le, i2);
+    n1.load(Lrow + i3 * PS, P, le, i3);
+    // fenced, so that the loads stay at the top and the copies into c0, c1 (which wait for them) at the end
+    __builtin_amdgcn_sched_barrier(0);
+    column(i, c0);
+    if (i + W < N) column(i + W, c1);
+    __builtin_amdgcn_sched_barrier(0);
+    c0 = n0;
+    c1 = n1;
   }
 }
 
@@ -411,7 +444,10 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LA
   const int l49 = lane < 48 ? lane : 48;
   T* yd = sm + SM::yd;
   const cptr<T> Lc = param_ptr<T>((const T*)ka.lapcache + (size_t)conf * LC::size);
-  const cptr<T> Lpt = Lc + LC::pt + le * N * 8;   // pair tanh's of the lane's row le
+  const cptr<T> Lpt = Lc + LC::pt + le * N * LC::pt_n;   // pair records of the lane's row le
+#ifdef AQ_PHASE_PROF
+  unsigned long long t_ph = __builtin_readcyclecounter();
+#endif
 
   if (w0 && lane < 3 * N) xs[lane] = ((const T*)ka.pos)[(size_t)conf * 3 * N + lane];
   T h0b[D0];
@@ -441,6 +477,7 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LA
       yd[(N + col) * 49 + l49] = yt.d2;
     }
   }
+  LPH(0);
   T jd1 = (!PH && w0 && dir) ? eo.jae.d1 : T(0);
   T jd2 = (!PH && w0 && dir) ? eo.jae.d2 : T(0);
 
@@ -448,9 +485,11 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LA
   // kLapPrefetch: each staged block's loads are issued one phase ahead (into spare VGPRs: the kernel
   // runs at 2 waves/SIMD, 256 VGPRs each) and written to LDS after the barrier that frees it, so
   // no wave waits a whole L2/HBM round trip at a stage boundary
+  LPH(1);
   StageRegs<T, LC::layer_n> lnext;
   if constexpr (kLapPrefetch) lnext.load(Lc + LC::layer_n);
   lap_layer<T, N, A, 0>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W, Lpt);
+  LPH(2);
   if constexpr (PH) {   // the e-e Jastrow terms and V_ee of layer 0's column loop: not part of theta
     jd1 = jd2 = vv = T(0);
   }
@@ -464,6 +503,7 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LA
   if constexpr (kLapPrefetch) lnext.store(ly);
   else stage_copy<T>(ly, Lc + 2 * LC::layer_n, LC::layer_n);
   __syncthreads();
+  LPH(3);
   StageRegs<T, 8 * N * N> qnext;
   StageRegs<T, (SM::stage_b ? 2 * N * N : 4)> bnext;
   if constexpr (kLapPrefetch) {
@@ -473,6 +513,7 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LA
   lap_layer<T, N, A, 2>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W, Lpt);
   if (W > 1) __syncthreads();   // the determinant terms read every wave's columns of dh/dx
 
+  LPH(4);
   // ------------------------------------------------------------------ determinant terms
   // (phases fenced so that the scheduler does not stretch their live ranges across each other)
   const int* rowsrc = ka.rowsrc;
@@ -508,6 +549,7 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LA
   __syncthreads();
   Qs = sm + SM::qs;
   if constexpr (SM::stage_b) Bu = sm + SM::bs;
+  LPH(5);
   // E2: w = Phi[e,:] * dYt[e,:], w.b_e, and t2 = Re sum_col (2 dPhi[e,col] Yt'[col] +
   //     Phi[e,col] Yt''[col]) B[col,e] with e = le (U of row e)
   const int spe = le < nup ? 0 : 1;
@@ -543,12 +585,14 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LA
     t2 += PH ? xr * bi + xi * br : xr * br - xi * bi;
   }
   __builtin_amdgcn_sched_barrier(0);
+  LPH(6);
   // E3: gradient: sum_{r,f} U Re Q_f[r,r] + Re(w . b_e) + Jastrow  (rows r = wv, wv + W, ...)
   T g = w0 ? jd1 + (PH ? wbi : wbr) : jd1;
 #pragma unroll 2
   for (int r = wv; r < N; r += W)
 #pragma unroll
     for (int f = 0; f < NH; ++f) g += UH(r, f) * Qs[((r * N + r) * NH + f) * 2 + (PH ? 1 : 0)];
+  LPH(7);
   // E4: cross = Re sum_r z_r S_re (z = B^T w);  ss = Re sum_{r,s} S_rs S_sr,  S_rs = sum_f U_rf Q_f[r,s]
   // (row r costs N - r: wave wv takes rows wv, 2W-1-wv, 2W+wv, ... so the shares balance)
   T cross = T(0), ss = T(0);
@@ -614,6 +658,7 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LA
   }
 #endif
 #undef UH
+  LPH(8);
   // (w.b_e)^2: its real part, or (PH) its imaginary part 2 Re Im
   const T wb2 = PH ? T(2) * wbr * wbi : wbr * wbr - wbi * wbi;
   T lap = (w0 ? t2 : T(0)) - (ss + T(2) * cross + (w0 ? wb2 : T(0))) + jd2 + acc;
@@ -636,6 +681,7 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LA
     }
   }
 
+  LPH(9);
   // ------------------------------------------------------------------ outputs
   const T gd = dir ? g : T(0);
   if constexpr (PH) {

@@ -976,7 +976,7 @@ k_walker_rev(KArgs ka) {
               for (int o = 0; o < 4; ++o) tp[o] = q[o];
             }
             if (PREP && icol) {   // LapCache: the same for k_walker_lap, the diagonal's finite values included
-              T* tp = Lw + LCc::pt + (k * N + ii) * 8 + j * 4;
+              T* tp = Lw + LCc::pt + (k * N + ii) * LCc::pt_n + j * 4;
 #pragma unroll
               for (int o = 0; o < 4; ++o) tp[o] = q[o];
             }
@@ -1867,10 +1867,10 @@ k_walker_rev(KArgs ka) {
         // the pair's double-layer tanh's: written by this lane in F2 (LapCache pt, same (k, i) per lane),
         // read back one pair ahead instead of re-running the value chain in each pass
         const int kfirst = k0 + ((kq - k0) & 3);
-        const T* tpb = Lw + LCc::pt + ii * 8;
+        const T* tpb = Lw + LCc::pt + ii * LCc::pt_n;
         T tq[8];
 #pragma unroll
-        for (int o = 0; o < 8; ++o) tq[o] = tpb[(kfirst < k1 ? kfirst : k0) * N * 8 + o];
+        for (int o = 0; o < 8; ++o) tq[o] = tpb[(kfirst < k1 ? kfirst : k0) * N * LCc::pt_n + o];
 #pragma unroll 1
         for (int k = kfirst; k < k1; k += 4) {
           const bool dg = (k == ii);
@@ -1879,7 +1879,7 @@ k_walker_rev(KArgs ka) {
 #pragma unroll
           for (int o = 0; o < 8; ++o) tcur[o] = tq[o];
 #pragma unroll
-          for (int o = 0; o < 8; ++o) tq[o] = tpb[(k + 4 < k1 ? k + 4 : k) * N * 8 + o];
+          for (int o = 0; o < 8; ++o) tq[o] = tpb[(k + 4 < k1 ? k + 4 : k) * N * LCc::pt_n + o];
           T d[3];
 #pragma unroll
           for (int c = 0; c < 3; ++c) d[c] = xs[ii * 3 + c] - xs[k * 3 + c];
