@@ -937,8 +937,26 @@ k_walker_rev(KArgs ka) {
         for (int G = 0; G < 2; ++G)
   #pragma unroll
           for (int f = 0; f < 4; ++f) acc[l][G][f] = T(0);
+      // the e-e Jastrow parameters of the lane's pairs, all issued before the first pair (loaded in the
+      // pair loop's k < i branch, each was a global round trip waited for on its own)
+      constexpr int NT = (N + 3) / 4;
+      T jcp[NT], jap[NT];
   #pragma unroll
-      for (int t = 0; t < (N + 3) / 4; ++t) {
+      for (int t = 0; t < NT; ++t) {
+        const int kk = kq + 4 * t < N ? kq + 4 * t : N - 1;
+        jcp[t] = P[Ly::jee_c + kk * N + ii];
+        jap[t] = P[Ly::jee_a + kk * N + ii];
+      }
+      // the two double layers' weights, loaded once (uniform 16-byte vector loads; as scalar loads they
+      // were re-issued and waited for per pair)
+      T dwv[2][16], dbv[2][4];
+  #pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        ld_vec<T, 16>(P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1), dwv[j]);
+        ld_vec<T, 4>(P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1), dbv[j]);
+      }
+  #pragma unroll
+      for (int t = 0; t < NT; ++t) {
         const int k = kq + 4 * t;
         if (k < N) {
           const bool diag = (k == ii);
@@ -949,7 +967,7 @@ k_walker_rev(KArgs ka) {
           const T r = f_sqrt(diag ? T(1) : r2);
           T p[4] = {diag ? T(0) : r, diag ? T(0) : d[0], diag ? T(0) : d[1], diag ? T(0) : d[2]};
           if (icol && k < ii) {
-            const T cusp = P[Ly::jee_c + k * N + ii], al = P[Ly::jee_a + k * N + ii];
+            const T cusp = jcp[t], al = jap[t];
             jve += f_div(cusp * r, al * r + T(1));
           }
           const bool G1 = k >= nup;
@@ -960,14 +978,12 @@ k_walker_rev(KArgs ka) {
           }
   #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            const cptr<T> dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
-            const cptr<T> db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
             T q[4];
   #pragma unroll
             for (int o = 0; o < 4; ++o) {
-              T s = db[o];
+              T s = dbv[j][o];
   #pragma unroll
-              for (int m = 0; m < 4; ++m) s += p[m] * dw[m * 4 + o];
+              for (int m = 0; m < 4; ++m) s += p[m] * dwv[j][m * 4 + o];
               q[o] = f_tanh(s);
             }
             if (!PREP && !isprop && icol && !diag) {   // walker cache: t_{j+1} of pair (k, i)
