@@ -202,6 +202,40 @@ template <int M, typename T> __device__ __forceinline__ T quad_bcast(T x) {
   return dpp<M | (M << 2) | (M << 4) | (M << 6)>(x);
 }
 
+// The first NU of an NV-element lane record (16-byte aligned) in loads of exactly those elements
+// (16-, 8- and 4-byte; the rest set to zero): a 16-byte load whose unused elements' registers are
+// reallocated must complete before they are overwritten, which placed a vmcnt(0) right behind the
+// F4 weight prefetch
+template <typename T, int NV, int NU>
+__device__ __forceinline__ void ld_use(cptr<T> p, T* out) {
+  static_assert(NU <= NV, "record");
+  if constexpr (sizeof(T) == 4) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const __attribute__((address_space(4))) f4* q = (const __attribute__((address_space(4))) f4*)p;
+#pragma unroll
+    for (int j = 0; j < NU / 4; ++j) {
+      const f4 v = q[j];
+      out[4 * j] = v.x;
+      out[4 * j + 1] = v.y;
+      out[4 * j + 2] = v.z;
+      out[4 * j + 3] = v.w;
+    }
+    constexpr int B = NU / 4 * 4, R = NU % 4;
+    if constexpr (R >= 2) {
+      const f2 v = *(const __attribute__((address_space(4))) f2*)(p + B);
+      out[B] = v.x;
+      out[B + 1] = v.y;
+    }
+    if constexpr (R == 1 || R == 3) out[B + R - 1] = p[B + R - 1];
+#pragma unroll
+    for (int k = NU; k < NV; ++k) out[k] = T(0);
+  } else {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) out[k] = k < NU ? p[k] : T(0);
+  }
+}
+
 // NV (a multiple of 16 bytes' worth) consecutive parameters from a 16-byte aligned offset of the
 // parameter buffer, in 16-byte loads (layout.h lane-order blocks)
 template <typename T, int NV>
@@ -1114,9 +1148,15 @@ k_walker_rev(KArgs ka) {
     if constexpr (xlane) {
       // the lane's records of the lane-order blocks: 2 + 2 + 1 sixteen-byte loads
       T cw8[Ly::XQ], sw8[Ly::XQ], cb4[Ly::XB];
-      ld_vec<T, Ly::XQ>(P + Ly::xcw(l) + (ic * 4 + ff) * Ly::XQ, cw8);
-      ld_vec<T, Ly::XQ>(P + Ly::xsw(l) + ff * Ly::XQ, sw8);
-      ld_vec<T, Ly::XB>(P + Ly::xcb(l) + (ic * 4 + ff) * Ly::XB, cb4);
+      if (l == 0) {
+        ld_use<T, Ly::XQ, Ly::Q0>(P + Ly::xcw(l) + (ic * 4 + ff) * Ly::XQ, cw8);
+        ld_use<T, Ly::XQ, Ly::Q0>(P + Ly::xsw(l) + ff * Ly::XQ, sw8);
+        ld_use<T, Ly::XB, Ly::CBN(Ly::Q0)>(P + Ly::xcb(l) + (ic * 4 + ff) * Ly::XB, cb4);
+      } else {
+        ld_use<T, Ly::XQ, Ly::Q1>(P + Ly::xcw(l) + (ic * 4 + ff) * Ly::XQ, cw8);
+        ld_use<T, Ly::XQ, Ly::Q1>(P + Ly::xsw(l) + ff * Ly::XQ, sw8);
+        ld_use<T, Ly::XB, Ly::CBN(Ly::Q1)>(P + Ly::xcb(l) + (ic * 4 + ff) * Ly::XB, cb4);
+      }
 #pragma unroll
       for (int q = 0; q < SM::QM; ++q)
         if (q < Q) {
@@ -1768,7 +1808,10 @@ k_walker_rev(KArgs ka) {
       const int QF = Q / 4;
       T cg[SM::QM];
       T bcw8[Ly::XQ];   // kXLane: this lane's conv weights (electron ic, unit ff), 2 sixteen-byte loads
-      if constexpr (xlane) ld_vec<T, Ly::XQ>(P + Ly::xcw(l) + (ic * 4 + ff) * Ly::XQ, bcw8);
+      if constexpr (xlane) {
+        if (l == 0) ld_use<T, Ly::XQ, Ly::Q0>(P + Ly::xcw(l) + (ic * 4 + ff) * Ly::XQ, bcw8);
+        else ld_use<T, Ly::XQ, Ly::Q1>(P + Ly::xcw(l) + (ic * 4 + ff) * Ly::XQ, bcw8);
+      }
 #pragma unroll
       for (int q = 0; q < SM::QM; ++q) {
         const bool full = q < 4 * QF;
