@@ -445,6 +445,8 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LA
   T* yd = sm + SM::yd;
   const cptr<T> Lc = param_ptr<T>((const T*)ka.lapcache + (size_t)conf * LC::size);
   const cptr<T> Lpt = Lc + LC::pt + le * N * LC::pt_n;   // pair records of the lane's row le
+  const int rsl = ka.rowsrc[lane < N ? lane : N - 1];      // determinant row lane's electron (E3, E4)
+  const int rsle = ka.rowsrc[le];                          // and row le's (E2)
 #ifdef AQ_PHASE_PROF
   unsigned long long t_ph = __builtin_readcyclecounter();
 #endif
@@ -520,7 +522,10 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LA
   const T* Qs = nullptr;                     // LDS copy, set after E1
   const T* Bu = (const T*)(Lc + LC::bm);     // LDS copy after E1 where it fits
   const cptr<T> Ph = Lc + LC::ph;
-#define UH(r, f) hb[(rowsrc[r] * 49 + l49) * NH + (f)]
+  // row r's electron rowsrc[r] by a lane read of rsl (lane r holds it, loaded at kernel start): read
+  // through the pointer, every (r, s) step of E3/E4 was a dependent global load (the kernel also writes
+  // global memory, so it cannot be a scalar load) waited for before its LDS address was known
+#define UH(r, f) hb[(__builtin_amdgcn_readlane(rsl, (r)) * 49 + l49) * NH + (f)]
   // E1: Yt row jets of electron le (stored after the per-electron stage)
   T Yd1[N], Yd2[N];
 #pragma unroll
@@ -555,7 +560,7 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LA
   const int spe = le < nup ? 0 : 1;
   T Ue[NH];
 #pragma unroll
-  for (int f = 0; f < NH; ++f) Ue[f] = UH(le, f);
+  for (int f = 0; f < NH; ++f) Ue[f] = hb[(rsle * 49 + l49) * NH + f];   // U of row le (per lane)
   T wr[N], wi[N];
   T wbr = T(0), wbi = T(0), t2 = T(0);
 #pragma unroll
