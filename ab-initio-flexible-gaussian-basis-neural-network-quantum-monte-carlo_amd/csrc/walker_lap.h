@@ -589,6 +589,14 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LA
     const T xi = T(2) * dpi * Yd1[col] + pm * Yd2[col];
     t2 += PH ? xr * bi + xi * br : xr * br - xi * bi;
   }
+  // t2 is consumed only at the end of the kernel: left alone, the compiler sinks E2's dPhi arithmetic
+  // past E4 while its weight loads stay here, and spills the weights (a scalar load, wait and lane
+  // write per weight pair; 193 VGPRs, 159 SGPRs spilled).  Pinned here: 154 VGPRs, 19 spilled SGPRs.
+  // Measured (profiles/r06_s9_ab_lap_e2pin.txt, N2): the multi-wave instantiation (2 or 4 waves per
+  // walker, small batches) gains -4 to -5 % (E_L pair 56.5 -> 53.6 us at 512 walkers, 76.6 -> 73.6
+  // at 1,024); the one-wave instantiation at 4,096 walkers loses +4.5 % (171 -> 179 us: the weight
+  // loads' latency then sits on E2's path instead of overlapping E3 / E4), so it is left alone there
+  if constexpr (WMAX > 1) asm volatile("" : "+v"(t2));
   __builtin_amdgcn_sched_barrier(0);
   LPH(6);
   // E3: gradient: sum_{r,f} U Re Q_f[r,r] + Re(w . b_e) + Jastrow  (rows r = wv, wv + W, ...)
