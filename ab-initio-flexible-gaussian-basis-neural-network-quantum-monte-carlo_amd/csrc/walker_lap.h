@@ -512,6 +512,13 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LA
     qnext.load(Lc + LC::qs);
     if constexpr (SM::stage_b) bnext.load(Lc + LC::bm);
   }
+  // E2's Phi row of electron le, issued a layer ahead (per-lane 16-byte loads of 2N contiguous values)
+  T phrow[2 * N];
+  if constexpr (2 * N % 4 == 0) ld_vec<T, 2 * N>(Lc + LC::ph + le * N * 2, phrow);
+  else {
+#pragma unroll
+    for (int k = 0; k < 2 * N; ++k) phrow[k] = Lc[LC::ph + le * N * 2 + k];
+  }
   lap_layer<T, N, A, 2>(P, xs, hb, ly, eo.hf, l49, lc, er, le, val, dir, live, nup, jd1, jd2, vv, acc, wv, W, Lpt);
   if (W > 1) __syncthreads();   // the determinant terms read every wave's columns of dh/dx
 
@@ -565,7 +572,7 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LA
   T wbr = T(0), wbi = T(0), t2 = T(0);
 #pragma unroll
   for (int col = 0; col < N; ++col) {
-    const T pr = Ph[(le * N + col) * 2], pm = Ph[(le * N + col) * 2 + 1];
+    const T pr = phrow[2 * col], pm = phrow[2 * col + 1];
     const T br = Bu[(col * N + le) * 2], bi = Bu[(col * N + le) * 2 + 1];
     wr[col] = pr * Yd1[col];
     wi[col] = pm * Yd1[col];
@@ -591,12 +598,13 @@ __global__ __launch_bounds__(64 * WMAX) __attribute__((amdgpu_waves_per_eu(AQ_LA
   }
   // t2 is consumed only at the end of the kernel: left alone, the compiler sinks E2's dPhi arithmetic
   // past E4 while its weight loads stay here, and spills the weights (a scalar load, wait and lane
-  // write per weight pair; 193 VGPRs, 159 SGPRs spilled).  Pinned here: 154 VGPRs, 19 spilled SGPRs.
-  // Measured (profiles/r06_s9_ab_lap_e2pin.txt, N2): the multi-wave instantiation (2 or 4 waves per
-  // walker, small batches) gains -4 to -5 % (E_L pair 56.5 -> 53.6 us at 512 walkers, 76.6 -> 73.6
-  // at 1,024); the one-wave instantiation at 4,096 walkers loses +4.5 % (171 -> 179 us: the weight
-  // loads' latency then sits on E2's path instead of overlapping E3 / E4), so it is left alone there
-  if constexpr (WMAX > 1) asm volatile("" : "+v"(t2));
+  // write per weight pair; 193 VGPRs, 159 SGPRs spilled).  Pinned here (with the Phi row prefetched a
+  // layer ahead, above): 187 VGPRs, 34 spilled SGPRs.  Measured (N2, interleaved): pinned alone, the
+  // multi-wave instantiation gains 4-5 % and the one-wave one loses 4.5 % (E2's Phi loads then sit on
+  // its path; profiles/r06_s9_ab_lap_e2pin.txt); pinned with the Phi row prefetch, the one-wave
+  // instantiation gains 2 % (E_L pair 169.8-171.0 -> 166.6-167.3 us at 4,096 walkers, fp64 bitwise,
+  // profiles/r06_s9_ab_lap_e2ph.txt)
+  asm volatile("" : "+v"(t2));
   __builtin_amdgcn_sched_barrier(0);
   LPH(6);
   // E3: gradient: sum_{r,f} U Re Q_f[r,r] + Re(w . b_e) + Jastrow  (rows r = wv, wv + W, ...)
