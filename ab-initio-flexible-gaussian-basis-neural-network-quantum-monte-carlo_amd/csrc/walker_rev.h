@@ -981,13 +981,18 @@ k_walker_rev(KArgs ka) {
         jcp[t] = P[Ly::jee_c + kk * N + ii];
         jap[t] = P[Ly::jee_a + kk * N + ii];
       }
-      // the two double layers' weights, loaded once (uniform 16-byte vector loads; as scalar loads they
-      // were re-issued and waited for per pair)
+      // the two double layers' weights, loaded once before the pair loop (element loads: their offsets
+      // are not 16-byte aligned for every shape; the compiler merges them into wide scalar loads).  Read
+      // inside the loop they were re-issued and waited for per pair
       T dwv[2][16], dbv[2][4];
   #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        ld_vec<T, 16>(P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1), dwv[j]);
-        ld_vec<T, 4>(P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1), dbv[j]);
+        const cptr<T> dw = P + (j == 0 ? Ly::dbl_w0 : Ly::dbl_w1);
+        const cptr<T> db = P + (j == 0 ? Ly::dbl_b0 : Ly::dbl_b1);
+  #pragma unroll
+        for (int k = 0; k < 16; ++k) dwv[j][k] = dw[k];
+  #pragma unroll
+        for (int k = 0; k < 4; ++k) dbv[j][k] = db[k];
       }
   #pragma unroll
       for (int t = 0; t < NT; ++t) {
