@@ -132,6 +132,12 @@ struct LapCache {
   static constexpr int pt_n = 8;
   static constexpr int pt = (scal + 4 + 3) / 4 * 4;
   static constexpr int size = (pt + pt_n * N * N + 31) / 32 * 32;
+  // 16-byte loads of k_walker_lap rely on these: the pair records (PairT), the Phi row of an even-N
+  // electron (ld_vec of 2N values; odd N loads it element-wise) and the staged blocks, from a 128-byte
+  // aligned walker record
+  static_assert(pt % 4 == 0 && pt_n % 4 == 0 && (N % 2 == 1 || ph % 4 == 0) && qs % 4 == 0 && bm % 4 == 0 &&
+                    size % 32 == 0,
+                "LapCache blocks must stay 16-byte aligned");
 };
 
 }  // namespace aq
